@@ -1,0 +1,251 @@
+"""Benchmark: published topics matched per second on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2]): 10M wildcard filters of the IoT tree
+``site/+/device/+/#`` family, every GPU matching batches of ``site/{s}/device/{d}/{m}/{k}``
+topics.  One step = one full match pass over one batch already resident in HBM: tokenise +
+hash, exact route-key probe, trie walk, CSR build, byte verification of every pair.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--cfg 3] [--shard topics|filters]
+
+N>1 is launched by the driver with torch.distributed.run (one rank per GPU).  ``--shard topics``
+(default) = every GPU holds the whole 10M-filter index and matches its own batch (weak scaling,
+no collective on the data path); ``--shard filters`` = the north-star layout (filters split by
+hash, batch broadcast + results gathered with RCCL every step).
+
+Rank 0 prints one JSON line.  ``roofline`` is for the dominant kernel (k_walk): algorithmic
+bytes per launch (DESIGN.md "Roofline") over its HIP-event-measured average duration.
+``cpu_baseline`` is the C++ restatement of the reference's emqx_trie match (oracle/ref_trie.cpp)
+timed on this host's cores on a bounded sample of the same topics (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--cfg", type=int, default=3)
+    ap.add_argument("--filters", type=int, default=None)
+    ap.add_argument("--topics", type=int, default=None, help="topics per GPU batch")
+    ap.add_argument("--shard", choices=["topics", "filters"], default="topics")
+    ap.add_argument("--wg-per-cu", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import workloads
+    from emqx_amd import Engine
+    from emqx_amd import dist as D
+
+    nf_default, nt_default, sf, st = workloads.DEFAULTS[args.cfg]
+    nf = args.filters or nf_default
+    nt = args.topics or nt_default
+
+    t0 = time.time()
+    seed_t = st + (1000 * rank if args.shard == "topics" else 0)
+    w = workloads.generate(args.cfg, nf, nt, sf, seed_t)
+    log(f"[rank {rank}] generated {w.nf} filters, {w.nt} topics in {time.time() - t0:.1f}s")
+
+    # ---- index ----
+    t0 = time.time()
+    eng = Engine(device=local, walk_wg_per_cu=args.wg_per_cu)
+    if args.shard == "filters" and world > 1:
+        mine = np.nonzero(D.filter_shards(w.fbytes, w.foff, world) == rank)[0]
+    else:
+        mine = np.arange(w.nf)
+    fb, fo = _subset(w, mine)
+    wild = w.fwild[mine].astype(bool)
+    eng.route_ref_many(fb, fo)
+    wb, wo = _subset_packed(fb, fo, np.nonzero(wild)[0])
+    eng.trie_insert_many(wb, wo)
+    eng.commit()
+    est = eng.stats()
+    log(f"[rank {rank}] index: {est['n_trie_filters']} trie filters, {est['n_route_keys']} route "
+        f"keys, {est['n_nodes']} nodes, {est['device_bytes'] / 2**20:.0f} MiB in "
+        f"{time.time() - t0:.1f}s")
+
+    tb = torch.from_numpy(w.tbytes).to(dev)
+    to = torch.from_numpy(w.toff.view(np.int32)).to(dev)
+    nbytes = int(w.toff[-1])
+    torch.cuda.synchronize()
+
+    # ---- one diagnostic census pass (outside the timed region): S(t), slot loads, pairs ----
+    census = eng.walk_census(tb.data_ptr(), to.data_ptr(), w.nt, nbytes)
+
+    def step():
+        if args.shard == "filters" and world > 1:
+            b, o = D.broadcast_batch(tb if rank == 0 else None, to if rank == 0 else None, dev)
+            r = eng.match_device(b.data_ptr(), o.data_ptr(), o.numel() - 1, b.numel())
+            row, fid, ex = D.device_result_to_torch(eng, r, dev)
+            gid_map = mine_t[fid] if fid.numel() else fid
+            exg = torch.where(ex == D.NONE, ex, mine_t[torch.clamp(ex, max=len(mine) - 1)])
+            return D.gather_merge(row, gid_map, exg)
+        return eng.match_device(tb.data_ptr(), to.data_ptr(), w.nt, nbytes)
+
+    mine_t = torch.from_numpy(mine.astype(np.int64)).to(dev)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    s0 = eng.stats()
+    eng.set_profiling(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    eng.set_profiling(False)
+    s1 = eng.stats()
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    launches = s1["walk_launches"] - s0["walk_launches"]
+    walk_ms = (s1["walk_ms"] - s0["walk_ms"]) / max(1, launches)
+    pipe_ms = (s1["total_ms"] - s0["total_ms"]) / max(1, args.steps)
+    # algorithmic bytes of one k_walk launch (DESIGN.md "Roofline"): per topic a 16-B record,
+    # the next-level token hashes (4 B per level), 3 x 16-B edge probes per matched trie state
+    # (SURVEY 8d's 48*S(t)), and a 12-B staged (topic, filter, rank) triple per match; plus 4 B
+    # of per-topic count.
+    walk_bytes = (16 + 4) * w.nt + 4 * census["words"] + 48 * census["states"] + 12 * census["pairs"]
+    achieved = walk_bytes / (walk_ms * 1e-3) / 1e9 if walk_ms > 0 else 0.0
+    topics_total = (w.nt * world) if args.shard == "topics" else w.nt
+    value = topics_total / (elapsed / args.steps)
+
+    traffic = _pmc_traffic(args.cfg, w.nt)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = _cpu_baseline(w, args)
+
+    if rank == 0:
+        line = {
+            "metric": "published topics matched/sec at 10M filters",
+            "value": round(value, 1),
+            "unit": "topics/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak" if args.shard == "topics" else "strong",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {
+                "workload": f"cfg{args.cfg}: {w.nf} filters "
+                            + ("(IoT site/+/device/+/# tree)" if args.cfg == 3 else ""),
+                "filters": int(w.nf), "topics_per_gpu_batch": int(w.nt),
+                "global_batch": int(topics_total), "parallelism":
+                    (f"topic-replica x{world}" if args.shard == "topics" else f"filter-shard x{world}"),
+                "pairs_per_batch": int(census["pairs"]),
+                "trie_states_per_batch": int(census["states"]),
+                "edge_slot_loads_per_batch": int(census["slot_loads"]),
+                "pipeline_ms_per_batch": round(pipe_ms, 4),
+            },
+            "roofline": {
+                "kernel": "k_walk",
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "walk_ms_per_launch": round(walk_ms, 4),
+                "algorithmic_bytes_per_launch": int(walk_bytes),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _subset(w, idx):
+    return _subset_packed(w.fbytes, w.foff, idx)
+
+
+def _subset_packed(fbytes, foff, idx):
+    idx = np.asarray(idx, dtype=np.int64)
+    if len(idx) == len(foff) - 1 and (len(idx) == 0 or (idx[0] == 0 and idx[-1] == len(idx) - 1)):
+        return fbytes, foff
+    lens = (foff[idx + 1] - foff[idx]).astype(np.int64)
+    off = np.zeros(len(idx) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    starts = foff[idx].astype(np.int64)
+    pos = np.repeat(starts - np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64), lens) \
+        + np.arange(int(lens.sum()), dtype=np.int64)
+    return fbytes[pos], off
+
+
+def _pmc_traffic(cfg, nt):
+    """HBM bytes per k_walk launch from the committed rocprofv3 PMC summary, if present."""
+    p = os.path.join(ROOT, "profiles", f"pmc_walk_cfg{cfg}.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if int(d.get("topics", -1)) == nt:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def _cpu_baseline(w, args):
+    """The reference algorithm (C++ restatement of emqx_trie match_compact with an ordered-set
+    index, oracle/ref_trie.cpp) on this host's cores, over a bounded sample of the topics."""
+    from oracle.cref import RefIndex
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    t0 = time.time()
+    ref = RefIndex(True)
+    ref.add_many(w.fbytes, w.foff, 2 + w.fwild)
+    build_s = time.time() - t0
+    n = min(w.nt, 20000)
+    dt, _ = ref.time_match(w.tbytes, w.toff[: n + 1], threads)
+    rate = n / max(dt, 1e-9)
+    n2 = int(min(w.nt, max(n, rate * args.cpu_seconds)))
+    if n2 > n:
+        dt, _ = ref.time_match(w.tbytes, w.toff[: n2 + 1], threads)
+        n = n2
+    log(f"cpu baseline: index build {build_s:.1f}s, {n} topics in {dt:.2f}s on {threads} threads")
+    return {"value": round(n / dt, 1), "unit": "topics/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} topics of the same batch against the same {w.nf} filters "
+                      f"(emqx_trie match_compact restated in C++, std::map ordered set), "
+                      f"{dt:.1f}s wall"}
+
+
+if __name__ == "__main__":
+    main()

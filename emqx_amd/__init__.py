@@ -1,0 +1,13 @@
+"""emqx_amd -- MI355X-native batched MQTT topic matching behind the EMQX routing API.
+
+The product is ``libemqx_gpumatch.so`` (gfx950 HIP kernels + host index builder + C-ABI,
+``include/emqx_gpumatch.h``).  This package is the host-side mirror of the reference's
+``emqx_trie`` / ``emqx_router`` modules over that library:
+
+    from emqx_amd import Trie, Router, Engine
+"""
+from .engine import NONE, DeviceResult, Engine, EngineError, MatchResult  # noqa: F401
+from .router import Router  # noqa: F401
+from .trie import Trie  # noqa: F401
+
+__all__ = ["Engine", "EngineError", "MatchResult", "DeviceResult", "Trie", "Router", "NONE"]

@@ -1,0 +1,897 @@
+// gm_engine.cpp -- host side of the MI355X topic-match engine: filter registry, device index
+// builder (snapshot/commit), batch driver and the C-ABI declared in include/emqx_gpumatch.h.
+//
+// Reference semantics mirrored here:
+//   * trie membership is a SET of filters (emqx_trie:insert is idempotent, delete of an absent
+//     filter is a no-op: emqx_trie.erl:121-127, 139-144);
+//   * route keys are refcounted by dests (the emqx_route bag, emqx_router_utils.erl:31-71);
+//   * readers only ever see committed state (mria transactions), so every mutation lands in
+//     the pending registry and becomes visible atomically at emqxgm_commit.
+#include <errno.h>
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/emqx_gpumatch.h"
+#include "gm_common.h"
+#include "gm_kernels.h"
+
+using namespace gm;
+
+namespace {
+
+uint64_t pow2_at_least(uint64_t x) {
+  uint64_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+// Open-addressing map u64 -> u32 (keys never equal ~0).
+struct U64Map {
+  std::vector<uint64_t> keys;
+  std::vector<uint32_t> vals;
+  uint64_t mask = 0, used = 0;
+  void init(uint64_t expect) {
+    const uint64_t cap = pow2_at_least(std::max<uint64_t>(16, expect * 2));
+    keys.assign(cap, ~0ull);
+    vals.assign(cap, 0);
+    mask = cap - 1;
+    used = 0;
+  }
+  void grow() {
+    std::vector<uint64_t> ok;
+    std::vector<uint32_t> ov;
+    ok.swap(keys);
+    ov.swap(vals);
+    const uint64_t cap = (mask + 1) * 2;
+    keys.assign(cap, ~0ull);
+    vals.assign(cap, 0);
+    mask = cap - 1;
+    used = 0;
+    for (size_t i = 0; i < ok.size(); ++i)
+      if (ok[i] != ~0ull) put(ok[i], ov[i]);
+  }
+  // returns pointer to value; inserted=true if new
+  uint32_t* get_or_insert(uint64_t k, bool& inserted) {
+    if ((used + 1) * 2 > mask + 1) grow();
+    uint64_t i = fmix64(k) & mask;
+    for (;;) {
+      if (keys[i] == k) {
+        inserted = false;
+        return &vals[i];
+      }
+      if (keys[i] == ~0ull) {
+        keys[i] = k;
+        ++used;
+        inserted = true;
+        return &vals[i];
+      }
+      i = (i + 1) & mask;
+    }
+  }
+  void put(uint64_t k, uint32_t v) {
+    bool ins;
+    *get_or_insert(k, ins) = v;
+  }
+};
+
+struct Filter {
+  uint64_t off;
+  uint32_t len;
+  uint8_t in_trie;
+  uint8_t wild;
+  uint8_t trie_committed;
+  uint32_t route_refs;
+};
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+}  // namespace
+
+struct emqxgm {
+  std::mutex mu;
+  emqxgm_cfg cfg{};
+  hipStream_t stream = nullptr;
+  std::string err;
+
+  // ---- registry (pending state) ----
+  std::vector<uint8_t> pool;
+  std::vector<Filter> filters;
+  std::vector<uint32_t> slots;  // id+1, open addressing on string hash
+  uint64_t slot_mask = 0;
+  uint64_t n_trie_pending = 0, n_route_pending = 0;
+  bool dirty = false;
+
+  // ---- committed device index ----
+  uint64_t epoch = 0;
+  DevIndex ix;
+  std::vector<DevBuf> ix_bufs;
+  uint64_t pool_uploaded = 0;  // bytes of pool already on device
+  DevBuf d_pool, d_foff;
+  uint64_t foff_uploaded = 0;
+  emqxgm_stats st{};
+
+  // ---- batch scratch ----
+  Scratch sc;
+  std::vector<DevBuf> sc_bufs;
+  WalkGeom geom;
+  uint8_t* d_in_bytes = nullptr;
+  uint32_t* d_in_off = nullptr;
+  uint64_t in_bytes_cap = 0, in_off_cap = 0;
+
+  // ---- host outputs ----
+  std::vector<uint64_t> h_row;
+  std::vector<uint32_t> h_fid, h_exact, h_row32, h_fid_tmp;
+
+  bool profiling = false;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+};
+
+namespace {
+
+int fail(emqxgm* h, hipError_t e, const char* what) {
+  h->err = std::string(what) + ": " + hipGetErrorString(e);
+  return -EIO;
+}
+
+#define HIPCHK(h, expr)                          \
+  do {                                           \
+    hipError_t _e = (expr);                      \
+    if (_e != hipSuccess) return fail(h, _e, #expr); \
+  } while (0)
+
+uint64_t str_hash(const uint8_t* p, uint32_t len) {
+  uint64_t x = FNV_OFF;
+  for (uint32_t i = 0; i < len; ++i) x = fnv_step(x, p[i]);
+  return fmix64(x);
+}
+
+bool is_wild(const uint8_t* p, uint32_t len) {  // emqx_topic:wildcard/1
+  uint32_t s = 0;
+  for (uint32_t i = 0; i <= len; ++i) {
+    if (i == len || p[i] == '/') {
+      if (i - s == 1 && (p[s] == '+' || p[s] == '#')) return true;
+      s = i + 1;
+    }
+  }
+  return false;
+}
+
+void slots_grow(emqxgm* h) {
+  const uint64_t cap = std::max<uint64_t>(1024, (h->slot_mask + 1) * 2);
+  std::vector<uint32_t> ns(cap, 0);
+  for (uint32_t id = 0; id < h->filters.size(); ++id) {
+    const Filter& f = h->filters[id];
+    uint64_t i = str_hash(h->pool.data() + f.off, f.len) & (cap - 1);
+    while (ns[i]) i = (i + 1) & (cap - 1);
+    ns[i] = id + 1;
+  }
+  h->slots.swap(ns);
+  h->slot_mask = cap - 1;
+}
+
+// Find or (if create) register a filter string; returns id or NONE.
+uint32_t find_id(emqxgm* h, const uint8_t* p, uint32_t len, bool create) {
+  if (h->slots.empty()) {
+    if (!create) return NONE;
+    slots_grow(h);
+  }
+  if (create && (h->filters.size() + 1) * 2 > h->slot_mask + 1) slots_grow(h);
+  uint64_t i = str_hash(p, len) & h->slot_mask;
+  for (;;) {
+    const uint32_t v = h->slots[i];
+    if (v == 0) break;
+    const Filter& f = h->filters[v - 1];
+    if (f.len == len && memcmp(h->pool.data() + f.off, p, len) == 0) return v - 1;
+    i = (i + 1) & h->slot_mask;
+  }
+  if (!create) return NONE;
+  const uint32_t id = (uint32_t)h->filters.size();
+  Filter f;
+  f.off = h->pool.size();
+  f.len = len;
+  f.in_trie = 0;
+  f.trie_committed = 0;
+  f.wild = is_wild(p, len) ? 1 : 0;
+  f.route_refs = 0;
+  h->pool.insert(h->pool.end(), p, p + len);
+  h->filters.push_back(f);
+  h->slots[i] = id + 1;
+  return id;
+}
+
+template <class T>
+int dev_upload(emqxgm* h, std::vector<DevBuf>& keep, const std::vector<T>& v, const T** out) {
+  DevBuf b;
+  b.bytes = std::max<size_t>(sizeof(T), v.size() * sizeof(T));
+  HIPCHK(h, hipMalloc(&b.p, b.bytes));
+  keep.push_back(b);
+  if (!v.empty()) HIPCHK(h, hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  *out = (const T*)b.p;
+  return 0;
+}
+
+void free_bufs(std::vector<DevBuf>& v) {
+  for (auto& b : v)
+    if (b.p) (void)hipFree(b.p);
+  v.clear();
+}
+
+// Node-level filter list during the build: NONE, a single fid, or LIST_MULTI|index.
+struct ListBuild {
+  std::vector<std::vector<uint32_t>> lists;
+  void add(uint32_t& slot, uint32_t fid) {
+    if (slot == NONE) {
+      slot = fid;
+    } else if (slot & LIST_MULTI) {
+      lists[slot & ~LIST_MULTI].push_back(fid);
+    } else {
+      lists.push_back({slot, fid});
+      slot = LIST_MULTI | (uint32_t)(lists.size() - 1);
+    }
+  }
+};
+
+// Build the device index from the pending registry and swap it in.
+int commit_locked(emqxgm* h) {
+  const uint32_t wmask =
+      h->cfg.word_hash_bits >= 32 ? 0xFFFFFFFFu : ((1u << h->cfg.word_hash_bits) - 1u);
+  const uint64_t fmask =
+      h->cfg.full_hash_bits >= 64 ? ~0ull : ((1ull << h->cfg.full_hash_bits) - 1ull);
+
+  // ---- trie: nodes keyed by (parent, level-token hash); root = node 0 ----
+  std::vector<uint32_t> nflags(1, 0), nhf(1, NONE), ntw(1, NONE), ntn(1, NONE);
+  U64Map emap;
+  emap.init(std::max<uint64_t>(1024, h->n_trie_pending * 2));
+  ListBuild lb;
+  std::vector<std::pair<uint64_t, uint32_t>> edges;  // (tag, child)
+  edges.reserve(h->n_trie_pending * 2 + 16);
+  uint32_t max_depth = 0;
+  uint64_t n_trie = 0;
+  std::vector<uint32_t> whs;
+  std::vector<uint8_t> is_plus, is_hash;
+  for (uint32_t id = 0; id < h->filters.size(); ++id) {
+    const Filter& f = h->filters[id];
+    if (!f.in_trie) continue;
+    ++n_trie;
+    const uint8_t* p = h->pool.data() + f.off;
+    whs.clear();
+    is_plus.clear();
+    is_hash.clear();
+    uint64_t hw = FNV_OFF;
+    uint32_t s = 0;
+    for (uint32_t i = 0; i <= f.len; ++i) {
+      if (i == f.len || p[i] == '/') {
+        const uint32_t wl = i - s;
+        const bool pl = (wl == 1 && p[s] == '+');
+        const bool hs = (wl == 1 && p[s] == '#');
+        whs.push_back(pl ? PLUS_WH : word_hash(hw, wmask));
+        is_plus.push_back(pl);
+        is_hash.push_back(hs);
+        hw = FNV_OFF;
+        s = i + 1;
+      } else {
+        hw = fnv_step(hw, p[i]);
+      }
+    }
+    const size_t nw = whs.size();
+    const bool hash_last = is_hash[nw - 1];
+    const size_t path_len = hash_last ? nw - 1 : nw;  // '#' last: attach to the parent node
+    uint32_t cur = 0;
+    for (size_t w = 0; w < path_len; ++w) {
+      const uint64_t tag = edge_tag(cur, whs[w]);
+      bool ins;
+      uint32_t* v = emap.get_or_insert(tag, ins);
+      if (ins) {
+        const uint32_t child = (uint32_t)nflags.size();
+        if (child > CF_ID_MASK) {
+          h->err = "trie exceeds 2^27 nodes";
+          return -E2BIG;
+        }
+        *v = child;
+        nflags.push_back(0);
+        nhf.push_back(NONE);
+        ntw.push_back(NONE);
+        ntn.push_back(NONE);
+        edges.emplace_back(tag, child);
+        nflags[cur] |= is_plus[w] ? CF_PLUS : CF_LIT;
+      }
+      cur = *v;
+    }
+    max_depth = std::max<uint32_t>(max_depth, (uint32_t)path_len);
+    if (hash_last) {
+      lb.add(nhf[cur], id);
+    } else if (f.wild) {
+      lb.add(ntw[cur], id);
+      nflags[cur] |= CF_TW;
+    } else {
+      lb.add(ntn[cur], id);
+      nflags[cur] |= CF_TN;
+    }
+  }
+  // flatten multi lists
+  std::vector<uint32_t> multi(1, 0);
+  std::vector<uint32_t> list_pos(lb.lists.size());
+  for (size_t i = 0; i < lb.lists.size(); ++i) {
+    list_pos[i] = (uint32_t)multi.size();
+    multi.push_back((uint32_t)lb.lists[i].size());
+    multi.insert(multi.end(), lb.lists[i].begin(), lb.lists[i].end());
+  }
+  auto resolve = [&](uint32_t v) -> uint32_t {
+    if (v == NONE || !(v & LIST_MULTI)) return v;
+    return LIST_MULTI | list_pos[v & ~LIST_MULTI];
+  };
+  const size_t n_nodes = nflags.size();
+  std::vector<uint32_t> node_tw(n_nodes), node_tn(n_nodes);
+  std::vector<uint32_t> cfv(n_nodes), hfv(n_nodes);
+  for (size_t i = 0; i < n_nodes; ++i) {
+    node_tw[i] = resolve(ntw[i]);
+    node_tn[i] = resolve(ntn[i]);
+    uint32_t hf = resolve(nhf[i]);
+    uint32_t flags = nflags[i];
+    if (hf != NONE && (hf & LIST_MULTI)) {
+      flags |= CF_HFM;
+      hf &= ~LIST_MULTI;
+    }
+    cfv[i] = (uint32_t)i | flags;
+    hfv[i] = hf;
+  }
+  const uint64_t ecap = pow2_at_least(std::max<uint64_t>(64, edges.size() * 2));
+  std::vector<uint4> eslots(ecap, make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, NONE));
+  for (const auto& e : edges) {
+    uint64_t i = edge_slot(e.first, ecap - 1);
+    while (eslots[i].x != 0xFFFFFFFFu || eslots[i].y != 0xFFFFFFFFu) i = (i + 1) & (ecap - 1);
+    eslots[i] = make_uint4((uint32_t)e.first, (uint32_t)(e.first >> 32), cfv[e.second],
+                           hfv[e.second]);
+  }
+
+  // ---- exact route keys ----
+  uint64_t n_route = 0;
+  for (const Filter& f : h->filters) n_route += f.route_refs > 0;
+  const uint64_t xcap = pow2_at_least(std::max<uint64_t>(64, n_route * 2));
+  std::vector<uint4> xslots(xcap, make_uint4(0u, 0u, NONE, 0u));
+  for (uint32_t id = 0; id < h->filters.size(); ++id) {
+    const Filter& f = h->filters[id];
+    if (!f.route_refs) continue;
+    uint64_t x = FNV_OFF;
+    const uint8_t* p = h->pool.data() + f.off;
+    for (uint32_t i = 0; i < f.len; ++i) x = fnv_step(x, p[i]);
+    const uint64_t fh = full_hash(x, fmask);
+    uint64_t i = exact_slot(fh, xcap - 1);
+    while (xslots[i].z != NONE) i = (i + 1) & (xcap - 1);
+    xslots[i] = make_uint4((uint32_t)fh, (uint32_t)(fh >> 32), id, f.len);
+  }
+
+  // ---- filter string pool (append-only on the device) ----
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return fail(h, hipErrorInvalidDevice, "hipSetDevice");
+  const uint64_t need_pool = std::max<uint64_t>(1, h->pool.size());
+  if (need_pool > h->d_pool.bytes) {
+    DevBuf nb;
+    nb.bytes = std::max<uint64_t>(need_pool, h->d_pool.bytes * 2);
+    HIPCHK(h, hipMalloc(&nb.p, nb.bytes));
+    if (h->pool_uploaded)
+      HIPCHK(h, hipMemcpy(nb.p, h->d_pool.p, h->pool_uploaded, hipMemcpyDeviceToDevice));
+    if (h->d_pool.p) (void)hipFree(h->d_pool.p);
+    h->d_pool = nb;
+  }
+  if (h->pool.size() > h->pool_uploaded)
+    HIPCHK(h, hipMemcpy((uint8_t*)h->d_pool.p + h->pool_uploaded, h->pool.data() + h->pool_uploaded,
+                        h->pool.size() - h->pool_uploaded, hipMemcpyHostToDevice));
+  h->pool_uploaded = h->pool.size();
+  const uint64_t nf = h->filters.size();
+  const uint64_t need_off = (nf + 1) * sizeof(uint64_t);
+  if (need_off > h->d_foff.bytes) {
+    DevBuf nb;
+    nb.bytes = std::max<uint64_t>(need_off, h->d_foff.bytes * 2);
+    HIPCHK(h, hipMalloc(&nb.p, nb.bytes));
+    if (h->foff_uploaded)
+      HIPCHK(h, hipMemcpy(nb.p, h->d_foff.p, h->foff_uploaded * sizeof(uint64_t),
+                          hipMemcpyDeviceToDevice));
+    if (h->d_foff.p) (void)hipFree(h->d_foff.p);
+    h->d_foff = nb;
+  }
+  if (nf + 1 > h->foff_uploaded) {
+    std::vector<uint64_t> offs;
+    const uint64_t from = h->foff_uploaded ? h->foff_uploaded - 1 : 0;
+    for (uint64_t i = from; i <= nf; ++i)
+      offs.push_back(i < nf ? h->filters[i].off : (uint64_t)h->pool.size());
+    HIPCHK(h, hipMemcpy((uint64_t*)h->d_foff.p + from, offs.data(), offs.size() * sizeof(uint64_t),
+                        hipMemcpyHostToDevice));
+    h->foff_uploaded = nf + 1;
+  }
+
+  // ---- upload and swap ----
+  std::vector<DevBuf> nbufs;
+  DevIndex nx;
+  int rc = 0;
+  if ((rc = dev_upload(h, nbufs, eslots, &nx.edges)) ||
+      (rc = dev_upload(h, nbufs, node_tw, &nx.node_tw)) ||
+      (rc = dev_upload(h, nbufs, node_tn, &nx.node_tn)) ||
+      (rc = dev_upload(h, nbufs, multi, &nx.multi)) ||
+      (rc = dev_upload(h, nbufs, xslots, &nx.exact))) {
+    free_bufs(nbufs);
+    return rc;
+  }
+  nx.emask = ecap - 1;
+  nx.xmask = xcap - 1;
+  nx.root_cf = cfv[0];
+  nx.root_hf = hfv[0];
+  nx.fbytes = (const uint8_t*)h->d_pool.p;
+  nx.foff = (const uint64_t*)h->d_foff.p;
+  nx.word_mask = wmask;
+  nx.full_mask = fmask;
+  nx.max_depth = max_depth;
+  nx.trie_empty = (n_trie == 0);
+  nx.exact_empty = (n_route == 0);
+  free_bufs(h->ix_bufs);
+  h->ix_bufs.swap(nbufs);
+  for (Filter& f : h->filters) f.trie_committed = f.in_trie;
+  h->ix = nx;
+  h->epoch += 1;
+  h->dirty = false;
+
+  h->st.epoch = h->epoch;
+  h->st.n_filters = nf;
+  h->st.n_trie_filters = n_trie;
+  h->st.n_route_keys = n_route;
+  h->st.n_nodes = n_nodes;
+  h->st.n_edges = edges.size();
+  h->st.edge_slots = ecap;
+  h->st.exact_slots = xcap;
+  h->st.max_depth = max_depth;
+  h->st.device_bytes = ecap * 16 + xcap * 16 + n_nodes * 8 + multi.size() * 4 + h->pool.size() +
+                       (nf + 1) * 8;
+  return 0;
+}
+
+int dev_alloc(emqxgm* h, void** p, size_t bytes) {
+  HIPCHK(h, hipMalloc(p, std::max<size_t>(bytes, 16)));
+  DevBuf b;
+  b.p = *p;
+  b.bytes = bytes;
+  h->sc_bufs.push_back(b);
+  return 0;
+}
+
+// (Re)allocate batch scratch for n topics, `words` words and `pairs` staged pairs.
+int ensure_scratch(emqxgm* h, uint32_t n, uint64_t words, uint32_t pairs) {
+  Scratch& s = h->sc;
+  const uint64_t spill_need =
+      (uint64_t)(h->ix.max_depth > 8 ? h->ix.max_depth - 8 + 1 : 0) * h->geom.lanes;
+  if (n <= s.n_cap && words <= s.w_cap && pairs <= s.p_cap && spill_need <= s.spill_cap &&
+      s.ctl)
+    return 0;
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  const uint32_t ncap = std::max(n, s.n_cap);
+  const uint64_t wcap = std::max(words, s.w_cap);
+  const uint32_t pcap = std::max(pairs, s.p_cap);
+  const uint64_t scap = std::max(spill_need, s.spill_cap);
+  free_bufs(h->sc_bufs);
+  if (s.ctl_host) {
+    (void)hipHostFree(s.ctl_host);
+    s.ctl_host = nullptr;
+  }
+  s = Scratch();
+  int rc = 0;
+  const uint32_t stw = scan_tmp_words(ncap);
+  if ((rc = dev_alloc(h, (void**)&s.nw, (size_t)ncap * 4)) ||
+      (rc = dev_alloc(h, (void**)&s.wbase, (size_t)(ncap + 1) * 4)) ||
+      (rc = dev_alloc(h, (void**)&s.wh, (size_t)wcap * 4)) ||
+      (rc = dev_alloc(h, (void**)&s.rec, (size_t)ncap * 16)) ||
+      (rc = dev_alloc(h, (void**)&s.cnt, (size_t)ncap * 4)) ||
+      (rc = dev_alloc(h, (void**)&s.row, (size_t)(ncap + 1) * 4)) ||
+      (rc = dev_alloc(h, (void**)&s.row2, (size_t)(ncap + 1) * 4)) ||
+      (rc = dev_alloc(h, (void**)&s.rej, (size_t)ncap * 4)) ||
+      (rc = dev_alloc(h, (void**)&s.exact_id, (size_t)ncap * 4)) ||
+      (rc = dev_alloc(h, (void**)&s.pt, (size_t)pcap * 4)) ||
+      (rc = dev_alloc(h, (void**)&s.pf, (size_t)pcap * 4)) ||
+      (rc = dev_alloc(h, (void**)&s.pr, (size_t)pcap * 4)) ||
+      (rc = dev_alloc(h, (void**)&s.out, (size_t)pcap * 4)) ||
+      (rc = dev_alloc(h, (void**)&s.out2, (size_t)pcap * 4)) ||
+      (rc = dev_alloc(h, (void**)&s.scan_tmp, (size_t)stw * 4)) ||
+      (rc = dev_alloc(h, (void**)&s.ctl, CTL_N * 4)) ||
+      (rc = dev_alloc(h, (void**)&s.census, 4 * sizeof(unsigned long long))) ||
+      (rc = dev_alloc(h, (void**)&s.spill, (size_t)std::max<uint64_t>(scap, 1) * 16)))
+    return rc;
+  HIPCHK(h, hipHostMalloc((void**)&s.ctl_host, CTL_N * 4, hipHostMallocDefault));
+  s.n_cap = ncap;
+  s.w_cap = wcap;
+  s.p_cap = pcap;
+  s.o_cap = pcap;
+  s.scan_tmp_cap = stw;
+  s.spill_cap = scap;
+  return 0;
+}
+
+// One device pass over n topics already in HBM.  Leaves results in h->sc (row, out, exact_id)
+// and the total pair count in *pairs.
+int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_t n,
+               uint64_t bytes_len, uint32_t* pairs, uint64_t* census = nullptr) {
+  const uint64_t words = bytes_len + n + 1;
+  uint32_t want_pairs = std::max<uint32_t>(h->sc.p_cap, std::max<uint32_t>(1u << 20, n * 4u));
+  int rc = ensure_scratch(h, std::max<uint32_t>(n, 1), words, want_pairs);
+  if (rc) return rc;
+  Scratch& s = h->sc;
+  hipStream_t st = h->stream;
+  if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[0], st));
+  HIPCHK(h, hipMemsetAsync(s.ctl, 0, CTL_N * 4, st));
+  if (n == 0) {
+    HIPCHK(h, hipMemsetAsync(s.row, 0, 4, st));
+    *pairs = 0;
+    HIPCHK(h, hipStreamSynchronize(st));
+    return 0;
+  }
+  for (int attempt = 0;; ++attempt) {
+    if (census) HIPCHK(h, hipMemsetAsync(s.census, 0, 4 * sizeof(unsigned long long), st));
+    HIPCHK(h, launch_tok_count(d_bytes, d_off, n, s.nw, st));
+    HIPCHK(h, launch_scan(s.nw, s.wbase, n, s.scan_tmp, s.ctl + CTL_WORDS, st));
+    HIPCHK(h, launch_tok_hash(d_bytes, d_off, n, h->ix, s, st));
+    if (h->ix.trie_empty) {
+      HIPCHK(h, hipMemsetAsync(s.row, 0, (size_t)(n + 1) * 4, st));
+      HIPCHK(h, hipMemsetAsync(s.ctl + CTL_TOTAL, 0, 4, st));
+    } else {
+      HIPCHK(h, hipMemsetAsync(s.rej, 0, (size_t)n * 4, st));
+      if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[1], st));
+      HIPCHK(h, launch_walk(h->ix, s, n, h->geom, st, census ? s.census : nullptr));
+      if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[2], st));
+      HIPCHK(h, launch_scan(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, st));
+      HIPCHK(h, launch_verify_scatter(d_bytes, d_off, h->ix, s, n, st));
+    }
+    if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[3], st));
+    HIPCHK(h, hipMemcpyAsync(s.ctl_host, s.ctl, CTL_N * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    const uint32_t top = s.ctl_host[CTL_PAIR_TOP];
+    if (top <= s.p_cap) break;
+    // staging overflow: nothing beyond the capacity was written; grow and redo the pass
+    h->st.reruns += 1;
+    if (attempt > 4) {
+      h->err = "pair staging overflow did not converge";
+      return -ENOMEM;
+    }
+    const uint64_t np = std::min<uint64_t>(0xF0000000ull, (uint64_t)top * 2 + (1u << 20));
+    rc = ensure_scratch(h, n, words, (uint32_t)np);
+    if (rc) return rc;
+    HIPCHK(h, hipMemsetAsync(s.ctl, 0, CTL_N * 4, st));
+  }
+  if (h->profiling) {
+    float a = 0, b = 0;
+    if (!h->ix.trie_empty) {
+      HIPCHK(h, hipEventElapsedTime(&a, h->ev[1], h->ev[2]));
+      h->st.walk_ms += a;
+      h->st.walk_launches += 1;
+    }
+    HIPCHK(h, hipEventElapsedTime(&b, h->ev[0], h->ev[3]));
+    h->st.total_ms += b;
+  }
+  if (s.ctl_host[CTL_ANY_REJ]) {
+    HIPCHK(h, launch_fixup(s, n, st));
+    HIPCHK(h, hipMemcpyAsync(s.ctl_host + CTL_TOTAL, s.ctl + CTL_TOTAL, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    std::swap(s.row, s.row2);
+    std::swap(s.out, s.out2);
+    h->st.rejected_pairs += 1;  // batches that needed the fix-up pass
+  }
+  *pairs = s.ctl_host[CTL_TOTAL];
+  if (census) {
+    unsigned long long c[4] = {0, 0, 0, 0};
+    HIPCHK(h, hipMemcpy(c, s.census, sizeof c, hipMemcpyDeviceToHost));
+    census[0] = c[0];
+    census[1] = c[1];
+    census[2] = *pairs;
+    census[3] = s.ctl_host[CTL_WORDS];
+  }
+  h->st.batches += 1;
+  h->st.topics += n;
+  h->st.pairs += *pairs;
+  return 0;
+}
+
+int ensure_input(emqxgm* h, uint64_t bytes, uint64_t offs) {
+  if (bytes > h->in_bytes_cap) {
+    if (h->d_in_bytes) (void)hipFree(h->d_in_bytes);
+    h->d_in_bytes = nullptr;
+    const uint64_t cap = std::max<uint64_t>(bytes, 1 << 20);
+    HIPCHK(h, hipMalloc((void**)&h->d_in_bytes, cap));
+    h->in_bytes_cap = cap;
+  }
+  if (offs > h->in_off_cap) {
+    if (h->d_in_off) (void)hipFree(h->d_in_off);
+    h->d_in_off = nullptr;
+    const uint64_t cap = std::max<uint64_t>(offs, 1 << 16);
+    HIPCHK(h, hipMalloc((void**)&h->d_in_off, cap * 4));
+    h->in_off_cap = cap;
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int emqxgm_abi_version(void) { return EMQXGM_ABI_VERSION; }
+
+int emqxgm_create(const emqxgm_cfg* cfg, emqxgm_t** out) {
+  if (!out) return -EINVAL;
+  *out = nullptr;
+  emqxgm* h = new (std::nothrow) emqxgm();
+  if (!h) return -ENOMEM;
+  if (cfg) h->cfg = *cfg;
+  if (h->cfg.word_hash_bits == 0 || h->cfg.word_hash_bits > 32) h->cfg.word_hash_bits = 32;
+  if (h->cfg.full_hash_bits == 0 || h->cfg.full_hash_bits > 64) h->cfg.full_hash_bits = 64;
+  if (h->cfg.batch_max == 0) h->cfg.batch_max = 4u << 20;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || h->cfg.device < 0 ||
+      h->cfg.device >= ndev) {
+    delete h;
+    return -EIO;
+  }
+  if (hipSetDevice(h->cfg.device) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return -EIO;
+  }
+  for (auto& e : h->ev)
+    if (hipEventCreate(&e) != hipSuccess) {
+      delete h;
+      return -EIO;
+    }
+  h->geom = walk_geometry(h->cfg.device, h->cfg.walk_wg_per_cu);
+  int rc = commit_locked(h);  // empty index
+  if (rc) {
+    emqxgm_destroy(h);
+    return rc;
+  }
+  *out = h;
+  return 0;
+}
+
+void emqxgm_destroy(emqxgm_t* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->cfg.device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  free_bufs(h->ix_bufs);
+  free_bufs(h->sc_bufs);
+  if (h->sc.ctl_host) (void)hipHostFree(h->sc.ctl_host);
+  if (h->d_pool.p) (void)hipFree(h->d_pool.p);
+  if (h->d_foff.p) (void)hipFree(h->d_foff.p);
+  if (h->d_in_bytes) (void)hipFree(h->d_in_bytes);
+  if (h->d_in_off) (void)hipFree(h->d_in_off);
+  for (auto& e : h->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+static int trie_insert_locked(emqxgm* h, const uint8_t* p, uint32_t len, uint32_t* id) {
+  if (len > 65535) return -EINVAL;  // emqx_topic.erl:47 MAX_TOPIC_LEN
+  if (h->filters.size() >= 0x7FFFFFFFu) return -E2BIG;
+  const uint32_t i = find_id(h, p, len, true);
+  if (!h->filters[i].in_trie) {
+    h->filters[i].in_trie = 1;
+    ++h->n_trie_pending;
+    h->dirty = true;
+  }
+  if (id) *id = i;
+  return 0;
+}
+
+static int route_ref_locked(emqxgm* h, const uint8_t* p, uint32_t len, uint32_t* id) {
+  if (len > 65535) return -EINVAL;
+  if (h->filters.size() >= 0x7FFFFFFFu) return -E2BIG;
+  const uint32_t i = find_id(h, p, len, true);
+  if (h->filters[i].route_refs++ == 0) {
+    ++h->n_route_pending;
+    h->dirty = true;
+  }
+  if (id) *id = i;
+  return 0;
+}
+
+int emqxgm_trie_insert(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t* id) {
+  if (!h || (!filter && len)) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  return trie_insert_locked(h, filter, len, id);
+}
+
+int emqxgm_trie_delete(emqxgm_t* h, const uint8_t* filter, uint32_t len) {
+  if (!h || (!filter && len)) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  const uint32_t i = find_id(h, filter, len, false);
+  if (i != NONE && h->filters[i].in_trie) {  // absent filter: no-op (emqx_trie.erl:139-144)
+    h->filters[i].in_trie = 0;
+    --h->n_trie_pending;
+    h->dirty = true;
+  }
+  return 0;
+}
+
+int emqxgm_route_ref(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t* id) {
+  if (!h || (!filter && len)) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  return route_ref_locked(h, filter, len, id);
+}
+
+int emqxgm_route_unref(emqxgm_t* h, const uint8_t* filter, uint32_t len) {
+  if (!h || (!filter && len)) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  const uint32_t i = find_id(h, filter, len, false);
+  if (i == NONE || h->filters[i].route_refs == 0) return -ENOENT;
+  if (--h->filters[i].route_refs == 0) {
+    --h->n_route_pending;
+    h->dirty = true;
+  }
+  return 0;
+}
+
+int emqxgm_trie_insert_many(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets,
+                            uint64_t n, uint32_t* ids) {
+  if (!h || !offsets || (!bytes && n)) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t b = offsets[i], e = offsets[i + 1];
+    if (e < b || e - b > 65535) return -EINVAL;
+    int rc = trie_insert_locked(h, bytes + b, (uint32_t)(e - b), ids ? ids + i : nullptr);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+int emqxgm_route_ref_many(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                          uint32_t* ids) {
+  if (!h || !offsets || (!bytes && n)) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t b = offsets[i], e = offsets[i + 1];
+    if (e < b || e - b > 65535) return -EINVAL;
+    int rc = route_ref_locked(h, bytes + b, (uint32_t)(e - b), ids ? ids + i : nullptr);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+int emqxgm_commit(emqxgm_t* h, uint64_t* epoch) {
+  if (!h) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  int rc = 0;
+  if (h->dirty) rc = commit_locked(h);
+  if (epoch) *epoch = h->epoch;
+  return rc;
+}
+
+int emqxgm_trie_empty(emqxgm_t* h) {
+  if (!h) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  return h->ix.trie_empty ? 1 : 0;
+}
+
+int emqxgm_trie_member(emqxgm_t* h, const uint8_t* filter, uint32_t len) {
+  if (!h || (!filter && len)) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  const uint32_t i = find_id(h, filter, len, false);
+  return (i != NONE && h->filters[i].trie_committed) ? 1 : 0;
+}
+
+int emqxgm_lookup_id(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t* id) {
+  if (!h || !id || (!filter && len)) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  const uint32_t i = find_id(h, filter, len, false);
+  if (i == NONE) return -ENOENT;
+  *id = i;
+  return 0;
+}
+
+int emqxgm_filter_bytes(emqxgm_t* h, uint32_t id, const uint8_t** p, uint32_t* len) {
+  if (!h || !p || !len) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (id >= h->filters.size()) return -ENOENT;
+  *p = h->pool.data() + h->filters[id].off;
+  *len = h->filters[id].len;
+  return 0;
+}
+
+int emqxgm_match_device(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_offsets, uint32_t n,
+                        uint64_t bytes_len, emqxgm_dev_out* out) {
+  if (!h || !out || (!d_offsets && n)) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
+  uint32_t pairs = 0;
+  int rc = run_device(h, d_bytes, d_offsets, n, bytes_len, &pairs);
+  if (rc) return rc;
+  out->n = n;
+  out->n_pairs = pairs;
+  out->row_ptr = h->sc.row;
+  out->filter_id = h->sc.out;
+  out->exact_id = h->sc.exact_id;
+  out->n_words = h->sc.nw;
+  return 0;
+}
+
+int emqxgm_match_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets, uint32_t n,
+                       emqxgm_out* out) {
+  if (!h || !out || (!offsets && n)) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
+  h->h_row.assign((size_t)n + 1, 0);
+  h->h_exact.assign(n, NONE);
+  h->h_fid.clear();
+  std::vector<uint32_t> loff;
+  for (uint32_t i0 = 0; i0 < n || (n == 0 && i0 == 0); i0 += h->cfg.batch_max) {
+    const uint32_t i1 = std::min<uint64_t>((uint64_t)i0 + h->cfg.batch_max, n);
+    const uint32_t m = i1 - i0;
+    const uint64_t b0 = n ? offsets[i0] : 0, b1 = n ? offsets[i1] : 0;
+    if (b1 < b0) return -EINVAL;
+    loff.resize((size_t)m + 1);
+    for (uint32_t i = 0; i <= m; ++i) {
+      if (offsets[i0 + i] < b0 || (i && offsets[i0 + i] < offsets[i0 + i - 1])) return -EINVAL;
+      loff[i] = (uint32_t)(offsets[i0 + i] - b0);
+    }
+    int rc = ensure_input(h, std::max<uint64_t>(b1 - b0, 1), (uint64_t)m + 1);
+    if (rc) return rc;
+    if (b1 > b0)
+      HIPCHK(h, hipMemcpyAsync(h->d_in_bytes, bytes + b0, b1 - b0, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->d_in_off, loff.data(), ((size_t)m + 1) * 4, hipMemcpyHostToDevice,
+                             h->stream));
+    uint32_t pairs = 0;
+    rc = run_device(h, h->d_in_bytes, h->d_in_off, m, b1 - b0, &pairs);
+    if (rc) return rc;
+    h->h_row32.resize((size_t)m + 1);
+    h->h_fid_tmp.resize(pairs);
+    if (m) {
+      HIPCHK(h, hipMemcpyAsync(h->h_row32.data(), h->sc.row, ((size_t)m + 1) * 4,
+                               hipMemcpyDeviceToHost, h->stream));
+      HIPCHK(h, hipMemcpyAsync(h->h_exact.data() + i0, h->sc.exact_id, (size_t)m * 4,
+                               hipMemcpyDeviceToHost, h->stream));
+    }
+    if (pairs)
+      HIPCHK(h, hipMemcpyAsync(h->h_fid_tmp.data(), h->sc.out, (size_t)pairs * 4,
+                               hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    const uint64_t base = h->h_fid.size();
+    for (uint32_t i = 0; i <= m; ++i) h->h_row[i0 + i] = base + h->h_row32[i];
+    h->h_fid.insert(h->h_fid.end(), h->h_fid_tmp.begin(), h->h_fid_tmp.end());
+    if (n == 0) break;
+  }
+  out->n = n;
+  out->n_pairs = h->h_fid.size();
+  out->row_ptr = h->h_row.data();
+  out->filter_id = h->h_fid.data();
+  out->exact_id = h->h_exact.data();
+  return 0;
+}
+
+int emqxgm_walk_census(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_offsets, uint32_t n,
+                       uint64_t bytes_len, uint64_t out[4]) {
+  if (!h || !out || (!d_offsets && n)) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
+  uint32_t pairs = 0;
+  memset(out, 0, 4 * sizeof(uint64_t));
+  return run_device(h, d_bytes, d_offsets, n, bytes_len, &pairs, out);
+}
+
+int emqxgm_set_profiling(emqxgm_t* h, int on) {
+  if (!h) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  h->profiling = on != 0;
+  return 0;
+}
+
+int emqxgm_get_stats(emqxgm_t* h, emqxgm_stats* st) {
+  if (!h || !st) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  *st = h->st;
+  return 0;
+}
+
+const char* emqxgm_last_error(emqxgm_t* h) { return h ? h->err.c_str() : "null handle"; }
+
+}  // extern "C"

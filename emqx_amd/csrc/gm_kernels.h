@@ -1,0 +1,87 @@
+// gm_kernels.h -- launch interface of the gfx950 match pipeline (gm_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gm {
+
+// Committed device index (all pointers are device memory).
+struct DevIndex {
+  const uint4* edges = nullptr;   // edge slots {tag.lo, tag.hi, cf, hf}
+  uint64_t emask = 0;             // edge capacity - 1
+  const uint32_t* node_tw = nullptr;
+  const uint32_t* node_tn = nullptr;
+  const uint32_t* multi = nullptr;  // [count, fid...] lists
+  uint32_t root_cf = 0, root_hf = 0xFFFFFFFFu;
+  const uint4* exact = nullptr;   // exact slots {hash.lo, hash.hi, fid, len}
+  uint64_t xmask = 0;
+  const uint8_t* fbytes = nullptr;  // filter string pool
+  const uint64_t* foff = nullptr;   // [n_filters+1]
+  uint32_t word_mask = 0xFFFFFFFFu;
+  uint64_t full_mask = ~0ull;
+  uint32_t max_depth = 0;           // deepest trie filter in levels
+  bool trie_empty = true;
+  bool exact_empty = true;
+};
+
+// Per-batch scratch (device memory, owned by the engine, grown on demand).
+struct Scratch {
+  uint32_t n_cap = 0;  // topic capacity
+  uint64_t w_cap = 0;  // word capacity
+  uint32_t* nw = nullptr;     // [n]   words per topic
+  uint32_t* wbase = nullptr;  // [n+1]
+  uint32_t* wh = nullptr;     // [w]   level-token hashes
+  uint4* rec = nullptr;       // [n]   {wbase, n_words, flags, wh0}
+  uint32_t* cnt = nullptr;    // [n]   trie matches per topic
+  uint32_t* row = nullptr;    // [n+1]
+  uint32_t* row2 = nullptr;   // [n+1] (fix-up)
+  uint32_t* rej = nullptr;    // [n]   rejected pairs per topic
+  uint32_t* exact_id = nullptr;  // [n]
+  uint32_t p_cap = 0;   // pair staging capacity
+  uint32_t* pt = nullptr;     // staged pair: topic
+  uint32_t* pf = nullptr;     // staged pair: filter
+  uint32_t* pr = nullptr;     // staged pair: rank within topic
+  uint32_t o_cap = 0;
+  uint32_t* out = nullptr;    // [pairs] CSR filter ids
+  uint32_t* out2 = nullptr;   // fix-up target
+  uint32_t* scan_tmp = nullptr;  // scan partials
+  uint32_t scan_tmp_cap = 0;
+  uint32_t* ctl = nullptr;    // control words (see CTL_*)
+  uint4* spill = nullptr;     // walk stack spill (depth beyond LDS)
+  uint64_t spill_cap = 0;     // entries
+  uint32_t* ctl_host = nullptr;  // pinned host mirror of ctl
+  unsigned long long* census = nullptr;  // [4] diagnostic walk counters
+};
+
+enum : int {
+  CTL_TOPIC_CTR = 0,  // walk topic-block claim counter
+  CTL_PAIR_TOP = 1,   // staged pair slots reserved
+  CTL_ANY_REJ = 2,    // a verification rejected some pair
+  CTL_TOTAL = 3,      // total pairs (row[n]) copied here
+  CTL_WORDS = 4,      // total words
+  CTL_N = 8
+};
+
+struct WalkGeom {
+  uint32_t blocks = 0;      // persistent workgroups
+  uint32_t lanes = 0;       // blocks * 256
+};
+
+WalkGeom walk_geometry(int device, uint32_t wg_per_cu);
+
+// Pipeline stages (all asynchronous on `s`).
+hipError_t launch_tok_count(const uint8_t* bytes, const uint32_t* off, uint32_t n, uint32_t* nw,
+                            hipStream_t s);
+hipError_t launch_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* tmp,
+                       uint32_t* total_dst, hipStream_t s);
+uint32_t scan_tmp_words(uint32_t n);
+hipError_t launch_tok_hash(const uint8_t* bytes, const uint32_t* off, uint32_t n,
+                           const DevIndex& ix, Scratch& sc, hipStream_t s);
+// census != nullptr selects the diagnostic walk that adds {states, slot loads} to census[0..1]
+hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGeom& g,
+                       hipStream_t s, unsigned long long* census = nullptr);
+hipError_t launch_verify_scatter(const uint8_t* bytes, const uint32_t* off, const DevIndex& ix,
+                                 Scratch& sc, uint32_t n, hipStream_t s);
+hipError_t launch_fixup(Scratch& sc, uint32_t n, hipStream_t s);  // after CTL_ANY_REJ
+
+}  // namespace gm

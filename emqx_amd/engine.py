@@ -1,0 +1,269 @@
+"""ctypes binding of the engine's C-ABI (include/emqx_gpumatch.h).
+
+This is the only way the Python host code reaches the device: there is no CPU fallback.  If the
+in-tree ``libemqx_gpumatch.so`` (built by ``emqx_amd.build``) is missing, importing this module
+raises; if the engine cannot be created on the device, ``Engine()`` raises ``EngineError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import errno
+import os
+from dataclasses import dataclass
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libemqx_gpumatch.so")
+NONE = 0xFFFFFFFF
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+class _Cfg(C.Structure):
+    _fields_ = [("device", C.c_int32), ("word_hash_bits", C.c_uint32),
+                ("full_hash_bits", C.c_uint32), ("batch_max", C.c_uint32),
+                ("walk_wg_per_cu", C.c_uint32), ("reserved", C.c_uint32 * 3)]
+
+
+class _Out(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("n_pairs", C.c_uint64),
+                ("row_ptr", C.POINTER(C.c_uint64)), ("filter_id", C.POINTER(C.c_uint32)),
+                ("exact_id", C.POINTER(C.c_uint32))]
+
+
+class _DevOut(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("n_pairs", C.c_uint32), ("row_ptr", C.c_void_p),
+                ("filter_id", C.c_void_p), ("exact_id", C.c_void_p), ("n_words", C.c_void_p)]
+
+
+class _Stats(C.Structure):
+    _fields_ = [("epoch", C.c_uint64), ("n_filters", C.c_uint64), ("n_trie_filters", C.c_uint64),
+                ("n_route_keys", C.c_uint64), ("n_nodes", C.c_uint64), ("n_edges", C.c_uint64),
+                ("edge_slots", C.c_uint64), ("exact_slots", C.c_uint64),
+                ("device_bytes", C.c_uint64), ("max_depth", C.c_uint32),
+                ("collisions_merged", C.c_uint32), ("batches", C.c_uint64),
+                ("topics", C.c_uint64), ("pairs", C.c_uint64), ("rejected_pairs", C.c_uint64),
+                ("reruns", C.c_uint64), ("walk_ms", C.c_double), ("walk_launches", C.c_uint64),
+                ("total_ms", C.c_double)]
+
+
+# name -> (restype, argtypes): exactly the entry points declared in include/emqx_gpumatch.h
+_P = C.c_void_p
+_U8P = C.POINTER(C.c_uint8)
+_U32P = C.POINTER(C.c_uint32)
+_U64P = C.POINTER(C.c_uint64)
+SYMBOLS = {
+    "emqxgm_abi_version": (C.c_int, []),
+    "emqxgm_create": (C.c_int, [C.POINTER(_Cfg), C.POINTER(_P)]),
+    "emqxgm_destroy": (None, [_P]),
+    "emqxgm_trie_insert": (C.c_int, [_P, C.c_char_p, C.c_uint32, _U32P]),
+    "emqxgm_trie_delete": (C.c_int, [_P, C.c_char_p, C.c_uint32]),
+    "emqxgm_route_ref": (C.c_int, [_P, C.c_char_p, C.c_uint32, _U32P]),
+    "emqxgm_route_unref": (C.c_int, [_P, C.c_char_p, C.c_uint32]),
+    "emqxgm_trie_insert_many": (C.c_int, [_P, _P, _P, C.c_uint64, _P]),
+    "emqxgm_route_ref_many": (C.c_int, [_P, _P, _P, C.c_uint64, _P]),
+    "emqxgm_commit": (C.c_int, [_P, _U64P]),
+    "emqxgm_trie_empty": (C.c_int, [_P]),
+    "emqxgm_trie_member": (C.c_int, [_P, C.c_char_p, C.c_uint32]),
+    "emqxgm_lookup_id": (C.c_int, [_P, C.c_char_p, C.c_uint32, _U32P]),
+    "emqxgm_filter_bytes": (C.c_int, [_P, C.POINTER(_U8P), _U32P]),
+    "emqxgm_match_batch": (C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(_Out)]),
+    "emqxgm_match_device": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, C.POINTER(_DevOut)]),
+    "emqxgm_walk_census": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, _U64P]),
+    "emqxgm_set_profiling": (C.c_int, [_P, C.c_int]),
+    "emqxgm_get_stats": (C.c_int, [_P, C.POINTER(_Stats)]),
+    "emqxgm_last_error": (C.c_char_p, [_P]),
+}
+
+
+def load_library(path: str = LIB_PATH) -> C.CDLL:
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} is missing: build the HIP engine first (python -m emqx_amd.build); "
+            "there is no CPU fallback")
+    lib = C.CDLL(path)
+    for name, (res, args) in SYMBOLS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.emqxgm_abi_version() != 1:
+        raise ImportError("emqx_gpumatch ABI mismatch")
+    return lib
+
+
+_lib: Optional[C.CDLL] = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        _lib = load_library()
+    return _lib
+
+
+def pack(items: Sequence[bytes], off_dtype=np.uint64) -> Tuple[np.ndarray, np.ndarray]:
+    """Pack byte strings into (bytes u8, offsets[n+1])."""
+    lens = np.fromiter((len(x) for x in items), dtype=np.uint64, count=len(items))
+    off = np.zeros(len(items) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=off[1:])
+    buf = np.frombuffer(b"".join(items), dtype=np.uint8) if items else np.zeros(0, np.uint8)
+    return buf, off.astype(off_dtype)
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p) if a.size else C.c_void_p(0)
+
+
+@dataclass
+class MatchResult:
+    """Host-resident result of a batch: CSR rows of trie filter ids + exact route key ids."""
+    row_ptr: np.ndarray    # uint64 [n+1]
+    filter_id: np.ndarray  # uint32 [n_pairs]
+    exact_id: np.ndarray   # uint32 [n]  (NONE = no route key equal to the topic)
+
+    def row(self, i: int) -> np.ndarray:
+        return self.filter_id[self.row_ptr[i]:self.row_ptr[i + 1]]
+
+
+@dataclass
+class DeviceResult:
+    n: int
+    n_pairs: int
+    row_ptr: int    # device pointers (valid until the next match on the engine)
+    filter_id: int
+    exact_id: int
+    n_words: int
+
+
+class Engine:
+    """One engine instance = one device index (one emqx_trie + route-key set) on one GPU."""
+
+    def __init__(self, device: int = 0, word_hash_bits: int = 32, full_hash_bits: int = 64,
+                 batch_max: int = 0, walk_wg_per_cu: int = 0):
+        self._lib = lib()
+        cfg = _Cfg(device, word_hash_bits, full_hash_bits, batch_max, walk_wg_per_cu)
+        h = C.c_void_p()
+        rc = self._lib.emqxgm_create(C.byref(cfg), C.byref(h))
+        if rc != 0:
+            raise EngineError(f"emqxgm_create failed ({rc}): no usable HIP device {device}")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.emqxgm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str):
+        if rc < 0:
+            msg = self._lib.emqxgm_last_error(self._h) or b""
+            raise EngineError(f"{what}: {errno.errorcode.get(-rc, rc)} {msg.decode(errors='replace')}")
+        return rc
+
+    # ---- index mutation ----
+    def trie_insert(self, f: bytes) -> int:
+        i = C.c_uint32()
+        self._check(self._lib.emqxgm_trie_insert(self._h, f, len(f), C.byref(i)), "trie_insert")
+        return i.value
+
+    def trie_delete(self, f: bytes) -> None:
+        self._check(self._lib.emqxgm_trie_delete(self._h, f, len(f)), "trie_delete")
+
+    def route_ref(self, f: bytes) -> int:
+        i = C.c_uint32()
+        self._check(self._lib.emqxgm_route_ref(self._h, f, len(f), C.byref(i)), "route_ref")
+        return i.value
+
+    def route_unref(self, f: bytes) -> None:
+        self._check(self._lib.emqxgm_route_unref(self._h, f, len(f)), "route_unref")
+
+    def trie_insert_many(self, buf: np.ndarray, off: np.ndarray) -> np.ndarray:
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        ids = np.empty(len(off) - 1, dtype=np.uint32)
+        self._check(self._lib.emqxgm_trie_insert_many(self._h, _ptr(buf), _ptr(off), len(ids),
+                                                       _ptr(ids)), "trie_insert_many")
+        return ids
+
+    def route_ref_many(self, buf: np.ndarray, off: np.ndarray) -> np.ndarray:
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        ids = np.empty(len(off) - 1, dtype=np.uint32)
+        self._check(self._lib.emqxgm_route_ref_many(self._h, _ptr(buf), _ptr(off), len(ids),
+                                                     _ptr(ids)), "route_ref_many")
+        return ids
+
+    def commit(self) -> int:
+        e = C.c_uint64()
+        self._check(self._lib.emqxgm_commit(self._h, C.byref(e)), "commit")
+        return e.value
+
+    def trie_empty(self) -> bool:
+        return bool(self._check(self._lib.emqxgm_trie_empty(self._h), "trie_empty"))
+
+    def trie_member(self, f: bytes) -> bool:
+        return bool(self._check(self._lib.emqxgm_trie_member(self._h, f, len(f)), "trie_member"))
+
+    def lookup_id(self, f: bytes) -> Optional[int]:
+        i = C.c_uint32()
+        rc = self._lib.emqxgm_lookup_id(self._h, f, len(f), C.byref(i))
+        return None if rc == -errno.ENOENT else (self._check(rc, "lookup_id") or i.value)
+
+    def filter_bytes(self, fid: int) -> bytes:
+        p = _U8P()
+        n = C.c_uint32()
+        self._check(self._lib.emqxgm_filter_bytes(self._h, fid, C.byref(p), C.byref(n)),
+                    "filter_bytes")
+        return C.string_at(p, n.value)
+
+    # ---- match ----
+    def match_packed(self, buf: np.ndarray, off: np.ndarray) -> MatchResult:
+        off32 = np.ascontiguousarray(off, dtype=np.uint32)
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        n = len(off32) - 1
+        out = _Out()
+        self._check(self._lib.emqxgm_match_batch(self._h, _ptr(buf), _ptr(off32), n,
+                                                 C.byref(out)), "match_batch")
+        row = np.ctypeslib.as_array(out.row_ptr, shape=(n + 1,)).copy()
+        fid = (np.ctypeslib.as_array(out.filter_id, shape=(out.n_pairs,)).copy()
+               if out.n_pairs else np.zeros(0, np.uint32))
+        ex = (np.ctypeslib.as_array(out.exact_id, shape=(n,)).copy() if n
+              else np.zeros(0, np.uint32))
+        return MatchResult(row, fid, ex)
+
+    def match(self, topics: Sequence[bytes]) -> MatchResult:
+        buf, off = pack(list(topics), np.uint64)
+        if len(buf) > 0xFFFFFFFF:
+            raise EngineError("batch larger than 4 GiB: split it")
+        return self.match_packed(buf, off)
+
+    def match_device(self, d_bytes: int, d_off: int, n: int, bytes_len: int) -> DeviceResult:
+        o = _DevOut()
+        self._check(self._lib.emqxgm_match_device(self._h, C.c_void_p(d_bytes), C.c_void_p(d_off),
+                                                  n, bytes_len, C.byref(o)), "match_device")
+        return DeviceResult(o.n, o.n_pairs, o.row_ptr or 0, o.filter_id or 0, o.exact_id or 0,
+                            o.n_words or 0)
+
+    def walk_census(self, d_bytes: int, d_off: int, n: int, bytes_len: int) -> dict:
+        """Instrumented pass: {'states': sum S(t), 'slot_loads', 'pairs', 'words'}."""
+        out = (C.c_uint64 * 4)()
+        self._check(self._lib.emqxgm_walk_census(self._h, C.c_void_p(d_bytes), C.c_void_p(d_off),
+                                                 n, bytes_len, out), "walk_census")
+        return {"states": out[0], "slot_loads": out[1], "pairs": out[2], "words": out[3]}
+
+    def set_profiling(self, on: bool) -> None:
+        self._check(self._lib.emqxgm_set_profiling(self._h, 1 if on else 0), "set_profiling")
+
+    def stats(self) -> dict:
+        s = _Stats()
+        self._check(self._lib.emqxgm_get_stats(self._h, C.byref(s)), "stats")
+        return {k: getattr(s, k) for k, _ in _Stats._fields_}

@@ -1,0 +1,148 @@
+/*
+ * emqx_gpumatch.h -- C-ABI of the MI355X-native batched MQTT topic-matching engine.
+ *
+ * This is the drop-in boundary for the publish-time match path of EMQX 5.0.14
+ * (fengyangdi/emqx).  Plain pointers and sizes only; no torch/HIP types.  Each entry point
+ * names the reference interface it replaces (paths relative to the reference checkout):
+ *
+ *   emqxgm_trie_insert   <- emqx_trie:insert/1        apps/emqx/src/emqx_trie.erl:113-127
+ *   emqxgm_trie_delete   <- emqx_trie:delete/1        apps/emqx/src/emqx_trie.erl:130-144
+ *   emqxgm_trie_empty    <- emqx_trie:empty/0         apps/emqx/src/emqx_trie.erl:172-178
+ *   emqxgm_trie_member   <- emqx_trie:lookup_topic/2  apps/emqx/src/emqx_trie.erl:267-271
+ *   emqxgm_route_ref     <- route-bag key insert      apps/emqx/src/emqx_router_utils.erl:31-39
+ *   emqxgm_route_unref   <- route-bag key delete      apps/emqx/src/emqx_router_utils.erl:48-71
+ *   emqxgm_commit        <- mnesia/mria commit point  (snapshot swap; readers never see partial
+ *                           state; emqx_router_utils.erl:74-135 is where writes commit)
+ *   emqxgm_match_batch   <- emqx_trie:match/1 + emqx_router:match_routes/1 over a batch of
+ *                           published topics        apps/emqx/src/emqx_trie.erl:147-169,
+ *                                                    apps/emqx/src/emqx_router.erl:141-157,
+ *                           tokenising per emqx_topic:words/1 (emqx_topic.erl:155-169)
+ *   emqxgm_match_device  <- the same with topic bytes / results resident in HBM
+ *   emqxgm_filter_bytes  <- filter id -> filter binary (the trie returns binaries)
+ *
+ * Result semantics (bit-exact with the reference, SURVEY.md 8a/8a'):
+ *   for topic t, trie row = { f in trie : emqx_trie:match(t) returns f }  (no duplicates;
+ *   [] for a wildcard topic name), exact_id[t] = id of the route key equal to t's bytes (or
+ *   EMQXGM_NONE).  match_routes(t) = routes(exact) ++ routes(row).  Row order is
+ *   deterministic for a given committed index, but callers should treat it as a set, as the
+ *   reference tests do (lists:sort).
+ *
+ * Return codes: 0 on success, or a negative errno: -EINVAL (bad argument), -ENOMEM (host or
+ * device allocation failed), -EIO (device/HIP failure), -ENOENT (unknown id), -E2BIG (index
+ * exceeds the device layout limits: 2^27 trie nodes, 2^31 filters).  There is no CPU fallback:
+ * a device failure is reported, never silently recomputed on the host.
+ *
+ * Ownership: input buffers are borrowed for the duration of the call.  Output arrays in
+ * emqxgm_out / emqxgm_dev_out are owned by the engine and stay valid until the next match
+ * call on the same handle or emqxgm_destroy.
+ *
+ * Threading: add/remove/commit and match calls are serialised by a per-handle lock; match
+ * always reads the last committed epoch.
+ */
+#ifndef EMQX_GPUMATCH_H
+#define EMQX_GPUMATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EMQXGM_NONE 0xFFFFFFFFu
+#define EMQXGM_ABI_VERSION 1
+
+typedef struct emqxgm emqxgm_t;
+
+typedef struct emqxgm_cfg {
+  int32_t device;          /* HIP device ordinal */
+  uint32_t word_hash_bits; /* bits kept of each 32-bit level-token hash; 32 in production,
+                              small values only to force collisions in tests */
+  uint32_t full_hash_bits; /* bits kept of the 64-bit whole-topic hash (exact table); 64 */
+  uint32_t batch_max;      /* topics per device pass of emqxgm_match_batch (0 = 4Mi) */
+  uint32_t walk_wg_per_cu; /* persistent walk workgroups per CU (0 = default) */
+  uint32_t reserved[3];
+} emqxgm_cfg;
+
+typedef struct emqxgm_out { /* host-resident result of emqxgm_match_batch */
+  uint32_t n;               /* topics */
+  uint64_t n_pairs;         /* total trie matches */
+  const uint64_t* row_ptr;  /* [n+1] CSR offsets into filter_id */
+  const uint32_t* filter_id;/* [n_pairs] matched trie filter ids */
+  const uint32_t* exact_id; /* [n] route key equal to the topic, or EMQXGM_NONE */
+} emqxgm_out;
+
+typedef struct emqxgm_dev_out { /* device-resident result of emqxgm_match_device */
+  uint32_t n;
+  uint32_t n_pairs;
+  const uint32_t* row_ptr;  /* device [n+1] */
+  const uint32_t* filter_id;/* device [n_pairs] */
+  const uint32_t* exact_id; /* device [n] */
+  const uint32_t* n_words;  /* device [n] level count per topic (emqx_topic:levels/1) */
+} emqxgm_dev_out;
+
+typedef struct emqxgm_stats {
+  uint64_t epoch;
+  uint64_t n_filters;       /* ids ever assigned */
+  uint64_t n_trie_filters;  /* committed trie members */
+  uint64_t n_route_keys;    /* committed route keys */
+  uint64_t n_nodes;         /* trie nodes (incl. root) */
+  uint64_t n_edges;
+  uint64_t edge_slots;
+  uint64_t exact_slots;
+  uint64_t device_bytes;    /* bytes of the committed device index */
+  uint32_t max_depth;       /* deepest trie filter (levels) */
+  uint32_t collisions_merged; /* trie edges merged by equal level-token hash */
+  uint64_t batches, topics, pairs, rejected_pairs, reruns;
+  double walk_ms;           /* summed walk-kernel time (HIP events), if profiling is on */
+  uint64_t walk_launches;
+  double total_ms;          /* summed device time of whole match passes, if profiling is on */
+} emqxgm_stats;
+
+int emqxgm_abi_version(void);
+int emqxgm_create(const emqxgm_cfg* cfg, emqxgm_t** out);
+void emqxgm_destroy(emqxgm_t* h);
+
+/* Index mutation (applies to the pending state; visible to match after emqxgm_commit). */
+int emqxgm_trie_insert(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t* id);
+int emqxgm_trie_delete(emqxgm_t* h, const uint8_t* filter, uint32_t len);
+int emqxgm_route_ref(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t* id);
+int emqxgm_route_unref(emqxgm_t* h, const uint8_t* filter, uint32_t len);
+/* Bulk forms: n filters packed in bytes, filter i = bytes[offsets[i] .. offsets[i+1]). */
+int emqxgm_trie_insert_many(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets,
+                            uint64_t n, uint32_t* ids /* nullable */);
+int emqxgm_route_ref_many(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets,
+                          uint64_t n, uint32_t* ids /* nullable */);
+int emqxgm_commit(emqxgm_t* h, uint64_t* epoch /* nullable */);
+/* 1 if the committed trie holds no filter, 0 otherwise (emqx_trie:empty/0). */
+int emqxgm_trie_empty(emqxgm_t* h);
+/* 1 if the committed trie holds exactly this filter key (emqx_trie:lookup_topic/2,
+ * emqx_trie.erl:267-271), 0 otherwise. */
+int emqxgm_trie_member(emqxgm_t* h, const uint8_t* filter, uint32_t len);
+
+int emqxgm_lookup_id(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t* id);
+int emqxgm_filter_bytes(emqxgm_t* h, uint32_t id, const uint8_t** p, uint32_t* len);
+
+/* Match n topics: topic i = bytes[offsets[i] .. offsets[i+1]), offsets has n+1 entries. */
+int emqxgm_match_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets, uint32_t n,
+                       emqxgm_out* out);
+/* Same, with bytes/offsets already in HBM on the handle's device; results stay in HBM.
+ * bytes_len = offsets[n] (passed so the engine never has to read it back). */
+int emqxgm_match_device(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_offsets,
+                        uint32_t n, uint64_t bytes_len, emqxgm_dev_out* out);
+
+/* Diagnostic pass (instrumented walk kernel, not the production launch): runs the device
+ * match and returns out[0] = trie states matched (SURVEY 8d S(t) summed over the batch),
+ * out[1] = edge slots loaded, out[2] = pairs, out[3] = levels (words) in the batch. */
+int emqxgm_walk_census(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_offsets,
+                       uint32_t n, uint64_t bytes_len, uint64_t out[4]);
+
+int emqxgm_set_profiling(emqxgm_t* h, int on);
+int emqxgm_get_stats(emqxgm_t* h, emqxgm_stats* st);
+/* Last HIP error string seen by the handle (for diagnostics). */
+const char* emqxgm_last_error(emqxgm_t* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EMQX_GPUMATCH_H */

@@ -1,0 +1,364 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the oracle, bit-exact.
+
+Every test here runs on a real MI355X (``-m gpu``).  Expected results come from the oracle
+(oracle/emqx_ref.py for golden/edge cases, oracle/ref_trie.cpp for the synthetic configs),
+which is itself pinned to the reference's own suites (tests/test_oracle_*.py).
+"""
+import random
+
+import numpy as np
+import pytest
+
+from oracle import emqx_ref as R
+from oracle.cref import RefIndex
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def emqx():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need the MI355X"
+    import emqx_amd
+    return emqx_amd
+
+
+def B(s):
+    return s.encode()
+
+
+def _rows_as_sets(engine, res, n):
+    return [sorted(engine.filter_bytes(int(f)) for f in res.row(i)) for i in range(n)]
+
+
+def _assert_engine_equals_ref(eng, ref, names, tbytes, toff):
+    """Compare engine CSR rows (ids) with the C++ oracle (same registration order)."""
+    res = eng.match_packed(tbytes, toff)
+    row, ids, ex = ref.match(tbytes, toff, threads=16)
+    assert len(res.row_ptr) == len(row)
+    n = len(row) - 1
+    # rows as sorted id lists; ids are equal because both registered filters in the same order
+    g_sorted = np.concatenate([np.sort(res.filter_id[res.row_ptr[i]:res.row_ptr[i + 1]])
+                               for i in range(n)]) if n else np.zeros(0, np.uint32)
+    assert np.array_equal(res.row_ptr, row)
+    assert np.array_equal(g_sorted, ids)
+    assert np.array_equal(res.exact_id, ex)
+    return res
+
+
+# ---------------------------------------------------------------- reference suites on device
+
+@pytest.mark.parametrize("compact", [True, False])
+def test_trie_suite_on_device(emqx, golden, compact):
+    for case, steps in golden["trie_cases"].items():
+        trie = emqx.Trie()
+        trie.set_compact(compact)
+        for step in steps:
+            op = step[0]
+            if op == "insert":
+                with trie.transaction():
+                    for f in step[1]:
+                        trie.insert(B(f))
+            elif op == "delete":
+                with trie.transaction():
+                    for f in step[1]:
+                        trie.delete(B(f))
+            elif op == "match":
+                assert sorted(trie.match(B(step[1]))) == [B(x) for x in step[2]], (case, step)
+            elif op == "match_len":
+                assert len(trie.match(B(step[1]))) == step[2], (case, step)
+            elif op == "empty":
+                assert trie.empty() is step[1], (case, step)
+            elif op == "lookup_topic":
+                assert trie.lookup_topic(B(step[1])) == [B(x) for x in step[2]], (case, step)
+        trie.engine.close()
+
+
+def test_router_suite_on_device(emqx, golden):
+    for case, steps in golden["router_cases"].items():
+        r = emqx.Router()
+        for step in steps:
+            if step[0] == "add_route":
+                for f, d in step[1]:
+                    r.add_route(B(f), d)
+            elif step[0] == "delete_route":
+                for f, d in step[1]:
+                    r.delete_route(B(f), d)
+            elif step[0] == "match_routes":
+                assert sorted(r.match_routes(B(step[1]))) == sorted(
+                    (B(f), d) for f, d in step[2]), (case, step)
+
+
+def test_match_vectors_as_single_filter_tries(emqx, golden):
+    """Every emqx_topic:match/2 vector, asked as: does a trie holding only F return F for N."""
+    cases = golden["match"] + golden["client_dollar"]
+    eng = emqx.Engine()
+    for name, filt, exp in cases:
+        if not R.wildcard(B(filt)):
+            continue  # exact filters are route keys, not trie members (emqx_router.erl:131-137)
+        eng.trie_insert(B(filt))
+    eng.commit()
+    topics = [B(n) for n, _, _ in cases]
+    res = eng.match(topics)
+    for i, (name, filt, exp) in enumerate(cases):
+        if not R.wildcard(B(filt)):
+            continue
+        got = eng.filter_bytes(eng.lookup_id(B(filt))) in {eng.filter_bytes(int(f)) for f in res.row(i)}
+        assert got is exp, (name, filt)
+
+
+def test_client_matrix(emqx, golden):
+    topics = [B(t) for t in golden["client_topics"]] + [B(golden["client_dollar"][0][0])]
+    wild = [B(w) for w in golden["client_wild"]]
+    t = emqx.Trie()
+    with t.transaction():
+        for w in wild:
+            t.insert(w)
+    got = t.match_batch(topics)
+    for i, topic in enumerate(topics):
+        assert sorted(got[i]) == sorted(w for w in wild if R.match(topic, w)), topic
+
+
+# ---------------------------------------------------------------- cfg5 edge semantics
+
+EDGE_FILTERS = ["$SYS/#", "$SYS/+", "+/#", "#", "+", "/+", "/#", "+/+", "$share/g/#", "$share/g/x",
+                "a/+", "a/#", "a//+", "+//b", "+/", "/", "a/+/#", "$x", "sport/+", "#/x",
+                "a/#/b", "++", "a/b+", "$SYS", "+/+/+/+/+/+/+/+/+/+/+/+/+/+/+/+/+/+/+/+/+/+/+/+/+/+/#",
+                "a/+/c/+/e/+/g/+/i/+/k/+/m/+/o/+/q/+/s/+/u/+/w/+/y/+/#"]
+EDGE_TOPICS = ["$share/g/x", "$SYS", "$SYS/a", "", "/", "//", "a//b", "/a", "a/", "a", "a/b",
+               "$x", "sport/", "sport", "a/+", "#", "+", "$SYS/+",
+               "a/b/c/d/e/f/g/h/i/j/k/l/m/n/o/p/q/r/s/t/u/v/w/x/y/z",
+               "/".join(str(i) for i in range(32)), "/".join("w" for _ in range(128)),
+               "/".join("w" for _ in range(129)), "x" * 65535]
+
+
+def _edge_engine(emqx, **kw):
+    eng = emqx.Engine(**kw)
+    filters = [B(f) for f in EDGE_FILTERS]
+    for f in filters:
+        eng.trie_insert(f)
+        eng.route_ref(f)
+    for f in (b"a/b", b"a//b", b"", b"x" * 65535, b"$share/g/x"):
+        eng.route_ref(f)
+    eng.trie_insert(b"a/b")  # non-wildcard key inserted straight into the trie (t_insert style)
+    eng.commit()
+    return eng, filters
+
+
+def _expected_edge(filters, topics):
+    py = R.Trie()
+    for f in filters + [b"a/b"]:
+        py.insert(f)
+    return [sorted(py.match(t)) for t in topics]
+
+
+@pytest.mark.parametrize("bits", [(32, 64), (2, 3), (1, 1)])
+def test_edge_semantics(emqx, bits):
+    eng, filters = _edge_engine(emqx, word_hash_bits=bits[0], full_hash_bits=bits[1])
+    topics = [B(t) for t in EDGE_TOPICS]
+    res = eng.match(topics)
+    exp = _expected_edge(filters, topics)
+    keys = set(filters) | {b"a/b", b"a//b", b"", b"x" * 65535, b"$share/g/x"}
+    for i, t in enumerate(topics):
+        got = sorted(eng.filter_bytes(int(f)) for f in res.row(i))
+        assert got == exp[i], (t[:40], got, exp[i])
+        ex = int(res.exact_id[i])
+        if t in keys:
+            assert ex != emqx.NONE and eng.filter_bytes(ex) == t  # match_routes exact lookup
+        else:
+            assert ex == emqx.NONE
+
+
+def test_wildcard_topic_routes_exact_only(emqx):
+    r = emqx.Router()
+    r.add_route(b"a/+")
+    r.add_route(b"a/#")
+    r.add_route(b"a/b")
+    assert r.match_routes(b"a/+") == [(b"a/+", "node")]  # emqx_router.erl:143 exact key only
+    assert sorted(r.match_routes(b"a/b")) == [(b"a/#", "node"), (b"a/+", "node"),
+                                               (b"a/b", "node")]
+
+
+def test_empty_batch_and_empty_index(emqx):
+    eng = emqx.Engine()
+    res = eng.match([])
+    assert list(res.row_ptr) == [0] and res.filter_id.size == 0
+    res = eng.match([b"a/b", b""])
+    assert list(res.row_ptr) == [0, 0, 0] and list(res.exact_id) == [emqx.NONE] * 2
+    eng.route_ref(b"a/b")
+    eng.commit()
+    res = eng.match([b"a/b", b""])
+    assert list(res.row_ptr) == [0, 0, 0] and res.exact_id[0] != emqx.NONE
+
+
+def test_commit_epochs_and_delete(emqx):
+    t = emqx.Trie()
+    with t.transaction():
+        for f in (b"sensor/+", b"sensor/+/metric/2", b"sensor/#"):
+            t.insert(f)
+    assert sorted(t.match(b"sensor/1")) == [b"sensor/#", b"sensor/+"]
+    e0 = t.engine.commit()
+    t.delete(b"sensor/+")  # pending until commit: the committed epoch still answers
+    assert sorted(t.engine.filter_bytes(int(f)) for f in t.engine.match([b"sensor/1"]).row(0)) == \
+        [b"sensor/#", b"sensor/+"]
+    assert t.engine.commit() == e0 + 1
+    assert t.match(b"sensor/1") == [b"sensor/#"]
+    t.delete(b"never/inserted")
+    assert t.match(b"sensor/1") == [b"sensor/#"]
+
+
+def test_many_matches_vs_oracle(emqx):
+    eng = emqx.Engine()
+    filters = [f"+/{i}/#".encode() for i in range(600)] + [f"+/{i}/+".encode() for i in range(600)]
+    filters += [b"#", b"+/#", b"+/+/#"]
+    for f in filters:
+        eng.trie_insert(f)
+    eng.commit()
+    topics = [f"t{j}/{j % 600}/z".encode() for j in range(4000)]
+    topics += [f"t{j}/{j % 7}".encode() for j in range(3000)]
+    res = eng.match(topics)
+    ref = RefIndex(True)
+    from emqx_amd.engine import pack
+    fb, fo = pack(filters)
+    ref.add_many(fb, fo, np.ones(len(filters), np.uint8))
+    tb, to = pack(topics, np.uint32)
+    row, ids, _ = ref.match(tb, to, threads=8)
+    assert np.array_equal(res.row_ptr, row)
+    for i in range(len(topics)):
+        assert sorted(res.row(i)) == list(ids[row[i]:row[i + 1]])
+
+
+def test_staging_overflow_rerun_and_deep_stack(emqx):
+    """Filters {a,+}^k/# for k <= 10: a 12-level topic a/a/.../a matches all 2047 of them, the
+    walk frontier doubles per level (stack deeper than the 8 LDS entries -> HBM spill) and
+    600 topics stage 1.2M pairs > the initial capacity max(1Mi, 4n) -> overflow re-run."""
+    import itertools
+    eng = emqx.Engine()
+    filters = []
+    for k in range(11):
+        for combo in itertools.product(["a", "+"], repeat=k):
+            filters.append(("/".join(list(combo) + ["#"])).encode())
+    for f in filters:
+        eng.trie_insert(f)
+    eng.commit()
+    topics = [b"/".join([b"a"] * 12)] * 600 + [b"/".join([b"a"] * 5 + [b"b"])] * 10
+    res = eng.match(topics)
+    assert eng.stats()["reruns"] >= 1
+    py = R.Trie()
+    for f in filters:
+        py.insert(f)
+    exp0 = sorted(py.match(topics[0]))
+    exp1 = sorted(py.match(topics[-1]))
+    assert len(exp0) == 2047
+    for i, t in enumerate(topics):
+        got = sorted(eng.filter_bytes(int(f)) for f in res.row(i))
+        assert got == (exp0 if i < 600 else exp1)
+
+
+# ---------------------------------------------------------------- synthetic configs vs oracle
+
+def _load_both(emqx, w, **kw):
+    eng = emqx.Engine(**kw)
+    wild = w.fwild.astype(bool)
+    idx = np.arange(w.nf)
+    # register in input order so that ids coincide with the oracle's first-registration ids
+    eng.route_ref_many(w.fbytes, w.foff)
+    wi = idx[wild]
+    if wi.size:
+        sub_off = np.zeros(wi.size + 1, np.uint64)
+        lens = (w.foff[wi + 1] - w.foff[wi]).astype(np.uint64)
+        np.cumsum(lens, out=sub_off[1:])
+        sub = np.concatenate([w.fbytes[w.foff[i]:w.foff[i + 1]] for i in wi]) if wi.size < 200000 \
+            else _gather(w, wi)
+        eng.trie_insert_many(sub, sub_off)
+    eng.commit()
+    ref = RefIndex(True)
+    ref.add_many(w.fbytes, w.foff, (2 + wild.astype(np.uint8)))
+    return eng, ref
+
+
+def _gather(w, wi):
+    lens = (w.foff[wi + 1] - w.foff[wi]).astype(np.int64)
+    starts = w.foff[wi].astype(np.int64)
+    pos = np.repeat(starts - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(lens.sum())
+    return w.fbytes[pos]
+
+
+def test_cfg1_full(emqx):
+    import workloads
+    w = workloads.generate(1)
+    eng, ref = _load_both(emqx, w)
+    _assert_engine_equals_ref(eng, ref, None, w.tbytes, w.toff)
+
+
+def test_cfg2_full(emqx):
+    import workloads
+    w = workloads.generate(2)
+    eng, ref = _load_both(emqx, w)
+    res = _assert_engine_equals_ref(eng, ref, None, w.tbytes, w.toff)
+    assert int(res.row_ptr[-1]) > 0 and (res.exact_id != emqx.NONE).any()
+
+
+def test_cfg3_sample_at_1m_filters(emqx):
+    import workloads
+    w = workloads.generate(3, 1_000_000, 200_000)
+    eng, ref = _load_both(emqx, w)
+    _assert_engine_equals_ref(eng, ref, None, w.tbytes, w.toff)
+
+
+@pytest.mark.parametrize("bits", [(4, 6), (8, 16)])
+def test_cfg2_slice_forced_collisions(emqx, bits):
+    """Few level-token hash bits: massive edge merging and exact-table collisions; the
+    string-pool verification must restore the exact reference result."""
+    import workloads
+    w = workloads.generate(2, 20_000, 20_000)
+    eng, ref = _load_both(emqx, w, word_hash_bits=bits[0], full_hash_bits=bits[1])
+    _assert_engine_equals_ref(eng, ref, None, w.tbytes, w.toff)
+
+
+def test_random_fuzz_against_python_oracle(emqx):
+    rng = random.Random(5)
+    vocab = ["a", "b", "", "$x", "c", "dd"]
+    filters = set()
+    while len(filters) < 500:
+        d = rng.randint(1, 6)
+        ws = []
+        for i in range(d):
+            r = rng.random()
+            ws.append("#" if (i == d - 1 and r < 0.15) else ("+" if r < 0.4 else rng.choice(vocab)))
+        filters.add("/".join(ws).encode())
+    filters = sorted(filters)
+    topics = ["/".join(rng.choice(vocab) for _ in range(rng.randint(1, 7))).encode()
+              for _ in range(3000)]
+    for bits in (32, 3):
+        eng = emqx.Engine(word_hash_bits=bits)
+        py = R.Trie()
+        for f in filters:
+            eng.trie_insert(f)
+            py.insert(f)
+        eng.commit()
+        res = eng.match(topics)
+        for i, t in enumerate(topics):
+            assert sorted(eng.filter_bytes(int(f)) for f in res.row(i)) == sorted(py.match(t)), t
+
+
+def test_device_api_matches_host_api(emqx):
+    import torch
+    import workloads
+    w = workloads.generate(1, 5000, 20000)
+    eng, _ = _load_both(emqx, w)
+    host = eng.match_packed(w.tbytes, w.toff)
+    db = torch.from_numpy(w.tbytes).cuda()
+    do = torch.from_numpy(w.toff.view(np.int32)).cuda()
+    torch.cuda.synchronize()
+    d = eng.match_device(db.data_ptr(), do.data_ptr(), w.nt, int(w.toff[-1]))
+    assert d.n_pairs == int(host.row_ptr[-1])
+    import ctypes
+    row = np.empty(w.nt + 1, np.uint32)
+    fid = np.empty(d.n_pairs, np.uint32)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    assert hip.hipMemcpy(row.ctypes.data, d.row_ptr, row.nbytes, 2) == 0
+    assert hip.hipMemcpy(fid.ctypes.data, d.filter_id, fid.nbytes, 2) == 0
+    assert np.array_equal(row.astype(np.uint64), host.row_ptr)
+    assert np.array_equal(fid, host.filter_id)

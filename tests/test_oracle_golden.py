@@ -1,0 +1,221 @@
+"""Pins the CPU oracle (oracle/emqx_ref.py) to the reference's own asserted vectors.
+
+CPU only.  Each table in tests/golden/reference_vectors.json cites the reference suite it was
+transcribed from (tests/golden/make_golden.py)."""
+import itertools
+import random
+
+import pytest
+
+from oracle import emqx_ref as R
+
+
+def B(s):
+    return s.encode()
+
+
+def W(x):
+    if isinstance(x, dict) and "atom" in x:
+        return x["atom"]
+    if isinstance(x, dict) and "words_of" in x:
+        return R.words(B(x["words_of"]))
+    return B(x)
+
+
+def test_match_vectors(golden):
+    for name, filt, exp in golden["match"]:
+        assert R.match(B(name), B(filt)) is exp, (name, filt)
+
+
+def test_wildcard_words_tokens_levels(golden):
+    for t, exp in golden["wildcard"]:
+        assert R.wildcard(B(t)) is exp
+    for t, exp in golden["words"]:
+        assert R.words(B(t)) == [W(x) for x in exp]
+    for t, exp in golden["tokens"]:
+        assert R.tokens(B(t)) == [B(x) for x in exp]
+    for t, exp in golden["levels"]:
+        assert R.levels(B(t)) == exp
+
+
+def test_join(golden):
+    for ws, exp in golden["join"]:
+        ws = W(ws) if isinstance(ws, dict) else [W(x) for x in ws]
+        assert R.join(ws) == B(exp)
+
+
+def test_validate(golden):
+    long_topic = b"".join(str(i).encode() + b"/" for i in range(0, 66667))
+    for kind, topic, exp in golden["validate"]:
+        t = long_topic if isinstance(topic, dict) else B(topic)
+        if exp is True:
+            assert R.validate((kind, t)) is True
+        else:
+            with pytest.raises(R.TopicError) as ei:
+                R.validate((kind, t))
+            assert ei.value.args[0] == exp
+
+
+def test_prepend_parse(golden):
+    for parent, w, exp in golden["prepend"]:
+        p = None if parent is None else W(parent)
+        assert R.prepend(p, B(w)) == B(exp)
+    for inp, opts, exp in golden["parse"]:
+        o = {k: (B(v) if isinstance(v, str) else v) for k, v in opts.items()}
+        if isinstance(exp, dict):
+            with pytest.raises(R.TopicError):
+                R.parse(B(inp), o)
+        else:
+            topic, eo = R.parse(B(inp), o)
+            assert topic == B(exp[0])
+            assert eo == {k: (B(v) if isinstance(v, str) else v) for k, v in exp[1].items()}
+
+
+def test_trie_key_layout(golden):
+    for compact, filt, tk, prefixes in golden["make_keys"]:
+        t = R.Trie(compact)
+        assert t.make_keys(B(filt)) == ((B(tk), 1), [(B(p), 0) for p in prefixes])
+    for compact, filt, prefixes in golden["make_prefixes"]:
+        assert R.Trie(compact).make_prefixes(R.words(B(filt))) == [B(p) for p in prefixes]
+    for filt, segs in golden["do_compact"]:
+        assert R.do_compact(R.words(B(filt))) == [B(s) for s in segs]
+
+
+@pytest.mark.parametrize("compact", [True, False])
+def test_trie_suite(golden, compact):
+    for case, steps in golden["trie_cases"].items():
+        t = R.Trie(compact)
+        for step in steps:
+            op = step[0]
+            if op == "insert":
+                for f in step[1]:
+                    t.insert(B(f))
+            elif op == "delete":
+                for f in step[1]:
+                    t.delete(B(f))
+            elif op == "match":
+                assert sorted(t.match(B(step[1]))) == [B(x) for x in step[2]], (case, step)
+            elif op == "match_len":
+                assert len(t.match(B(step[1]))) == step[2], (case, step)
+            elif op == "empty":
+                assert t.empty() is step[1], (case, step)
+            elif op == "lookup_topic":
+                assert t.lookup_topic(B(step[1])) == [B(x) for x in step[2]], (case, step)
+
+
+def test_router_suite(golden):
+    for case, steps in golden["router_cases"].items():
+        r = R.Router()
+        for step in steps:
+            op = step[0]
+            if op == "add_route":
+                for f, d in step[1]:
+                    r.add_route(B(f), d)
+            elif op == "delete_route":
+                for f, d in step[1]:
+                    r.delete_route(B(f), d)
+            elif op == "match_routes":
+                got = sorted(r.match_routes(B(step[1])))
+                assert got == sorted((B(f), d) for f, d in step[2]), (case, step)
+
+
+def test_client_matrix(golden):
+    topics = [B(t) for t in golden["client_topics"]]
+    wild = [B(w) for w in golden["client_wild"]]
+    tr = R.Trie()
+    for w in wild:
+        tr.insert(w)
+    for t in topics:
+        assert sorted(tr.match(t)) == sorted(w for w in wild if R.match(t, w))
+    for name, filt, exp in golden["client_dollar"]:
+        assert R.match(B(name), B(filt)) is exp
+        t2 = R.Trie()
+        t2.insert(B(filt))
+        assert (B(filt) in t2.match(B(name))) is exp
+
+
+def test_bench_pattern_one_route(golden):
+    """emqx_broker_bench: sub_ptn rendered per id/num, each publisher topic has 1 route."""
+    bp = golden["bench_patterns"]
+    r = R.Router()
+    subs, sub_ops = 8, 50
+    for i in range(1, subs + 1):
+        for n in range(1, sub_ops + 1):
+            r.add_route(B(bp["sub_ptn"].replace("{{id}}", str(i)).replace("{{num}}", str(n))))
+    for i in range(1, subs + 1):
+        topic = B(bp["pub_ptn"].replace("{{id}}", str(i)).replace("{{num}}", "1"))
+        assert len(r.match_routes(topic)) == bp["expect_routes_per_lookup"]
+
+
+# --- the two independent restatements agree (SURVEY 8c "Golden vectors") ----------------
+
+def _rand_filters(rng, vocab, n, depth):
+    out = set()
+    while len(out) < n:
+        d = rng.randint(1, depth)
+        ws = []
+        for i in range(d):
+            r = rng.random()
+            if i == d - 1 and r < 0.15:
+                ws.append("#")
+            elif r < 0.35:
+                ws.append("+")
+            else:
+                ws.append(rng.choice(vocab))
+        out.add(B("/".join(ws)))
+    return sorted(out)
+
+
+def _rand_topics(rng, vocab, n, depth):
+    out = []
+    for _ in range(n):
+        d = rng.randint(1, depth)
+        ws = [rng.choice(vocab) for _ in range(d)]
+        if rng.random() < 0.1:
+            ws[0] = "$SYS"
+        out.append(B("/".join(ws)))
+    return out
+
+
+@pytest.mark.parametrize("compact", [True, False])
+def test_trie_walk_equals_bruteforce(compact):
+    rng = random.Random(7)
+    vocab = ["a", "b", "c", "", "$x", "dd"]
+    filters = _rand_filters(rng, vocab, 400, 5)
+    topics = _rand_topics(rng, vocab, 600, 6) + [b"", b"/", b"//", b"a//b", b"/a", b"a/",
+                                                 b"$SYS", b"$x", b"a/+", b"#"]
+    t = R.Trie(compact)
+    for f in filters:
+        t.insert(f)
+    for topic in topics:
+        got = t.match(topic)
+        assert len(got) == len(set(got)), topic  # no duplicates
+        assert sorted(got) == sorted(R.trie_match_bruteforce(topic, filters, [
+            f for f in filters if not R.wildcard(f)])), topic
+
+
+def test_trie_delete_restores_state():
+    rng = random.Random(3)
+    vocab = ["a", "b", "", "c"]
+    filters = _rand_filters(rng, vocab, 120, 4)
+    for compact in (True, False):
+        t = R.Trie(compact)
+        for f in filters:
+            t.insert(f)
+            t.insert(f)  # idempotent
+        keep = filters[::2]
+        for f in filters[1::2]:
+            t.delete(f)
+            t.delete(f)  # no-op
+        ref = R.Trie(compact)
+        for f in keep:
+            ref.insert(f)
+        assert t.tab == ref.tab
+
+
+def test_aggre():
+    routes = [(b"a", "n1"), (b"b", ("g", "n1")), (b"b", ("g", "n2"))]
+    assert R.aggre([]) == []
+    assert R.aggre([(b"a", "n1")]) == [(b"a", "n1")]
+    assert R.aggre([(b"a", ("g", "n1"))]) == [(b"a", "g")]
+    assert R.aggre(routes) == [(b"a", "n1"), (b"b", "g")]
