@@ -116,8 +116,10 @@ struct emqxgm {
   DevIndex ix;
   std::vector<DevBuf> ix_bufs;
   uint64_t pool_uploaded = 0;  // bytes of pool already on device
-  DevBuf d_pool, d_foff;
-  uint64_t foff_uploaded = 0;
+  DevBuf d_pool, d_foff, d_fver;
+  uint64_t foff_uploaded = 0, fver_uploaded = 0;  // bytes
+  std::vector<uint64_t> foff_host;  // [n_filters+1]
+  std::vector<uint8_t> fver_host;   // 64 B per filter
   emqxgm_stats st{};
 
   // ---- batch scratch ----
@@ -134,6 +136,7 @@ struct emqxgm {
 
   bool profiling = false;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  uint32_t reject_cap = 1u << 20;  // cfg.reserved[0] overrides (tests force the legacy path)
 };
 
 namespace {
@@ -241,14 +244,33 @@ struct ListBuild {
   }
 };
 
+// Grow-and-append a device mirror of an append-only host array (bytes [uploaded, total)).
+int append_upload(emqxgm* h, DevBuf& buf, uint64_t& uploaded, const void* src, uint64_t total) {
+  const uint64_t need = std::max<uint64_t>(16, total);
+  if (need > buf.bytes) {
+    DevBuf nb;
+    nb.bytes = std::max<uint64_t>(need, buf.bytes * 2);
+    HIPCHK(h, hipMalloc(&nb.p, nb.bytes));
+    if (uploaded) HIPCHK(h, hipMemcpy(nb.p, buf.p, uploaded, hipMemcpyDeviceToDevice));
+    if (buf.p) (void)hipFree(buf.p);
+    buf = nb;
+  }
+  if (total > uploaded)
+    HIPCHK(h, hipMemcpy((uint8_t*)buf.p + uploaded, (const uint8_t*)src + uploaded,
+                        total - uploaded, hipMemcpyHostToDevice));
+  uploaded = total;
+  return 0;
+}
+
 // Build the device index from the pending registry and swap it in.
 int commit_locked(emqxgm* h) {
-  const uint32_t wmask =
-      h->cfg.word_hash_bits >= 32 ? 0xFFFFFFFFu : ((1u << h->cfg.word_hash_bits) - 1u);
+  const uint64_t wmask = h->cfg.word_hash_bits >= WH_BITS
+                             ? WH_MASK
+                             : ((1ull << h->cfg.word_hash_bits) - 1ull);
   const uint64_t fmask =
       h->cfg.full_hash_bits >= 64 ? ~0ull : ((1ull << h->cfg.full_hash_bits) - 1ull);
 
-  // ---- trie: nodes keyed by (parent, level-token hash); root = node 0 ----
+  // ---- trie: nodes keyed by (parent, level token); root = node 0 ----
   std::vector<uint32_t> nflags(1, 0), nhf(1, NONE), ntw(1, NONE), ntn(1, NONE);
   U64Map emap;
   emap.init(std::max<uint64_t>(1024, h->n_trie_pending * 2));
@@ -257,7 +279,7 @@ int commit_locked(emqxgm* h) {
   edges.reserve(h->n_trie_pending * 2 + 16);
   uint32_t max_depth = 0;
   uint64_t n_trie = 0;
-  std::vector<uint32_t> whs;
+  std::vector<uint64_t> whs;
   std::vector<uint8_t> is_plus, is_hash;
   for (uint32_t id = 0; id < h->filters.size(); ++id) {
     const Filter& f = h->filters[id];
@@ -293,8 +315,8 @@ int commit_locked(emqxgm* h) {
       uint32_t* v = emap.get_or_insert(tag, ins);
       if (ins) {
         const uint32_t child = (uint32_t)nflags.size();
-        if (child > CF_ID_MASK) {
-          h->err = "trie exceeds 2^27 nodes";
+        if (child >= MAX_NODES) {
+          h->err = "trie exceeds 2^27-1 nodes";
           return -E2BIG;
         }
         *v = child;
@@ -331,11 +353,8 @@ int commit_locked(emqxgm* h) {
     return LIST_MULTI | list_pos[v & ~LIST_MULTI];
   };
   const size_t n_nodes = nflags.size();
-  std::vector<uint32_t> node_tw(n_nodes), node_tn(n_nodes);
   std::vector<uint32_t> cfv(n_nodes), hfv(n_nodes);
   for (size_t i = 0; i < n_nodes; ++i) {
-    node_tw[i] = resolve(ntw[i]);
-    node_tn[i] = resolve(ntn[i]);
     uint32_t hf = resolve(nhf[i]);
     uint32_t flags = nflags[i];
     if (hf != NONE && (hf & LIST_MULTI)) {
@@ -345,13 +364,16 @@ int commit_locked(emqxgm* h) {
     cfv[i] = (uint32_t)i | flags;
     hfv[i] = hf;
   }
+  // 32-B slots: {tag, cf, hf} {tw, tn, 0, 0}; load factor <= 1/2
   const uint64_t ecap = pow2_at_least(std::max<uint64_t>(64, edges.size() * 2));
-  std::vector<uint4> eslots(ecap, make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, NONE));
+  std::vector<uint4> eslots(2 * ecap, make_uint4(0u, 0u, 0u, 0u));
+  for (uint64_t i = 0; i < ecap; ++i) eslots[2 * i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, NONE);
   for (const auto& e : edges) {
     uint64_t i = edge_slot(e.first, ecap - 1);
-    while (eslots[i].x != 0xFFFFFFFFu || eslots[i].y != 0xFFFFFFFFu) i = (i + 1) & (ecap - 1);
-    eslots[i] = make_uint4((uint32_t)e.first, (uint32_t)(e.first >> 32), cfv[e.second],
-                           hfv[e.second]);
+    while (eslots[2 * i].x != 0xFFFFFFFFu || eslots[2 * i].y != 0xFFFFFFFFu) i = (i + 1) & (ecap - 1);
+    eslots[2 * i] = make_uint4((uint32_t)e.first, (uint32_t)(e.first >> 32), cfv[e.second],
+                               hfv[e.second]);
+    eslots[2 * i + 1] = make_uint4(resolve(ntw[e.second]), resolve(ntn[e.second]), 0u, 0u);
   }
 
   // ---- exact route keys ----
@@ -371,51 +393,31 @@ int commit_locked(emqxgm* h) {
     xslots[i] = make_uint4((uint32_t)fh, (uint32_t)(fh >> 32), id, f.len);
   }
 
-  // ---- filter string pool (append-only on the device) ----
+  // ---- filter string pool, offsets and 64-B verification records (append-only) ----
   if (hipSetDevice(h->cfg.device) != hipSuccess) return fail(h, hipErrorInvalidDevice, "hipSetDevice");
-  const uint64_t need_pool = std::max<uint64_t>(1, h->pool.size());
-  if (need_pool > h->d_pool.bytes) {
-    DevBuf nb;
-    nb.bytes = std::max<uint64_t>(need_pool, h->d_pool.bytes * 2);
-    HIPCHK(h, hipMalloc(&nb.p, nb.bytes));
-    if (h->pool_uploaded)
-      HIPCHK(h, hipMemcpy(nb.p, h->d_pool.p, h->pool_uploaded, hipMemcpyDeviceToDevice));
-    if (h->d_pool.p) (void)hipFree(h->d_pool.p);
-    h->d_pool = nb;
-  }
-  if (h->pool.size() > h->pool_uploaded)
-    HIPCHK(h, hipMemcpy((uint8_t*)h->d_pool.p + h->pool_uploaded, h->pool.data() + h->pool_uploaded,
-                        h->pool.size() - h->pool_uploaded, hipMemcpyHostToDevice));
-  h->pool_uploaded = h->pool.size();
   const uint64_t nf = h->filters.size();
-  const uint64_t need_off = (nf + 1) * sizeof(uint64_t);
-  if (need_off > h->d_foff.bytes) {
-    DevBuf nb;
-    nb.bytes = std::max<uint64_t>(need_off, h->d_foff.bytes * 2);
-    HIPCHK(h, hipMalloc(&nb.p, nb.bytes));
-    if (h->foff_uploaded)
-      HIPCHK(h, hipMemcpy(nb.p, h->d_foff.p, h->foff_uploaded * sizeof(uint64_t),
-                          hipMemcpyDeviceToDevice));
-    if (h->d_foff.p) (void)hipFree(h->d_foff.p);
-    h->d_foff = nb;
+  if (h->foff_host.empty()) h->foff_host.push_back(0);
+  for (uint64_t i = h->foff_host.size() - 1; i < nf; ++i)  // pool is append-only
+    h->foff_host.push_back(h->filters[i].off + h->filters[i].len);
+  for (uint64_t i = h->fver_host.size() / VREC; i < nf; ++i) {
+    const Filter& f = h->filters[i];
+    uint8_t r[VREC] = {0};
+    memcpy(r, &f.len, 4);
+    memcpy(r + 4, h->pool.data() + f.off, std::min<uint32_t>(f.len, VINL));
+    h->fver_host.insert(h->fver_host.end(), r, r + VREC);
   }
-  if (nf + 1 > h->foff_uploaded) {
-    std::vector<uint64_t> offs;
-    const uint64_t from = h->foff_uploaded ? h->foff_uploaded - 1 : 0;
-    for (uint64_t i = from; i <= nf; ++i)
-      offs.push_back(i < nf ? h->filters[i].off : (uint64_t)h->pool.size());
-    HIPCHK(h, hipMemcpy((uint64_t*)h->d_foff.p + from, offs.data(), offs.size() * sizeof(uint64_t),
-                        hipMemcpyHostToDevice));
-    h->foff_uploaded = nf + 1;
-  }
+  int rc = 0;
+  if ((rc = append_upload(h, h->d_pool, h->pool_uploaded, h->pool.data(), h->pool.size())) ||
+      (rc = append_upload(h, h->d_foff, h->foff_uploaded, h->foff_host.data(),
+                          h->foff_host.size() * sizeof(uint64_t))) ||
+      (rc = append_upload(h, h->d_fver, h->fver_uploaded, h->fver_host.data(),
+                          h->fver_host.size())))
+    return rc;
 
   // ---- upload and swap ----
   std::vector<DevBuf> nbufs;
   DevIndex nx;
-  int rc = 0;
   if ((rc = dev_upload(h, nbufs, eslots, &nx.edges)) ||
-      (rc = dev_upload(h, nbufs, node_tw, &nx.node_tw)) ||
-      (rc = dev_upload(h, nbufs, node_tn, &nx.node_tn)) ||
       (rc = dev_upload(h, nbufs, multi, &nx.multi)) ||
       (rc = dev_upload(h, nbufs, xslots, &nx.exact))) {
     free_bufs(nbufs);
@@ -427,6 +429,7 @@ int commit_locked(emqxgm* h) {
   nx.root_hf = hfv[0];
   nx.fbytes = (const uint8_t*)h->d_pool.p;
   nx.foff = (const uint64_t*)h->d_foff.p;
+  nx.fver = (const uint4*)h->d_fver.p;
   nx.word_mask = wmask;
   nx.full_mask = fmask;
   nx.max_depth = max_depth;
@@ -448,8 +451,8 @@ int commit_locked(emqxgm* h) {
   h->st.edge_slots = ecap;
   h->st.exact_slots = xcap;
   h->st.max_depth = max_depth;
-  h->st.device_bytes = ecap * 16 + xcap * 16 + n_nodes * 8 + multi.size() * 4 + h->pool.size() +
-                       (nf + 1) * 8;
+  h->st.device_bytes = ecap * 32 + xcap * 16 + multi.size() * 4 + h->pool.size() +
+                       (nf + 1) * 8 + nf * VREC;
   return 0;
 }
 
@@ -466,7 +469,7 @@ int dev_alloc(emqxgm* h, void** p, size_t bytes) {
 int ensure_scratch(emqxgm* h, uint32_t n, uint64_t words, uint32_t pairs) {
   Scratch& s = h->sc;
   const uint64_t spill_need =
-      (uint64_t)(h->ix.max_depth > 8 ? h->ix.max_depth - 8 + 1 : 0) * h->geom.lanes;
+      (uint64_t)(h->ix.max_depth > WALK_LDS_STACK ? h->ix.max_depth - WALK_LDS_STACK + 1 : 0) * h->geom.lanes;
   if (n <= s.n_cap && words <= s.w_cap && pairs <= s.p_cap && spill_need <= s.spill_cap &&
       s.ctl)
     return 0;
@@ -485,7 +488,7 @@ int ensure_scratch(emqxgm* h, uint32_t n, uint64_t words, uint32_t pairs) {
   const uint32_t stw = scan_tmp_words(ncap);
   if ((rc = dev_alloc(h, (void**)&s.nw, (size_t)ncap * 4)) ||
       (rc = dev_alloc(h, (void**)&s.wbase, (size_t)(ncap + 1) * 4)) ||
-      (rc = dev_alloc(h, (void**)&s.wh, (size_t)wcap * 4)) ||
+      (rc = dev_alloc(h, (void**)&s.wh, (size_t)wcap * 8)) ||
       (rc = dev_alloc(h, (void**)&s.rec, (size_t)ncap * 16)) ||
       (rc = dev_alloc(h, (void**)&s.cnt, (size_t)ncap * 4)) ||
       (rc = dev_alloc(h, (void**)&s.row, (size_t)(ncap + 1) * 4)) ||
@@ -500,8 +503,10 @@ int ensure_scratch(emqxgm* h, uint32_t n, uint64_t words, uint32_t pairs) {
       (rc = dev_alloc(h, (void**)&s.scan_tmp, (size_t)stw * 4)) ||
       (rc = dev_alloc(h, (void**)&s.ctl, CTL_N * 4)) ||
       (rc = dev_alloc(h, (void**)&s.census, 4 * sizeof(unsigned long long))) ||
-      (rc = dev_alloc(h, (void**)&s.spill, (size_t)std::max<uint64_t>(scap, 1) * 16)))
+      (rc = dev_alloc(h, (void**)&s.spill, (size_t)std::max<uint64_t>(scap, 1) * 16)) ||
+      (rc = dev_alloc(h, (void**)&s.rlist, (size_t)h->reject_cap * 8)))
     return rc;
+  s.r_cap = h->reject_cap;
   HIPCHK(h, hipHostMalloc((void**)&s.ctl_host, CTL_N * 4, hipHostMallocDefault));
   s.n_cap = ncap;
   s.w_cap = wcap;
@@ -514,6 +519,10 @@ int ensure_scratch(emqxgm* h, uint32_t n, uint64_t words, uint32_t pairs) {
 
 // One device pass over n topics already in HBM.  Leaves results in h->sc (row, out, exact_id)
 // and the total pair count in *pairs.
+//
+// Production order: tokenise -> walk -> verify (flags rejects, fixes counts) -> scan -> scatter.
+// If a batch rejected more pairs than k_scatter adjusts in-line (a weak-hash test config or an
+// adversarial index), the pass is redone on the legacy path: scan -> verify+scatter -> compaction.
 int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_t n,
                uint64_t bytes_len, uint32_t* pairs, uint64_t* census = nullptr) {
   const uint64_t words = bytes_len + n + 1;
@@ -522,45 +531,58 @@ int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_
   if (rc) return rc;
   Scratch& s = h->sc;
   hipStream_t st = h->stream;
-  if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[0], st));
-  HIPCHK(h, hipMemsetAsync(s.ctl, 0, CTL_N * 4, st));
   if (n == 0) {
     HIPCHK(h, hipMemsetAsync(s.row, 0, 4, st));
-    *pairs = 0;
     HIPCHK(h, hipStreamSynchronize(st));
+    *pairs = 0;
     return 0;
   }
+  bool legacy = false;
   for (int attempt = 0;; ++attempt) {
+    if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[0], st));
+    HIPCHK(h, hipMemsetAsync(s.ctl, 0, CTL_N * 4, st));
     if (census) HIPCHK(h, hipMemsetAsync(s.census, 0, 4 * sizeof(unsigned long long), st));
     HIPCHK(h, launch_tok_count(d_bytes, d_off, n, s.nw, st));
     HIPCHK(h, launch_scan(s.nw, s.wbase, n, s.scan_tmp, s.ctl + CTL_WORDS, st));
     HIPCHK(h, launch_tok_hash(d_bytes, d_off, n, h->ix, s, st));
     if (h->ix.trie_empty) {
       HIPCHK(h, hipMemsetAsync(s.row, 0, (size_t)(n + 1) * 4, st));
-      HIPCHK(h, hipMemsetAsync(s.ctl + CTL_TOTAL, 0, 4, st));
     } else {
       HIPCHK(h, hipMemsetAsync(s.rej, 0, (size_t)n * 4, st));
       if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[1], st));
       HIPCHK(h, launch_walk(h->ix, s, n, h->geom, st, census ? s.census : nullptr));
       if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[2], st));
-      HIPCHK(h, launch_scan(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, st));
-      HIPCHK(h, launch_verify_scatter(d_bytes, d_off, h->ix, s, n, st));
+      if (!legacy) {
+        HIPCHK(h, launch_verify(d_bytes, d_off, h->ix, s, n, h->geom, st));
+        HIPCHK(h, launch_scan(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, st));
+        HIPCHK(h, launch_scatter(s, n, h->geom, st));
+      } else {
+        HIPCHK(h, launch_scan(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, st));
+        HIPCHK(h, launch_verify_scatter(d_bytes, d_off, h->ix, s, n, st));
+      }
     }
     if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[3], st));
     HIPCHK(h, hipMemcpyAsync(s.ctl_host, s.ctl, CTL_N * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipStreamSynchronize(st));
-    const uint32_t top = s.ctl_host[CTL_PAIR_TOP];
-    if (top <= s.p_cap) break;
-    // staging overflow: nothing beyond the capacity was written; grow and redo the pass
-    h->st.reruns += 1;
-    if (attempt > 4) {
-      h->err = "pair staging overflow did not converge";
+    if (attempt > 6) {
+      h->err = "match pass did not converge";
       return -ENOMEM;
     }
-    const uint64_t np = std::min<uint64_t>(0xF0000000ull, (uint64_t)top * 2 + (1u << 20));
-    rc = ensure_scratch(h, n, words, (uint32_t)np);
-    if (rc) return rc;
-    HIPCHK(h, hipMemsetAsync(s.ctl, 0, CTL_N * 4, st));
+    const uint32_t top = s.ctl_host[CTL_PAIR_TOP];
+    if (top > s.p_cap) {
+      // staging overflow: nothing beyond the capacity was written; grow and redo the pass
+      h->st.reruns += 1;
+      const uint64_t np = std::min<uint64_t>(0xF0000000ull, (uint64_t)top * 2 + (1u << 20));
+      rc = ensure_scratch(h, n, words, (uint32_t)np);
+      if (rc) return rc;
+      continue;
+    }
+    if (!legacy && s.ctl_host[CTL_LEGACY]) {
+      h->st.reruns += 1;
+      legacy = true;
+      continue;
+    }
+    break;
   }
   if (h->profiling) {
     float a = 0, b = 0;
@@ -572,14 +594,15 @@ int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_
     HIPCHK(h, hipEventElapsedTime(&b, h->ev[0], h->ev[3]));
     h->st.total_ms += b;
   }
-  if (s.ctl_host[CTL_ANY_REJ]) {
+  if (legacy && s.ctl_host[CTL_ANY_REJ]) {
     HIPCHK(h, launch_fixup(s, n, st));
     HIPCHK(h, hipMemcpyAsync(s.ctl_host + CTL_TOTAL, s.ctl + CTL_TOTAL, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(h, hipStreamSynchronize(st));
     std::swap(s.row, s.row2);
     std::swap(s.out, s.out2);
-    h->st.rejected_pairs += 1;  // batches that needed the fix-up pass
   }
+  if (s.ctl_host[CTL_ANY_REJ]) h->st.rejected_pairs += legacy ? 0 : s.ctl_host[CTL_NREJ];
+  if (legacy) h->st.legacy_batches += 1;
   *pairs = s.ctl_host[CTL_TOTAL];
   if (census) {
     unsigned long long c[4] = {0, 0, 0, 0};
@@ -625,9 +648,10 @@ int emqxgm_create(const emqxgm_cfg* cfg, emqxgm_t** out) {
   emqxgm* h = new (std::nothrow) emqxgm();
   if (!h) return -ENOMEM;
   if (cfg) h->cfg = *cfg;
-  if (h->cfg.word_hash_bits == 0 || h->cfg.word_hash_bits > 32) h->cfg.word_hash_bits = 32;
+  if (h->cfg.word_hash_bits == 0 || h->cfg.word_hash_bits > WH_BITS) h->cfg.word_hash_bits = WH_BITS;
   if (h->cfg.full_hash_bits == 0 || h->cfg.full_hash_bits > 64) h->cfg.full_hash_bits = 64;
   if (h->cfg.batch_max == 0) h->cfg.batch_max = 4u << 20;
+  if (h->cfg.reject_cap) h->reject_cap = h->cfg.reject_cap;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || h->cfg.device < 0 ||
       h->cfg.device >= ndev) {
@@ -663,6 +687,7 @@ void emqxgm_destroy(emqxgm_t* h) {
   if (h->sc.ctl_host) (void)hipHostFree(h->sc.ctl_host);
   if (h->d_pool.p) (void)hipFree(h->d_pool.p);
   if (h->d_foff.p) (void)hipFree(h->d_foff.p);
+  if (h->d_fver.p) (void)hipFree(h->d_fver.p);
   if (h->d_in_bytes) (void)hipFree(h->d_in_bytes);
   if (h->d_in_off) (void)hipFree(h->d_in_off);
   for (auto& e : h->ev)

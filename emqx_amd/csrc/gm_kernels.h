@@ -7,17 +7,16 @@ namespace gm {
 
 // Committed device index (all pointers are device memory).
 struct DevIndex {
-  const uint4* edges = nullptr;   // edge slots {tag.lo, tag.hi, cf, hf}
-  uint64_t emask = 0;             // edge capacity - 1
-  const uint32_t* node_tw = nullptr;
-  const uint32_t* node_tn = nullptr;
+  const uint4* edges = nullptr;   // 2 x uint4 per slot (gm_common.h "Edge slot")
+  uint64_t emask = 0;             // slot capacity - 1
   const uint32_t* multi = nullptr;  // [count, fid...] lists
   uint32_t root_cf = 0, root_hf = 0xFFFFFFFFu;
   const uint4* exact = nullptr;   // exact slots {hash.lo, hash.hi, fid, len}
   uint64_t xmask = 0;
   const uint8_t* fbytes = nullptr;  // filter string pool
   const uint64_t* foff = nullptr;   // [n_filters+1]
-  uint32_t word_mask = 0xFFFFFFFFu;
+  const uint4* fver = nullptr;      // 64-B verification record per filter id
+  uint64_t word_mask = 0;
   uint64_t full_mask = ~0ull;
   uint32_t max_depth = 0;           // deepest trie filter in levels
   bool trie_empty = true;
@@ -30,25 +29,27 @@ struct Scratch {
   uint64_t w_cap = 0;  // word capacity
   uint32_t* nw = nullptr;     // [n]   words per topic
   uint32_t* wbase = nullptr;  // [n+1]
-  uint32_t* wh = nullptr;     // [w]   level-token hashes
-  uint4* rec = nullptr;       // [n]   {wbase, n_words, flags, wh0}
+  uint64_t* wh = nullptr;     // [w]   level tokens
+  uint4* rec = nullptr;       // [n]   {wbase, n_words, flags|tok0_hi<<8, tok0_lo}
   uint32_t* cnt = nullptr;    // [n]   trie matches per topic
   uint32_t* row = nullptr;    // [n+1]
-  uint32_t* row2 = nullptr;   // [n+1] (fix-up)
+  uint32_t* row2 = nullptr;   // [n+1] (legacy fix-up)
   uint32_t* rej = nullptr;    // [n]   rejected pairs per topic
   uint32_t* exact_id = nullptr;  // [n]
   uint32_t p_cap = 0;   // pair staging capacity
   uint32_t* pt = nullptr;     // staged pair: topic
   uint32_t* pf = nullptr;     // staged pair: filter
-  uint32_t* pr = nullptr;     // staged pair: rank within topic
+  uint32_t* pr = nullptr;     // staged pair: rank within topic (bit 31 = rejected)
   uint32_t o_cap = 0;
   uint32_t* out = nullptr;    // [pairs] CSR filter ids
-  uint32_t* out2 = nullptr;   // fix-up target
+  uint32_t* out2 = nullptr;   // legacy fix-up target
   uint32_t* scan_tmp = nullptr;  // scan partials
   uint32_t scan_tmp_cap = 0;
   uint32_t* ctl = nullptr;    // control words (see CTL_*)
   uint4* spill = nullptr;     // walk stack spill (depth beyond LDS)
   uint64_t spill_cap = 0;     // entries
+  uint2* rlist = nullptr;     // rejected (topic, rank) list
+  uint32_t r_cap = 0;
   uint32_t* ctl_host = nullptr;  // pinned host mirror of ctl
   unsigned long long* census = nullptr;  // [4] diagnostic walk counters
 };
@@ -59,12 +60,19 @@ enum : int {
   CTL_ANY_REJ = 2,    // a verification rejected some pair
   CTL_TOTAL = 3,      // total pairs (row[n]) copied here
   CTL_WORDS = 4,      // total words
+  CTL_NREJ = 5,       // rejected pairs appended to rlist
+  CTL_LEGACY = 6,     // deferred scatter could not place rejects: re-run with the fix-up path
   CTL_N = 8
 };
+
+constexpr uint32_t REJ_BIT = 0x80000000u;
+constexpr uint32_t REJ_SCAN_MAX = 4096;  // rejects the deferred scatter handles in-line
+constexpr uint32_t WALK_LDS_STACK = 4;   // walk stack entries per lane kept in LDS (rest spill)
 
 struct WalkGeom {
   uint32_t blocks = 0;      // persistent workgroups
   uint32_t lanes = 0;       // blocks * 256
+  uint32_t cus = 0;
 };
 
 WalkGeom walk_geometry(int device, uint32_t wg_per_cu);
@@ -80,8 +88,13 @@ hipError_t launch_tok_hash(const uint8_t* bytes, const uint32_t* off, uint32_t n
 // census != nullptr selects the diagnostic walk that adds {states, slot loads} to census[0..1]
 hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGeom& g,
                        hipStream_t s, unsigned long long* census = nullptr);
+// production: verify (flags + counts) -> [scan] -> deferred scatter
+hipError_t launch_verify(const uint8_t* bytes, const uint32_t* off, const DevIndex& ix,
+                         Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_t s);
+hipError_t launch_scatter(Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_t s);
+// legacy path (reject list overflow): scan -> verify+scatter -> compaction
 hipError_t launch_verify_scatter(const uint8_t* bytes, const uint32_t* off, const DevIndex& ix,
                                  Scratch& sc, uint32_t n, hipStream_t s);
-hipError_t launch_fixup(Scratch& sc, uint32_t n, hipStream_t s);  // after CTL_ANY_REJ
+hipError_t launch_fixup(Scratch& sc, uint32_t n, hipStream_t s);
 
 }  // namespace gm

@@ -26,7 +26,8 @@ class EngineError(RuntimeError):
 class _Cfg(C.Structure):
     _fields_ = [("device", C.c_int32), ("word_hash_bits", C.c_uint32),
                 ("full_hash_bits", C.c_uint32), ("batch_max", C.c_uint32),
-                ("walk_wg_per_cu", C.c_uint32), ("reserved", C.c_uint32 * 3)]
+                ("walk_wg_per_cu", C.c_uint32), ("reject_cap", C.c_uint32),
+                ("reserved", C.c_uint32 * 2)]
 
 
 class _Out(C.Structure):
@@ -45,7 +46,7 @@ class _Stats(C.Structure):
                 ("n_route_keys", C.c_uint64), ("n_nodes", C.c_uint64), ("n_edges", C.c_uint64),
                 ("edge_slots", C.c_uint64), ("exact_slots", C.c_uint64),
                 ("device_bytes", C.c_uint64), ("max_depth", C.c_uint32),
-                ("collisions_merged", C.c_uint32), ("batches", C.c_uint64),
+                ("legacy_batches", C.c_uint32), ("batches", C.c_uint64),
                 ("topics", C.c_uint64), ("pairs", C.c_uint64), ("rejected_pairs", C.c_uint64),
                 ("reruns", C.c_uint64), ("walk_ms", C.c_double), ("walk_launches", C.c_uint64),
                 ("total_ms", C.c_double)]
@@ -70,7 +71,7 @@ SYMBOLS = {
     "emqxgm_trie_empty": (C.c_int, [_P]),
     "emqxgm_trie_member": (C.c_int, [_P, C.c_char_p, C.c_uint32]),
     "emqxgm_lookup_id": (C.c_int, [_P, C.c_char_p, C.c_uint32, _U32P]),
-    "emqxgm_filter_bytes": (C.c_int, [_P, C.POINTER(_U8P), _U32P]),
+    "emqxgm_filter_bytes": (C.c_int, [_P, C.c_uint32, C.POINTER(_U8P), _U32P]),
     "emqxgm_match_batch": (C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(_Out)]),
     "emqxgm_match_device": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, C.POINTER(_DevOut)]),
     "emqxgm_walk_census": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, _U64P]),
@@ -142,10 +143,10 @@ class DeviceResult:
 class Engine:
     """One engine instance = one device index (one emqx_trie + route-key set) on one GPU."""
 
-    def __init__(self, device: int = 0, word_hash_bits: int = 32, full_hash_bits: int = 64,
-                 batch_max: int = 0, walk_wg_per_cu: int = 0):
+    def __init__(self, device: int = 0, word_hash_bits: int = 0, full_hash_bits: int = 64,
+                 batch_max: int = 0, walk_wg_per_cu: int = 0, reject_cap: int = 0):
         self._lib = lib()
-        cfg = _Cfg(device, word_hash_bits, full_hash_bits, batch_max, walk_wg_per_cu)
+        cfg = _Cfg(device, word_hash_bits, full_hash_bits, batch_max, walk_wg_per_cu, reject_cap)
         h = C.c_void_p()
         rc = self._lib.emqxgm_create(C.byref(cfg), C.byref(h))
         if rc != 0:

@@ -56,12 +56,14 @@ typedef struct emqxgm emqxgm_t;
 
 typedef struct emqxgm_cfg {
   int32_t device;          /* HIP device ordinal */
-  uint32_t word_hash_bits; /* bits kept of each 32-bit level-token hash; 32 in production,
+  uint32_t word_hash_bits; /* bits kept of each 37-bit level token (0 = 37, production);
                               small values only to force collisions in tests */
   uint32_t full_hash_bits; /* bits kept of the 64-bit whole-topic hash (exact table); 64 */
   uint32_t batch_max;      /* topics per device pass of emqxgm_match_batch (0 = 4Mi) */
   uint32_t walk_wg_per_cu; /* persistent walk workgroups per CU (0 = default) */
-  uint32_t reserved[3];
+  uint32_t reject_cap;     /* verification rejects handled in-line per batch (0 = 1Mi);
+                              beyond it a batch is redone on the compaction path */
+  uint32_t reserved[2];
 } emqxgm_cfg;
 
 typedef struct emqxgm_out { /* host-resident result of emqxgm_match_batch */
@@ -92,8 +94,10 @@ typedef struct emqxgm_stats {
   uint64_t exact_slots;
   uint64_t device_bytes;    /* bytes of the committed device index */
   uint32_t max_depth;       /* deepest trie filter (levels) */
-  uint32_t collisions_merged; /* trie edges merged by equal level-token hash */
-  uint64_t batches, topics, pairs, rejected_pairs, reruns;
+  uint32_t legacy_batches;  /* batches redone on the compaction path (many rejects) */
+  uint64_t batches, topics, pairs;
+  uint64_t rejected_pairs;  /* staged pairs rejected by byte verification (hash collisions) */
+  uint64_t reruns;          /* passes redone (staging growth or legacy path) */
   double walk_ms;           /* summed walk-kernel time (HIP events), if profiling is on */
   uint64_t walk_launches;
   double total_ms;          /* summed device time of whole match passes, if profiling is on */

@@ -306,14 +306,20 @@ def test_cfg3_sample_at_1m_filters(emqx):
     _assert_engine_equals_ref(eng, ref, None, w.tbytes, w.toff)
 
 
-@pytest.mark.parametrize("bits", [(4, 6), (8, 16)])
+@pytest.mark.parametrize("bits", [(4, 6, 0), (8, 16, 0), (12, 16, 0), (4, 6, 16)])
 def test_cfg2_slice_forced_collisions(emqx, bits):
     """Few level-token hash bits: massive edge merging and exact-table collisions; the
-    string-pool verification must restore the exact reference result."""
+    verification must restore the exact reference result -- on the in-line path (k_scatter's
+    rank adjustment) and, with a tiny reject capacity, on the legacy compaction path."""
     import workloads
     w = workloads.generate(2, 20_000, 20_000)
-    eng, ref = _load_both(emqx, w, word_hash_bits=bits[0], full_hash_bits=bits[1])
+    eng, ref = _load_both(emqx, w, word_hash_bits=bits[0], full_hash_bits=bits[1],
+                          reject_cap=bits[2])
     _assert_engine_equals_ref(eng, ref, None, w.tbytes, w.toff)
+    st = eng.stats()
+    assert st["rejected_pairs"] > 0 or st["legacy_batches"] > 0
+    if bits[2]:
+        assert st["legacy_batches"] >= 1
 
 
 def test_random_fuzz_against_python_oracle(emqx):
