@@ -22,7 +22,8 @@ ORACLE_SO = os.path.join(ROOT, "oracle", "build", "libemqx_ref.so")
 WORKLOAD_SO = os.path.join(ROOT, "workloads", "libemqx_workload.so")
 
 ENGINE_SRCS = ["gm_kernels.hip", "gm_engine.cpp"]
-ENGINE_DEPS = ENGINE_SRCS + ["gm_common.h", "gm_kernels.h"]
+ENGINE_DEPS = ENGINE_SRCS + ["gm_common.h", "gm_kernels.h", "gm_tok.inc", "gm_walk.inc",
+                              "gm_verify.inc"]
 
 
 def _hipcc() -> str:

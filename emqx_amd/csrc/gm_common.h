@@ -1,5 +1,5 @@
-// gm_common.h -- layout constants and hash functions shared by the host index builder and
-// the gfx950 kernels.  The device index layout is described in DESIGN.md "Data layout".
+// gm_common.h -- layout constants and token/hash functions shared by the host index builder
+// and the gfx950 kernels.  The device index layout is described in DESIGN.md "Data layout".
 #pragma once
 #include <stdint.h>
 
@@ -13,37 +13,15 @@ namespace gm {
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 
-// Level tokens are 37-bit hashes of one topic level; the all-ones token is reserved for '+'.
-constexpr uint32_t WH_BITS = 37;
-constexpr uint64_t WH_MASK = (1ull << WH_BITS) - 1;
-constexpr uint64_t PLUS_WH = WH_MASK;
-constexpr uint64_t EMPTY_TAG = ~0ull;  // parent id 2^27-1 is never assigned
-
-// Edge slot (32 B = 2 x uint4):
-//   a = {tag.lo, tag.hi, cf, hf}, b = {tw, tn, 0, 0}
-//   tag = (parent_node << 37) | level_token        (exact key on (parent, token))
-//   cf  = child node id (27 bits) | child flags (5 bits)
-//   hf  = filter id of "child_path/#", NONE, or (CF_HFM) index into the multi[] list pool
-//   tw  = wildcard filter(s) ending exactly at the child (fid, or LIST_MULTI|multi index)
-//   tn  = non-wildcard trie key(s) ending at the child (same encoding)
-constexpr uint32_t CF_ID_BITS = 27;
-constexpr uint32_t CF_ID_MASK = (1u << CF_ID_BITS) - 1;
-constexpr uint32_t MAX_NODES = CF_ID_MASK;  // ids 0 .. 2^27-2
-constexpr uint32_t CF_LIT = 1u << 27;   // child has literal (non-'+') children
-constexpr uint32_t CF_PLUS = 1u << 28;  // child has a '+' child
-constexpr uint32_t CF_HFM = 1u << 29;   // hf is a multi[] index
-constexpr uint32_t CF_TW = 1u << 30;    // child terminates >=1 wildcard filter
-constexpr uint32_t CF_TN = 1u << 31;    // child terminates >=1 non-wildcard trie key
-constexpr uint32_t LIST_MULTI = 0x80000000u;  // tw/tn value is a multi[] index
-
-// Filter verification record (64 B per filter id): {u32 len, 60 bytes of the filter}; the
-// bytes of longer filters are read from the string pool.
-constexpr uint32_t VREC = 64;
-constexpr uint32_t VINL = 60;
-
-// Per-topic record written by the tokenizer (uint4): {wbase, n_words, flags|tok0_hi<<8, tok0_lo}
-constexpr uint32_t T_WILD = 1u;    // some level is exactly '+' or '#'  -> trie result []
-constexpr uint32_t T_DOLLAR = 2u;  // first byte is '$' -> no root '+'/'#' (emqx_trie.erl:282)
+// ---- level tokens ---------------------------------------------------------------------
+// A level token identifies one topic level (emqx_topic:words/1 element).  A word of at most
+// 7 bytes is packed injectively: bytes little-endian in bits 0..55, length in bits 56..62,
+// bit 63 clear -- two different short words can never share a token, so trie edges over
+// short words are exact.  A longer word gets bit 63 set and a 63-bit hash; only filters with
+// such a word need the byte verification pass.  '+' has a token no word can have.
+constexpr uint64_t TOK_HASHED = 1ull << 63;
+constexpr uint64_t PLUS_TOK = 0x7FFFFFFFFFFFFFFFull;  // length field 127: impossible for a word
+constexpr uint32_t TOK_INLINE_MAX = 7;
 
 constexpr uint64_t FNV_OFF = 0xcbf29ce484222325ull;
 constexpr uint64_t FNV_PRIME = 0x100000001b3ull;
@@ -59,20 +37,52 @@ GM_HD uint64_t fmix64(uint64_t k) {
 
 GM_HD uint64_t fnv_step(uint64_t h, uint32_t b) { return (h ^ b) * FNV_PRIME; }
 
-// Level token of one word (from its FNV-1a state after the word's bytes); `mask` keeps
-// WH_BITS bits in production and fewer only to force collisions in tests.
-GM_HD uint64_t word_hash(uint64_t fnv_state, uint64_t mask) {
-  const uint64_t h = fmix64(fnv_state) & mask;
-  return h == PLUS_WH ? PLUS_WH - 1 : h;
+// Token of a finished word: `packed` = its first bytes little-endian, `fnv` = FNV-1a state
+// over all its bytes, `len` = its length.  `test_mask` != 0 selects the collision-test mode in
+// which every word is hashed and only the masked bits of the hash are kept.
+GM_HD uint64_t word_token(uint64_t packed, uint64_t fnv, uint32_t len, uint64_t test_mask) {
+  if (test_mask) return TOK_HASHED | (fmix64(fnv) & test_mask);
+  if (len <= TOK_INLINE_MAX) return packed | ((uint64_t)len << 56);
+  return TOK_HASHED | (fmix64(fnv) >> 1);
 }
 
-// Whole-topic hash (exact route table key).
-GM_HD uint64_t full_hash(uint64_t fnv_state, uint64_t mask) {
-  return fmix64(fnv_state ^ 0x9e3779b97f4a7c15ull) & mask;
+// Whole-topic hash (exact route-key table), folded over the level tokens in order.
+GM_HD uint64_t topic_hash_step(uint64_t h, uint64_t tok) { return fmix64(h ^ tok) + FNV_PRIME; }
+GM_HD uint64_t topic_hash_final(uint64_t h, uint32_t n, uint64_t mask) {
+  return fmix64(h ^ ((uint64_t)n * 0x9e3779b97f4a7c15ull)) & mask;
 }
 
-GM_HD uint64_t edge_tag(uint32_t parent, uint64_t wh) { return ((uint64_t)parent << WH_BITS) | wh; }
-GM_HD uint64_t edge_slot(uint64_t tag, uint64_t mask) { return fmix64(tag * 0x9e3779b97f4a7c15ull) & mask; }
+// ---- edge slots -------------------------------------------------------------------------
+// 32 B per slot, 2 x uint4:  a = {tok.lo, tok.hi, parent, cf}   b = {hf, tw, tn, 0}
+//   key = (parent node id, level token), exact
+//   cf  = child node id (27 bits) | child flags (5 bits)
+//   hf  = filter id of "child_path/#", NONE, or (CF_HFM) index into the multi[] list pool
+//   tw  = wildcard filter(s) ending exactly at the child (fid, or LIST_MULTI|multi index)
+//   tn  = non-wildcard trie key(s) ending at the child (same encoding)
+// An empty slot has parent == NONE.
+constexpr uint32_t CF_ID_BITS = 27;
+constexpr uint32_t CF_ID_MASK = (1u << CF_ID_BITS) - 1;
+constexpr uint32_t MAX_NODES = CF_ID_MASK;
+constexpr uint32_t CF_LIT = 1u << 27;   // child has literal (non-'+') children
+constexpr uint32_t CF_PLUS = 1u << 28;  // child has a '+' child
+constexpr uint32_t CF_HFM = 1u << 29;   // hf is a multi[] index
+constexpr uint32_t CF_TW = 1u << 30;    // child terminates >=1 wildcard filter
+constexpr uint32_t CF_TN = 1u << 31;    // child terminates >=1 non-wildcard trie key
+constexpr uint32_t LIST_MULTI = 0x80000000u;  // tw/tn value is a multi[] index
+
+GM_HD uint64_t edge_slot(uint32_t parent, uint64_t tok, uint64_t mask) {
+  return fmix64(tok ^ ((uint64_t)parent * 0x9e3779b97f4a7c15ull)) & mask;
+}
 GM_HD uint64_t exact_slot(uint64_t fh, uint64_t mask) { return fmix64(fh + 0x632be59bd9b4e019ull) & mask; }
+
+// Filter verification record (64 B per filter id): {u32 len, 60 bytes of the filter}; the
+// bytes of longer filters are read from the string pool.
+constexpr uint32_t VREC = 64;
+constexpr uint32_t VINL = 60;
+
+// Per-topic record written by the tokenizer (uint4): {wbase, n_words | flags << 24, tok0.lo,
+// tok0.hi}; topics have at most 32,768 levels (65,535 bytes).
+constexpr uint32_t T_WILD = 1u;    // some level is exactly '+' or '#'  -> trie result []
+constexpr uint32_t T_DOLLAR = 2u;  // first byte is '$' -> no root '+'/'#' (emqx_trie.erl:282)
 
 }  // namespace gm

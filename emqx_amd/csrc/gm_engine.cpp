@@ -32,54 +32,82 @@ uint64_t pow2_at_least(uint64_t x) {
   return p;
 }
 
-// Open-addressing map u64 -> u32 (keys never equal ~0).
-struct U64Map {
-  std::vector<uint64_t> keys;
-  std::vector<uint32_t> vals;
+// Open-addressing map (parent node, level token) -> child node (host-side trie builder).
+struct EdgeMap {
+  struct Ent {
+    uint64_t tok;
+    uint32_t parent;  // NONE = empty
+    uint32_t child;
+  };
+  std::vector<Ent> ents;
   uint64_t mask = 0, used = 0;
   void init(uint64_t expect) {
     const uint64_t cap = pow2_at_least(std::max<uint64_t>(16, expect * 2));
-    keys.assign(cap, ~0ull);
-    vals.assign(cap, 0);
+    ents.assign(cap, Ent{0, NONE, 0});
     mask = cap - 1;
     used = 0;
   }
   void grow() {
-    std::vector<uint64_t> ok;
-    std::vector<uint32_t> ov;
-    ok.swap(keys);
-    ov.swap(vals);
-    const uint64_t cap = (mask + 1) * 2;
-    keys.assign(cap, ~0ull);
-    vals.assign(cap, 0);
-    mask = cap - 1;
+    std::vector<Ent> old;
+    old.swap(ents);
+    ents.assign(old.size() * 2, Ent{0, NONE, 0});
+    mask = ents.size() - 1;
     used = 0;
-    for (size_t i = 0; i < ok.size(); ++i)
-      if (ok[i] != ~0ull) put(ok[i], ov[i]);
+    bool ins;
+    for (const Ent& e : old)
+      if (e.parent != NONE) *get_or_insert(e.parent, e.tok, ins) = e.child;
   }
-  // returns pointer to value; inserted=true if new
-  uint32_t* get_or_insert(uint64_t k, bool& inserted) {
+  // returns pointer to the child slot; inserted=true if new
+  uint32_t* get_or_insert(uint32_t parent, uint64_t tok, bool& inserted) {
     if ((used + 1) * 2 > mask + 1) grow();
-    uint64_t i = fmix64(k) & mask;
+    uint64_t i = edge_slot(parent, tok, mask);
     for (;;) {
-      if (keys[i] == k) {
+      Ent& e = ents[i];
+      if (e.parent == parent && e.tok == tok) {
         inserted = false;
-        return &vals[i];
+        return &e.child;
       }
-      if (keys[i] == ~0ull) {
-        keys[i] = k;
+      if (e.parent == NONE) {
+        e.parent = parent;
+        e.tok = tok;
         ++used;
         inserted = true;
-        return &vals[i];
+        return &e.child;
       }
       i = (i + 1) & mask;
     }
   }
-  void put(uint64_t k, uint32_t v) {
-    bool ins;
-    *get_or_insert(k, ins) = v;
-  }
 };
+
+// Level tokens of a filter/topic string, exactly as the device tokenizer computes them.
+// is_plus/is_hash flag words that are exactly '+' / '#'; `hashed` = some literal word got a
+// hashed token (its trie pairs need byte verification).
+void tokenize(const uint8_t* p, uint32_t len, uint64_t test_mask, std::vector<uint64_t>& toks,
+              std::vector<uint8_t>& is_plus, std::vector<uint8_t>& is_hash, bool& hashed) {
+  toks.clear();
+  is_plus.clear();
+  is_hash.clear();
+  hashed = false;
+  uint32_t s = 0;
+  for (uint32_t i = 0; i <= len; ++i) {
+    if (i == len || p[i] == '/') {
+      const uint32_t wl = i - s;
+      uint64_t packed = 0, fnv = FNV_OFF;
+      for (uint32_t q = 0; q < wl; ++q) {
+        if (q < 8) packed |= (uint64_t)p[s + q] << (8 * q);
+        fnv = fnv_step(fnv, p[s + q]);
+      }
+      const bool pl = (wl == 1 && p[s] == '+');
+      const bool hs = (wl == 1 && p[s] == '#');
+      const uint64_t tok = word_token(packed, fnv, wl, test_mask);
+      toks.push_back(tok);
+      is_plus.push_back(pl);
+      is_hash.push_back(hs);
+      if (!pl && !hs && (tok & TOK_HASHED)) hashed = true;
+      s = i + 1;
+    }
+  }
+}
 
 struct Filter {
   uint64_t off;
@@ -136,7 +164,8 @@ struct emqxgm {
 
   bool profiling = false;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  uint32_t reject_cap = 1u << 20;  // cfg.reserved[0] overrides (tests force the legacy path)
+  uint32_t reject_cap = 1u << 20;  // cfg.reject_cap overrides (tests force the legacy path)
+  uint64_t test_mask = 0;          // != 0: collision-test tokens (cfg.word_hash_bits)
 };
 
 namespace {
@@ -264,55 +293,46 @@ int append_upload(emqxgm* h, DevBuf& buf, uint64_t& uploaded, const void* src, u
 
 // Build the device index from the pending registry and swap it in.
 int commit_locked(emqxgm* h) {
-  const uint64_t wmask = h->cfg.word_hash_bits >= WH_BITS
-                             ? WH_MASK
-                             : ((1ull << h->cfg.word_hash_bits) - 1ull);
+  const uint64_t test_mask = h->test_mask;
   const uint64_t fmask =
       h->cfg.full_hash_bits >= 64 ? ~0ull : ((1ull << h->cfg.full_hash_bits) - 1ull);
+  const uint64_t nf = h->filters.size();
 
   // ---- trie: nodes keyed by (parent, level token); root = node 0 ----
   std::vector<uint32_t> nflags(1, 0), nhf(1, NONE), ntw(1, NONE), ntn(1, NONE);
-  U64Map emap;
+  EdgeMap emap;
   emap.init(std::max<uint64_t>(1024, h->n_trie_pending * 2));
   ListBuild lb;
-  std::vector<std::pair<uint64_t, uint32_t>> edges;  // (tag, child)
+  struct Edge {
+    uint64_t tok;
+    uint32_t parent, child;
+  };
+  std::vector<Edge> edges;
   edges.reserve(h->n_trie_pending * 2 + 16);
+  std::vector<uint32_t> fvbits((nf + 31) / 32 + 1, 0u);
+  bool needs_verify = false;
   uint32_t max_depth = 0;
   uint64_t n_trie = 0;
-  std::vector<uint64_t> whs;
+  std::vector<uint64_t> toks;
   std::vector<uint8_t> is_plus, is_hash;
   for (uint32_t id = 0; id < h->filters.size(); ++id) {
     const Filter& f = h->filters[id];
     if (!f.in_trie) continue;
     ++n_trie;
-    const uint8_t* p = h->pool.data() + f.off;
-    whs.clear();
-    is_plus.clear();
-    is_hash.clear();
-    uint64_t hw = FNV_OFF;
-    uint32_t s = 0;
-    for (uint32_t i = 0; i <= f.len; ++i) {
-      if (i == f.len || p[i] == '/') {
-        const uint32_t wl = i - s;
-        const bool pl = (wl == 1 && p[s] == '+');
-        const bool hs = (wl == 1 && p[s] == '#');
-        whs.push_back(pl ? PLUS_WH : word_hash(hw, wmask));
-        is_plus.push_back(pl);
-        is_hash.push_back(hs);
-        hw = FNV_OFF;
-        s = i + 1;
-      } else {
-        hw = fnv_step(hw, p[i]);
-      }
+    bool hashed;
+    tokenize(h->pool.data() + f.off, f.len, test_mask, toks, is_plus, is_hash, hashed);
+    if (hashed) {
+      fvbits[id >> 5] |= 1u << (id & 31);
+      needs_verify = true;
     }
-    const size_t nw = whs.size();
+    const size_t nw = toks.size();
     const bool hash_last = is_hash[nw - 1];
     const size_t path_len = hash_last ? nw - 1 : nw;  // '#' last: attach to the parent node
     uint32_t cur = 0;
     for (size_t w = 0; w < path_len; ++w) {
-      const uint64_t tag = edge_tag(cur, whs[w]);
+      const uint64_t tok = is_plus[w] ? PLUS_TOK : toks[w];
       bool ins;
-      uint32_t* v = emap.get_or_insert(tag, ins);
+      uint32_t* v = emap.get_or_insert(cur, tok, ins);
       if (ins) {
         const uint32_t child = (uint32_t)nflags.size();
         if (child >= MAX_NODES) {
@@ -324,7 +344,7 @@ int commit_locked(emqxgm* h) {
         nhf.push_back(NONE);
         ntw.push_back(NONE);
         ntn.push_back(NONE);
-        edges.emplace_back(tag, child);
+        edges.push_back(Edge{tok, cur, child});
         nflags[cur] |= is_plus[w] ? CF_PLUS : CF_LIT;
       }
       cur = *v;
@@ -364,16 +384,15 @@ int commit_locked(emqxgm* h) {
     cfv[i] = (uint32_t)i | flags;
     hfv[i] = hf;
   }
-  // 32-B slots: {tag, cf, hf} {tw, tn, 0, 0}; load factor <= 1/2
+  // 32-B slots: {tok.lo, tok.hi, parent, cf} {hf, tw, tn, 0}; load factor <= 1/2
   const uint64_t ecap = pow2_at_least(std::max<uint64_t>(64, edges.size() * 2));
   std::vector<uint4> eslots(2 * ecap, make_uint4(0u, 0u, 0u, 0u));
-  for (uint64_t i = 0; i < ecap; ++i) eslots[2 * i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, NONE);
-  for (const auto& e : edges) {
-    uint64_t i = edge_slot(e.first, ecap - 1);
-    while (eslots[2 * i].x != 0xFFFFFFFFu || eslots[2 * i].y != 0xFFFFFFFFu) i = (i + 1) & (ecap - 1);
-    eslots[2 * i] = make_uint4((uint32_t)e.first, (uint32_t)(e.first >> 32), cfv[e.second],
-                               hfv[e.second]);
-    eslots[2 * i + 1] = make_uint4(resolve(ntw[e.second]), resolve(ntn[e.second]), 0u, 0u);
+  for (uint64_t i = 0; i < ecap; ++i) eslots[2 * i] = make_uint4(0u, 0u, NONE, 0u);
+  for (const Edge& e : edges) {
+    uint64_t i = edge_slot(e.parent, e.tok, ecap - 1);
+    while (eslots[2 * i].z != NONE) i = (i + 1) & (ecap - 1);
+    eslots[2 * i] = make_uint4((uint32_t)e.tok, (uint32_t)(e.tok >> 32), e.parent, cfv[e.child]);
+    eslots[2 * i + 1] = make_uint4(hfv[e.child], resolve(ntw[e.child]), resolve(ntn[e.child]), 0u);
   }
 
   // ---- exact route keys ----
@@ -384,10 +403,11 @@ int commit_locked(emqxgm* h) {
   for (uint32_t id = 0; id < h->filters.size(); ++id) {
     const Filter& f = h->filters[id];
     if (!f.route_refs) continue;
+    bool hashed;
+    tokenize(h->pool.data() + f.off, f.len, test_mask, toks, is_plus, is_hash, hashed);
     uint64_t x = FNV_OFF;
-    const uint8_t* p = h->pool.data() + f.off;
-    for (uint32_t i = 0; i < f.len; ++i) x = fnv_step(x, p[i]);
-    const uint64_t fh = full_hash(x, fmask);
+    for (uint64_t tk : toks) x = topic_hash_step(x, tk);
+    const uint64_t fh = topic_hash_final(x, (uint32_t)toks.size(), fmask);
     uint64_t i = exact_slot(fh, xcap - 1);
     while (xslots[i].z != NONE) i = (i + 1) & (xcap - 1);
     xslots[i] = make_uint4((uint32_t)fh, (uint32_t)(fh >> 32), id, f.len);
@@ -395,7 +415,6 @@ int commit_locked(emqxgm* h) {
 
   // ---- filter string pool, offsets and 64-B verification records (append-only) ----
   if (hipSetDevice(h->cfg.device) != hipSuccess) return fail(h, hipErrorInvalidDevice, "hipSetDevice");
-  const uint64_t nf = h->filters.size();
   if (h->foff_host.empty()) h->foff_host.push_back(0);
   for (uint64_t i = h->foff_host.size() - 1; i < nf; ++i)  // pool is append-only
     h->foff_host.push_back(h->filters[i].off + h->filters[i].len);
@@ -419,6 +438,7 @@ int commit_locked(emqxgm* h) {
   DevIndex nx;
   if ((rc = dev_upload(h, nbufs, eslots, &nx.edges)) ||
       (rc = dev_upload(h, nbufs, multi, &nx.multi)) ||
+      (rc = dev_upload(h, nbufs, fvbits, &nx.fvbits)) ||
       (rc = dev_upload(h, nbufs, xslots, &nx.exact))) {
     free_bufs(nbufs);
     return rc;
@@ -430,7 +450,8 @@ int commit_locked(emqxgm* h) {
   nx.fbytes = (const uint8_t*)h->d_pool.p;
   nx.foff = (const uint64_t*)h->d_foff.p;
   nx.fver = (const uint4*)h->d_fver.p;
-  nx.word_mask = wmask;
+  nx.test_mask = test_mask;
+  nx.needs_verify = needs_verify;
   nx.full_mask = fmask;
   nx.max_depth = max_depth;
   nx.trie_empty = (n_trie == 0);
@@ -553,7 +574,8 @@ int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_
       HIPCHK(h, launch_walk(h->ix, s, n, h->geom, st, census ? s.census : nullptr));
       if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[2], st));
       if (!legacy) {
-        HIPCHK(h, launch_verify(d_bytes, d_off, h->ix, s, n, h->geom, st));
+        // pairs of filters made of short (exact) tokens need no byte check (gm_verify.inc)
+        if (h->ix.needs_verify) HIPCHK(h, launch_verify(d_bytes, d_off, h->ix, s, n, h->geom, st));
         HIPCHK(h, launch_scan(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, st));
         HIPCHK(h, launch_scatter(s, n, h->geom, st));
       } else {
@@ -648,7 +670,10 @@ int emqxgm_create(const emqxgm_cfg* cfg, emqxgm_t** out) {
   emqxgm* h = new (std::nothrow) emqxgm();
   if (!h) return -ENOMEM;
   if (cfg) h->cfg = *cfg;
-  if (h->cfg.word_hash_bits == 0 || h->cfg.word_hash_bits > WH_BITS) h->cfg.word_hash_bits = WH_BITS;
+  // word_hash_bits 0 (or >= 63): production tokens (short words exact, long words hashed);
+  // 1..62: collision-test mode, every word hashed and masked to that many bits
+  if (h->cfg.word_hash_bits >= 63) h->cfg.word_hash_bits = 0;
+  h->test_mask = h->cfg.word_hash_bits ? ((1ull << h->cfg.word_hash_bits) - 1ull) : 0ull;
   if (h->cfg.full_hash_bits == 0 || h->cfg.full_hash_bits > 64) h->cfg.full_hash_bits = 64;
   if (h->cfg.batch_max == 0) h->cfg.batch_max = 4u << 20;
   if (h->cfg.reject_cap) h->reject_cap = h->cfg.reject_cap;
@@ -908,6 +933,18 @@ int emqxgm_set_profiling(emqxgm_t* h, int on) {
   std::lock_guard<std::mutex> g(h->mu);
   h->profiling = on != 0;
   return 0;
+}
+
+int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
+  if (!h || !key) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (strcmp(key, "walk_wg_per_cu") == 0) {
+    if (value < 1 || value > 16) return -EINVAL;
+    h->cfg.walk_wg_per_cu = (uint32_t)value;
+    h->geom = walk_geometry(h->cfg.device, h->cfg.walk_wg_per_cu);
+    return 0;  // spill scratch is re-sized by the next match (ensure_scratch)
+  }
+  return -EINVAL;
 }
 
 int emqxgm_get_stats(emqxgm_t* h, emqxgm_stats* st) {

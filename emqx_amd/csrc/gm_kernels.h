@@ -7,7 +7,7 @@ namespace gm {
 
 // Committed device index (all pointers are device memory).
 struct DevIndex {
-  const uint4* edges = nullptr;   // 2 x uint4 per slot (gm_common.h "Edge slot")
+  const uint4* edges = nullptr;   // 2 x uint4 per slot (gm_common.h "edge slots")
   uint64_t emask = 0;             // slot capacity - 1
   const uint32_t* multi = nullptr;  // [count, fid...] lists
   uint32_t root_cf = 0, root_hf = 0xFFFFFFFFu;
@@ -16,11 +16,13 @@ struct DevIndex {
   const uint8_t* fbytes = nullptr;  // filter string pool
   const uint64_t* foff = nullptr;   // [n_filters+1]
   const uint4* fver = nullptr;      // 64-B verification record per filter id
-  uint64_t word_mask = 0;
+  const uint32_t* fvbits = nullptr; // bit per filter id: its trie pairs need byte verification
+  uint64_t test_mask = 0;           // != 0: collision-test tokens (every word hashed, masked)
   uint64_t full_mask = ~0ull;
   uint32_t max_depth = 0;           // deepest trie filter in levels
   bool trie_empty = true;
   bool exact_empty = true;
+  bool needs_verify = false;        // some trie filter has a hashed (long or test) token
 };
 
 // Per-batch scratch (device memory, owned by the engine, grown on demand).
@@ -30,7 +32,7 @@ struct Scratch {
   uint32_t* nw = nullptr;     // [n]   words per topic
   uint32_t* wbase = nullptr;  // [n+1]
   uint64_t* wh = nullptr;     // [w]   level tokens
-  uint4* rec = nullptr;       // [n]   {wbase, n_words, flags|tok0_hi<<8, tok0_lo}
+  uint4* rec = nullptr;       // [n]   {wbase, n_words | flags << 24, tok0.lo, tok0.hi}
   uint32_t* cnt = nullptr;    // [n]   trie matches per topic
   uint32_t* row = nullptr;    // [n+1]
   uint32_t* row2 = nullptr;   // [n+1] (legacy fix-up)

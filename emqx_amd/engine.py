@@ -76,6 +76,7 @@ SYMBOLS = {
     "emqxgm_match_device": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, C.POINTER(_DevOut)]),
     "emqxgm_walk_census": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, _U64P]),
     "emqxgm_set_profiling": (C.c_int, [_P, C.c_int]),
+    "emqxgm_tune": (C.c_int, [_P, C.c_char_p, C.c_int64]),
     "emqxgm_get_stats": (C.c_int, [_P, C.POINTER(_Stats)]),
     "emqxgm_last_error": (C.c_char_p, [_P]),
 }
@@ -260,6 +261,9 @@ class Engine:
         self._check(self._lib.emqxgm_walk_census(self._h, C.c_void_p(d_bytes), C.c_void_p(d_off),
                                                  n, bytes_len, out), "walk_census")
         return {"states": out[0], "slot_loads": out[1], "pairs": out[2], "words": out[3]}
+
+    def tune(self, key: str, value: int) -> None:
+        self._check(self._lib.emqxgm_tune(self._h, key.encode(), int(value)), f"tune({key})")
 
     def set_profiling(self, on: bool) -> None:
         self._check(self._lib.emqxgm_set_profiling(self._h, 1 if on else 0), "set_profiling")

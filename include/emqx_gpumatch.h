@@ -142,6 +142,8 @@ int emqxgm_walk_census(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_of
                        uint32_t n, uint64_t bytes_len, uint64_t out[4]);
 
 int emqxgm_set_profiling(emqxgm_t* h, int on);
+/* Runtime tuning knobs: "walk_wg_per_cu" (persistent walk workgroups per CU). */
+int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value);
 int emqxgm_get_stats(emqxgm_t* h, emqxgm_stats* st);
 /* Last HIP error string seen by the handle (for diagnostics). */
 const char* emqxgm_last_error(emqxgm_t* h);
