@@ -53,13 +53,20 @@ GM_HD uint64_t topic_hash_final(uint64_t h, uint32_t n, uint64_t mask) {
 }
 
 // ---- edge slots -------------------------------------------------------------------------
-// 32 B per slot, 2 x uint4:  a = {tok.lo, tok.hi, parent, cf}   b = {hf, tw, tn, 0}
-//   key = (parent node id, level token), exact
-//   cf  = child node id (27 bits) | child flags (5 bits)
-//   hf  = filter id of "child_path/#", NONE, or (CF_HFM) index into the multi[] list pool
-//   tw  = wildcard filter(s) ending exactly at the child (fid, or LIST_MULTI|multi index)
-//   tn  = non-wildcard trie key(s) ending at the child (same encoding)
+// 64 B per slot, 4 x uint4, one slot per trie edge (parent --level token--> child C):
+//   s0 = {tok.lo, tok.hi, parent, cf}       key = (parent node id, level token), exact
+//   s1 = {hf, tw, tn, p.cf}
+//   s2 = {p.hf, p.tw, pp.cf, pp.hf}
+//   s3 = {pp.tw, 0, 0, 0}
+//   cf  = C's node id (27 bits) | C's flags (5 bits)
+//   hf  = filter id of "C_path/#", NONE, or (CF_HFM) index into the multi[] list pool
+//   tw  = wildcard filter(s) ending exactly at C (fid, or LIST_MULTI|multi index)
+//   tn  = non-wildcard trie key(s) ending at C (same encoding)
+//   p   = C's '+' child, pp = p's '+' child: {cf, hf, tw} of each, cf = 0 if there is none
+//         (node 0 is the root, never a child).  Embedding them lets the walk expand '+'
+//         children without a probe; only a third consecutive '+' level probes (C/+, '+').
 // An empty slot has parent == NONE.
+constexpr uint32_t SLOT_U4 = 4;
 constexpr uint32_t CF_ID_BITS = 27;
 constexpr uint32_t CF_ID_MASK = (1u << CF_ID_BITS) - 1;
 constexpr uint32_t MAX_NODES = CF_ID_MASK;

@@ -384,15 +384,43 @@ int commit_locked(emqxgm* h) {
     cfv[i] = (uint32_t)i | flags;
     hfv[i] = hf;
   }
-  // 32-B slots: {tok.lo, tok.hi, parent, cf} {hf, tw, tn, 0}; load factor <= 1/2
+  // '+' child of every node (0 = none); its info is embedded one and two levels deep in the
+  // slot of the edge that leads to the node, so the walk never probes for most '+' children
+  std::vector<uint32_t> pchild(n_nodes, 0u);
+  for (const Edge& e : edges)
+    if (e.tok == PLUS_TOK) pchild[e.parent] = e.child;
+  // 64-B slots (gm_common.h "edge slots"); load factor <= 1/2
   const uint64_t ecap = pow2_at_least(std::max<uint64_t>(64, edges.size() * 2));
-  std::vector<uint4> eslots(2 * ecap, make_uint4(0u, 0u, 0u, 0u));
-  for (uint64_t i = 0; i < ecap; ++i) eslots[2 * i] = make_uint4(0u, 0u, NONE, 0u);
+  std::vector<uint4> eslots(SLOT_U4 * ecap, make_uint4(0u, 0u, 0u, 0u));
+  for (uint64_t i = 0; i < ecap; ++i) eslots[SLOT_U4 * i] = make_uint4(0u, 0u, NONE, 0u);
+  auto pinfo = [&](uint32_t node, uint32_t& cf, uint32_t& hf, uint32_t& tw) {
+    if (node == 0) {
+      cf = 0u;
+      hf = tw = NONE;
+    } else {
+      cf = cfv[node];
+      hf = hfv[node];
+      tw = resolve(ntw[node]);
+    }
+  };
   for (const Edge& e : edges) {
     uint64_t i = edge_slot(e.parent, e.tok, ecap - 1);
-    while (eslots[2 * i].z != NONE) i = (i + 1) & (ecap - 1);
-    eslots[2 * i] = make_uint4((uint32_t)e.tok, (uint32_t)(e.tok >> 32), e.parent, cfv[e.child]);
-    eslots[2 * i + 1] = make_uint4(hfv[e.child], resolve(ntw[e.child]), resolve(ntn[e.child]), 0u);
+    while (eslots[SLOT_U4 * i].z != NONE) i = (i + 1) & (ecap - 1);
+    const uint32_t c = e.child, p = pchild[c], pp = p ? pchild[p] : 0u;
+    uint32_t pcf, phf, ptw, ppcf, pphf, pptw;
+    pinfo(p, pcf, phf, ptw);
+    pinfo(pp, ppcf, pphf, pptw);
+    uint4* sl = &eslots[SLOT_U4 * i];
+    sl[0] = make_uint4((uint32_t)e.tok, (uint32_t)(e.tok >> 32), e.parent, cfv[c]);
+    sl[1] = make_uint4(hfv[c], resolve(ntw[c]), resolve(ntn[c]), pcf);
+    sl[2] = make_uint4(phf, ptw, ppcf, pphf);
+    sl[3] = make_uint4(pptw, 0u, 0u, 0u);
+  }
+  uint32_t root_q[6];
+  {
+    const uint32_t p = pchild[0], pp = p ? pchild[p] : 0u;
+    pinfo(p, root_q[0], root_q[1], root_q[2]);
+    pinfo(pp, root_q[3], root_q[4], root_q[5]);
   }
 
   // ---- exact route keys ----
@@ -447,6 +475,7 @@ int commit_locked(emqxgm* h) {
   nx.xmask = xcap - 1;
   nx.root_cf = cfv[0];
   nx.root_hf = hfv[0];
+  for (int q = 0; q < 6; ++q) nx.root_q[q] = root_q[q];
   nx.fbytes = (const uint8_t*)h->d_pool.p;
   nx.foff = (const uint64_t*)h->d_foff.p;
   nx.fver = (const uint4*)h->d_fver.p;
@@ -472,7 +501,7 @@ int commit_locked(emqxgm* h) {
   h->st.edge_slots = ecap;
   h->st.exact_slots = xcap;
   h->st.max_depth = max_depth;
-  h->st.device_bytes = ecap * 32 + xcap * 16 + multi.size() * 4 + h->pool.size() +
+  h->st.device_bytes = ecap * SLOT_U4 * 16 + xcap * 16 + multi.size() * 4 + h->pool.size() +
                        (nf + 1) * 8 + nf * VREC;
   return 0;
 }
@@ -508,7 +537,6 @@ int ensure_scratch(emqxgm* h, uint32_t n, uint64_t words, uint32_t pairs) {
   int rc = 0;
   const uint32_t stw = scan_tmp_words(ncap);
   if ((rc = dev_alloc(h, (void**)&s.nw, (size_t)ncap * 4)) ||
-      (rc = dev_alloc(h, (void**)&s.wbase, (size_t)(ncap + 1) * 4)) ||
       (rc = dev_alloc(h, (void**)&s.wh, (size_t)wcap * 8)) ||
       (rc = dev_alloc(h, (void**)&s.rec, (size_t)ncap * 16)) ||
       (rc = dev_alloc(h, (void**)&s.cnt, (size_t)ncap * 4)) ||
@@ -524,7 +552,7 @@ int ensure_scratch(emqxgm* h, uint32_t n, uint64_t words, uint32_t pairs) {
       (rc = dev_alloc(h, (void**)&s.scan_tmp, (size_t)stw * 4)) ||
       (rc = dev_alloc(h, (void**)&s.ctl, CTL_N * 4)) ||
       (rc = dev_alloc(h, (void**)&s.census, 4 * sizeof(unsigned long long))) ||
-      (rc = dev_alloc(h, (void**)&s.spill, (size_t)std::max<uint64_t>(scap, 1) * 16)) ||
+      (rc = dev_alloc(h, (void**)&s.spill, (size_t)std::max<uint64_t>(scap, 1) * 16 * SPILL_U4)) ||
       (rc = dev_alloc(h, (void**)&s.rlist, (size_t)h->reject_cap * 8)))
     return rc;
   s.r_cap = h->reject_cap;
@@ -563,9 +591,7 @@ int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_
     if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[0], st));
     HIPCHK(h, hipMemsetAsync(s.ctl, 0, CTL_N * 4, st));
     if (census) HIPCHK(h, hipMemsetAsync(s.census, 0, 4 * sizeof(unsigned long long), st));
-    HIPCHK(h, launch_tok_count(d_bytes, d_off, n, s.nw, st));
-    HIPCHK(h, launch_scan(s.nw, s.wbase, n, s.scan_tmp, s.ctl + CTL_WORDS, st));
-    HIPCHK(h, launch_tok_hash(d_bytes, d_off, n, h->ix, s, st));
+    HIPCHK(h, launch_tok(d_bytes, d_off, n, h->ix, s, st));
     if (h->ix.trie_empty) {
       HIPCHK(h, hipMemsetAsync(s.row, 0, (size_t)(n + 1) * 4, st));
     } else {

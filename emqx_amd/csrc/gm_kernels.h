@@ -7,10 +7,11 @@ namespace gm {
 
 // Committed device index (all pointers are device memory).
 struct DevIndex {
-  const uint4* edges = nullptr;   // 2 x uint4 per slot (gm_common.h "edge slots")
+  const uint4* edges = nullptr;   // SLOT_U4 x uint4 per slot (gm_common.h "edge slots")
   uint64_t emask = 0;             // slot capacity - 1
   const uint32_t* multi = nullptr;  // [count, fid...] lists
   uint32_t root_cf = 0, root_hf = 0xFFFFFFFFu;
+  uint32_t root_q[6] = {0u, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0xFFFFFFFFu, 0xFFFFFFFFu};  // p, pp
   const uint4* exact = nullptr;   // exact slots {hash.lo, hash.hi, fid, len}
   uint64_t xmask = 0;
   const uint8_t* fbytes = nullptr;  // filter string pool
@@ -30,7 +31,6 @@ struct Scratch {
   uint32_t n_cap = 0;  // topic capacity
   uint64_t w_cap = 0;  // word capacity
   uint32_t* nw = nullptr;     // [n]   words per topic
-  uint32_t* wbase = nullptr;  // [n+1]
   uint64_t* wh = nullptr;     // [w]   level tokens
   uint4* rec = nullptr;       // [n]   {wbase, n_words | flags << 24, tok0.lo, tok0.hi}
   uint32_t* cnt = nullptr;    // [n]   trie matches per topic
@@ -70,6 +70,7 @@ enum : int {
 constexpr uint32_t REJ_BIT = 0x80000000u;
 constexpr uint32_t REJ_SCAN_MAX = 4096;  // rejects the deferred scatter handles in-line
 constexpr uint32_t WALK_LDS_STACK = 4;   // walk stack entries per lane kept in LDS (rest spill)
+constexpr uint32_t SPILL_U4 = 3;         // uint4 per spilled walk stack entry
 
 struct WalkGeom {
   uint32_t blocks = 0;      // persistent workgroups
@@ -80,13 +81,13 @@ struct WalkGeom {
 WalkGeom walk_geometry(int device, uint32_t wg_per_cu);
 
 // Pipeline stages (all asynchronous on `s`).
-hipError_t launch_tok_count(const uint8_t* bytes, const uint32_t* off, uint32_t n, uint32_t* nw,
-                            hipStream_t s);
 hipError_t launch_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* tmp,
                        uint32_t* total_dst, hipStream_t s);
 uint32_t scan_tmp_words(uint32_t n);
-hipError_t launch_tok_hash(const uint8_t* bytes, const uint32_t* off, uint32_t n,
-                           const DevIndex& ix, Scratch& sc, hipStream_t s);
+// tokenise: levels (nw), level tokens (wh), topic records (rec), exact route-key ids; adds the
+// batch's level count to ctl[CTL_WORDS]
+hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
+                      Scratch& sc, hipStream_t s);
 // census != nullptr selects the diagnostic walk that adds {states, slot loads} to census[0..1]
 hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGeom& g,
                        hipStream_t s, unsigned long long* census = nullptr);

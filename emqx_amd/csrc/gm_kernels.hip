@@ -1,9 +1,8 @@
 // gm_kernels.hip -- gfx950 (MI355X, CDNA4) kernels of the batched MQTT publish-match pipeline.
 //
 // Pipeline for one batch of N published topics (DESIGN.md "Kernels"):
-//   k_tok_count      levels per topic                                   (gm_tok.inc)
-//   k_scan_*         exclusive scan -> word base of each topic
-//   k_tok_hash       level tokens, wildcard/'$' flags, exact route-key probe (gm_tok.inc)
+//   k_tok            levels, level tokens, wildcard/'$' flags, exact route-key probe
+//                    (one fused pass per 256-topic tile)                        (gm_tok.inc)
 //   k_walk           persistent trie walk, matches staged as (topic, filter, rank) (gm_walk.inc)
 //   k_verify         byte re-check of pairs whose filter has a hashed token   (gm_verify.inc)
 //   k_scan_*         per-topic match counts -> CSR row pointers
@@ -72,8 +71,6 @@ __device__ __forceinline__ bool mqtt_match(PT T, uint32_t tl, PF F, uint32_t fl)
     if (flast) return i > tl;  // match([], []) -> true ; match([_|_], []) -> false
   }
 }
-
-#include "gm_tok.inc"
 
 // ----------------------------------------------------------------------------------------
 // exclusive scan (u32), reduce-then-scan over tiles of SCAN_TILE elements
@@ -150,6 +147,7 @@ __global__ __launch_bounds__(WG) void k_scan_final(const uint32_t* __restrict__ 
   }
 }
 
+#include "gm_tok.inc"
 #include "gm_walk.inc"
 #include "gm_verify.inc"
 
@@ -176,13 +174,6 @@ WalkGeom walk_geometry(int device, uint32_t wg_per_cu) {
   return g;
 }
 
-hipError_t launch_tok_count(const uint8_t* bytes, const uint32_t* off, uint32_t n, uint32_t* nw,
-                            hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_tok_count, dim3(grid_for(n, 8192)), dim3(WG), 0, s, bytes, off, n, nw);
-  return hipGetLastError();
-}
-
 uint32_t scan_tmp_words(uint32_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 1; }
 
 hipError_t launch_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* tmp,
@@ -194,17 +185,18 @@ hipError_t launch_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* 
   return hipGetLastError();
 }
 
-hipError_t launch_tok_hash(const uint8_t* bytes, const uint32_t* off, uint32_t n,
-                           const DevIndex& ix, Scratch& sc, hipStream_t s) {
+hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
+                      Scratch& sc, hipStream_t s) {
   if (n == 0) return hipSuccess;
   TokArgs a;
   a.bytes = bytes;
   a.off = off;
   a.n = n;
-  a.wbase = sc.wbase;
+  a.nw = sc.nw;
   a.wh = sc.wh;
   a.rec = sc.rec;
   a.exact_id = sc.exact_id;
+  a.ctl = sc.ctl;
   a.exact = ix.exact;
   a.xmask = ix.xmask;
   a.fbytes = ix.fbytes;
@@ -213,7 +205,7 @@ hipError_t launch_tok_hash(const uint8_t* bytes, const uint32_t* off, uint32_t n
   a.test_mask = ix.test_mask;
   a.full_mask = ix.full_mask;
   a.exact_empty = ix.exact_empty;
-  hipLaunchKernelGGL(k_tok_hash, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a);
+  hipLaunchKernelGGL(k_tok, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a);
   return hipGetLastError();
 }
 
@@ -227,6 +219,7 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   a.multi = ix.multi;
   a.root_cf = ix.root_cf;
   a.root_hf = ix.root_hf;
+  for (int q = 0; q < 6; ++q) a.root_q[q] = ix.root_q[q];
   a.n = n;
   a.ctl = sc.ctl;
   a.cnt = sc.cnt;
