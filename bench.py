@@ -178,6 +178,8 @@ def main():
                 "pairs_per_batch": int(census["pairs"]),
                 "trie_states_per_batch": int(census["states"]),
                 "edge_slot_loads_per_batch": int(census["slot_loads"]),
+                "walk_lane_iterations_per_batch": int(census["lane_iters"]),
+                "walk_wave_iterations_per_batch": int(census["wave_iters"]),
                 "pipeline_ms_per_batch": round(pipe_ms, 4),
             },
             "roofline": {

@@ -80,6 +80,9 @@ constexpr uint32_t LIST_MULTI = 0x80000000u;  // tw/tn value is a multi[] index
 GM_HD uint64_t edge_slot(uint32_t parent, uint64_t tok, uint64_t mask) {
   return fmix64(tok ^ ((uint64_t)parent * 0x9e3779b97f4a7c15ull)) & mask;
 }
+// Exact route-key table: buckets of XBUCKET 16-B entries {hash.lo, hash.hi, fid, len}, filled
+// in order (linear probing over buckets); exact_slot gives the home bucket.
+constexpr uint32_t XBUCKET = 4;
 GM_HD uint64_t exact_slot(uint64_t fh, uint64_t mask) { return fmix64(fh + 0x632be59bd9b4e019ull) & mask; }
 
 // Filter verification record (64 B per filter id): {u32 len, 60 bytes of the filter}; the
@@ -87,8 +90,12 @@ GM_HD uint64_t exact_slot(uint64_t fh, uint64_t mask) { return fmix64(fh + 0x632
 constexpr uint32_t VREC = 64;
 constexpr uint32_t VINL = 60;
 
-// Per-topic record written by the tokenizer (uint4): {wbase, n_words | flags << 24, tok0.lo,
-// tok0.hi}; topics have at most 32,768 levels (65,535 bytes).
+// Per-topic record written by the tokenizer, 64 B = REC_U4 x uint4:
+//   {wbase, n_words | flags << 24, tok0.lo, tok0.hi} {tok1, tok2} {tok3, tok4} {tok5, tok6}
+// (tokens past the last level are 0); level tokens from REC_TOKS on are read from the token
+// array at wbase.  Topics have at most 32,768 levels (65,535 bytes).
+constexpr uint32_t REC_U4 = 4;
+constexpr uint32_t REC_TOKS = 7;
 constexpr uint32_t T_WILD = 1u;    // some level is exactly '+' or '#'  -> trie result []
 constexpr uint32_t T_DOLLAR = 2u;  // first byte is '$' -> no root '+'/'#' (emqx_trie.erl:282)
 

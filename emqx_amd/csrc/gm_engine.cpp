@@ -164,6 +164,7 @@ struct emqxgm {
 
   bool profiling = false;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  uint32_t spill_want = 0;         // walk spill items per lane (grown on overflow)
   uint32_t reject_cap = 1u << 20;  // cfg.reject_cap overrides (tests force the legacy path)
   uint64_t test_mask = 0;          // != 0: collision-test tokens (cfg.word_hash_bits)
 };
@@ -426,8 +427,9 @@ int commit_locked(emqxgm* h) {
   // ---- exact route keys ----
   uint64_t n_route = 0;
   for (const Filter& f : h->filters) n_route += f.route_refs > 0;
-  const uint64_t xcap = pow2_at_least(std::max<uint64_t>(64, n_route * 2));
-  std::vector<uint4> xslots(xcap, make_uint4(0u, 0u, NONE, 0u));
+  // buckets of XBUCKET entries, load factor <= 1/2, filled in order (gm_common.h)
+  const uint64_t xcap = pow2_at_least(std::max<uint64_t>(16, (n_route * 2 + XBUCKET - 1) / XBUCKET));
+  std::vector<uint4> xslots(xcap * XBUCKET, make_uint4(0u, 0u, NONE, 0u));
   for (uint32_t id = 0; id < h->filters.size(); ++id) {
     const Filter& f = h->filters[id];
     if (!f.route_refs) continue;
@@ -436,9 +438,16 @@ int commit_locked(emqxgm* h) {
     uint64_t x = FNV_OFF;
     for (uint64_t tk : toks) x = topic_hash_step(x, tk);
     const uint64_t fh = topic_hash_final(x, (uint32_t)toks.size(), fmask);
-    uint64_t i = exact_slot(fh, xcap - 1);
-    while (xslots[i].z != NONE) i = (i + 1) & (xcap - 1);
-    xslots[i] = make_uint4((uint32_t)fh, (uint32_t)(fh >> 32), id, f.len);
+    uint64_t b = exact_slot(fh, xcap - 1);
+    for (;;) {
+      uint32_t j = 0;
+      while (j < XBUCKET && xslots[b * XBUCKET + j].z != NONE) ++j;
+      if (j < XBUCKET) {
+        xslots[b * XBUCKET + j] = make_uint4((uint32_t)fh, (uint32_t)(fh >> 32), id, f.len);
+        break;
+      }
+      b = (b + 1) & (xcap - 1);
+    }
   }
 
   // ---- filter string pool, offsets and 64-B verification records (append-only) ----
@@ -499,9 +508,9 @@ int commit_locked(emqxgm* h) {
   h->st.n_nodes = n_nodes;
   h->st.n_edges = edges.size();
   h->st.edge_slots = ecap;
-  h->st.exact_slots = xcap;
+  h->st.exact_slots = xcap * XBUCKET;
   h->st.max_depth = max_depth;
-  h->st.device_bytes = ecap * SLOT_U4 * 16 + xcap * 16 + multi.size() * 4 + h->pool.size() +
+  h->st.device_bytes = ecap * SLOT_U4 * 16 + xcap * XBUCKET * 16 + multi.size() * 4 + h->pool.size() +
                        (nf + 1) * 8 + nf * VREC;
   return 0;
 }
@@ -518,16 +527,16 @@ int dev_alloc(emqxgm* h, void** p, size_t bytes) {
 // (Re)allocate batch scratch for n topics, `words` words and `pairs` staged pairs.
 int ensure_scratch(emqxgm* h, uint32_t n, uint64_t words, uint32_t pairs) {
   Scratch& s = h->sc;
-  const uint64_t spill_need =
-      (uint64_t)(h->ix.max_depth > WALK_LDS_STACK ? h->ix.max_depth - WALK_LDS_STACK + 1 : 0) * h->geom.lanes;
-  if (n <= s.n_cap && words <= s.w_cap && pairs <= s.p_cap && spill_need <= s.spill_cap &&
+  const uint32_t spill_need = std::max<uint32_t>(h->spill_want, WALK_SPILL_MIN);
+  if (n <= s.n_cap && words <= s.w_cap && pairs <= s.p_cap && spill_need <= s.spill_items &&
+      s.spill_lanes == h->geom.lanes &&
       s.ctl)
     return 0;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   const uint32_t ncap = std::max(n, s.n_cap);
   const uint64_t wcap = std::max(words, s.w_cap);
   const uint32_t pcap = std::max(pairs, s.p_cap);
-  const uint64_t scap = std::max(spill_need, s.spill_cap);
+  const uint32_t scap = std::max(spill_need, s.spill_items);
   free_bufs(h->sc_bufs);
   if (s.ctl_host) {
     (void)hipHostFree(s.ctl_host);
@@ -538,12 +547,13 @@ int ensure_scratch(emqxgm* h, uint32_t n, uint64_t words, uint32_t pairs) {
   const uint32_t stw = scan_tmp_words(ncap);
   if ((rc = dev_alloc(h, (void**)&s.nw, (size_t)ncap * 4)) ||
       (rc = dev_alloc(h, (void**)&s.wh, (size_t)wcap * 8)) ||
-      (rc = dev_alloc(h, (void**)&s.rec, (size_t)ncap * 16)) ||
+      (rc = dev_alloc(h, (void**)&s.rec, (size_t)ncap * 16 * REC_U4)) ||
       (rc = dev_alloc(h, (void**)&s.cnt, (size_t)ncap * 4)) ||
       (rc = dev_alloc(h, (void**)&s.row, (size_t)(ncap + 1) * 4)) ||
       (rc = dev_alloc(h, (void**)&s.row2, (size_t)(ncap + 1) * 4)) ||
       (rc = dev_alloc(h, (void**)&s.rej, (size_t)ncap * 4)) ||
       (rc = dev_alloc(h, (void**)&s.exact_id, (size_t)ncap * 4)) ||
+      (rc = dev_alloc(h, (void**)&s.th, (size_t)ncap * 8)) ||
       (rc = dev_alloc(h, (void**)&s.pt, (size_t)pcap * 4)) ||
       (rc = dev_alloc(h, (void**)&s.pf, (size_t)pcap * 4)) ||
       (rc = dev_alloc(h, (void**)&s.pr, (size_t)pcap * 4)) ||
@@ -551,8 +561,8 @@ int ensure_scratch(emqxgm* h, uint32_t n, uint64_t words, uint32_t pairs) {
       (rc = dev_alloc(h, (void**)&s.out2, (size_t)pcap * 4)) ||
       (rc = dev_alloc(h, (void**)&s.scan_tmp, (size_t)stw * 4)) ||
       (rc = dev_alloc(h, (void**)&s.ctl, CTL_N * 4)) ||
-      (rc = dev_alloc(h, (void**)&s.census, 4 * sizeof(unsigned long long))) ||
-      (rc = dev_alloc(h, (void**)&s.spill, (size_t)std::max<uint64_t>(scap, 1) * 16 * SPILL_U4)) ||
+      (rc = dev_alloc(h, (void**)&s.census, CENSUS_N * sizeof(unsigned long long))) ||
+      (rc = dev_alloc(h, (void**)&s.spill, (size_t)scap * h->geom.lanes * sizeof(uint2))) ||
       (rc = dev_alloc(h, (void**)&s.rlist, (size_t)h->reject_cap * 8)))
     return rc;
   s.r_cap = h->reject_cap;
@@ -562,7 +572,8 @@ int ensure_scratch(emqxgm* h, uint32_t n, uint64_t words, uint32_t pairs) {
   s.p_cap = pcap;
   s.o_cap = pcap;
   s.scan_tmp_cap = stw;
-  s.spill_cap = scap;
+  s.spill_items = scap;
+  s.spill_lanes = h->geom.lanes;
   return 0;
 }
 
@@ -574,7 +585,11 @@ int ensure_scratch(emqxgm* h, uint32_t n, uint64_t words, uint32_t pairs) {
 // adversarial index), the pass is redone on the legacy path: scan -> verify+scatter -> compaction.
 int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_t n,
                uint64_t bytes_len, uint32_t* pairs, uint64_t* census = nullptr) {
-  const uint64_t words = bytes_len + n + 1;
+  const uint64_t words = bytes_len + n + 1;  // token array: level k of topic t at off[t] + t + k
+  if (words > 0xFFFFFFFFull) {
+    h->err = "batch too large: topic bytes + topics must stay below 2^32";
+    return -E2BIG;
+  }
   uint32_t want_pairs = std::max<uint32_t>(h->sc.p_cap, std::max<uint32_t>(1u << 20, n * 4u));
   int rc = ensure_scratch(h, std::max<uint32_t>(n, 1), words, want_pairs);
   if (rc) return rc;
@@ -590,8 +605,9 @@ int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_
   for (int attempt = 0;; ++attempt) {
     if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[0], st));
     HIPCHK(h, hipMemsetAsync(s.ctl, 0, CTL_N * 4, st));
-    if (census) HIPCHK(h, hipMemsetAsync(s.census, 0, 4 * sizeof(unsigned long long), st));
+    if (census) HIPCHK(h, hipMemsetAsync(s.census, 0, CENSUS_N * sizeof(unsigned long long), st));
     HIPCHK(h, launch_tok(d_bytes, d_off, n, h->ix, s, st));
+    HIPCHK(h, launch_exact(d_bytes, d_off, n, h->ix, s, st));
     if (h->ix.trie_empty) {
       HIPCHK(h, hipMemsetAsync(s.row, 0, (size_t)(n + 1) * 4, st));
     } else {
@@ -625,6 +641,19 @@ int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_
       if (rc) return rc;
       continue;
     }
+    if (s.ctl_host[CTL_ERR]) {
+      // a walk lane's item stack outgrew the spill: grow it to the proven bound and redo
+      const uint32_t bound = walk_spill_bound(h->ix.max_depth);
+      if (s.spill_items >= bound) {
+        h->err = "walk item stack exceeded its bound";
+        return -EIO;
+      }
+      h->st.reruns += 1;
+      h->spill_want = bound;
+      rc = ensure_scratch(h, n, words, s.p_cap);
+      if (rc) return rc;
+      continue;
+    }
     if (!legacy && s.ctl_host[CTL_LEGACY]) {
       h->st.reruns += 1;
       legacy = true;
@@ -653,12 +682,18 @@ int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_
   if (legacy) h->st.legacy_batches += 1;
   *pairs = s.ctl_host[CTL_TOTAL];
   if (census) {
-    unsigned long long c[4] = {0, 0, 0, 0};
+    unsigned long long c[CENSUS_N] = {0, 0, 0, 0};
     HIPCHK(h, hipMemcpy(c, s.census, sizeof c, hipMemcpyDeviceToHost));
     census[0] = c[0];
     census[1] = c[1];
     census[2] = *pairs;
-    census[3] = s.ctl_host[CTL_WORDS];
+    std::vector<uint32_t> nw(n);
+    HIPCHK(h, hipMemcpy(nw.data(), s.nw, (size_t)n * 4, hipMemcpyDeviceToHost));
+    uint64_t nwords = 0;
+    for (uint32_t v : nw) nwords += v;
+    census[3] = nwords;
+    census[4] = c[2];
+    census[5] = c[3];
   }
   h->st.batches += 1;
   h->st.topics += n;
@@ -945,12 +980,12 @@ int emqxgm_match_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offset
 }
 
 int emqxgm_walk_census(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_offsets, uint32_t n,
-                       uint64_t bytes_len, uint64_t out[4]) {
+                       uint64_t bytes_len, uint64_t out[6]) {
   if (!h || !out || (!d_offsets && n)) return -EINVAL;
   std::lock_guard<std::mutex> g(h->mu);
   if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
   uint32_t pairs = 0;
-  memset(out, 0, 4 * sizeof(uint64_t));
+  memset(out, 0, 6 * sizeof(uint64_t));
   return run_device(h, d_bytes, d_offsets, n, bytes_len, &pairs, out);
 }
 

@@ -12,8 +12,8 @@ struct DevIndex {
   const uint32_t* multi = nullptr;  // [count, fid...] lists
   uint32_t root_cf = 0, root_hf = 0xFFFFFFFFu;
   uint32_t root_q[6] = {0u, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0xFFFFFFFFu, 0xFFFFFFFFu};  // p, pp
-  const uint4* exact = nullptr;   // exact slots {hash.lo, hash.hi, fid, len}
-  uint64_t xmask = 0;
+  const uint4* exact = nullptr;   // exact buckets of XBUCKET {hash.lo, hash.hi, fid, len}
+  uint64_t xmask = 0;             // bucket count - 1
   const uint8_t* fbytes = nullptr;  // filter string pool
   const uint64_t* foff = nullptr;   // [n_filters+1]
   const uint4* fver = nullptr;      // 64-B verification record per filter id
@@ -32,12 +32,13 @@ struct Scratch {
   uint64_t w_cap = 0;  // word capacity
   uint32_t* nw = nullptr;     // [n]   words per topic
   uint64_t* wh = nullptr;     // [w]   level tokens
-  uint4* rec = nullptr;       // [n]   {wbase, n_words | flags << 24, tok0.lo, tok0.hi}
+  uint4* rec = nullptr;       // [n * REC_U4] 64-B topic records (gm_common.h)
   uint32_t* cnt = nullptr;    // [n]   trie matches per topic
   uint32_t* row = nullptr;    // [n+1]
   uint32_t* row2 = nullptr;   // [n+1] (legacy fix-up)
   uint32_t* rej = nullptr;    // [n]   rejected pairs per topic
   uint32_t* exact_id = nullptr;  // [n]
+  uint64_t* th = nullptr;        // [n]   whole-topic hash (exact route-key probe)
   uint32_t p_cap = 0;   // pair staging capacity
   uint32_t* pt = nullptr;     // staged pair: topic
   uint32_t* pf = nullptr;     // staged pair: filter
@@ -48,12 +49,13 @@ struct Scratch {
   uint32_t* scan_tmp = nullptr;  // scan partials
   uint32_t scan_tmp_cap = 0;
   uint32_t* ctl = nullptr;    // control words (see CTL_*)
-  uint4* spill = nullptr;     // walk stack spill (depth beyond LDS)
-  uint64_t spill_cap = 0;     // entries
+  uint2* spill = nullptr;     // walk probe items beyond the LDS stack
+  uint32_t spill_items = 0;   // spill entries per walk lane
+  uint32_t spill_lanes = 0;   // walk lanes the spill was sized for
   uint2* rlist = nullptr;     // rejected (topic, rank) list
   uint32_t r_cap = 0;
   uint32_t* ctl_host = nullptr;  // pinned host mirror of ctl
-  unsigned long long* census = nullptr;  // [4] diagnostic walk counters
+  unsigned long long* census = nullptr;  // [CENSUS_N] diagnostic walk counters
 };
 
 enum : int {
@@ -61,16 +63,30 @@ enum : int {
   CTL_PAIR_TOP = 1,   // staged pair slots reserved
   CTL_ANY_REJ = 2,    // a verification rejected some pair
   CTL_TOTAL = 3,      // total pairs (row[n]) copied here
-  CTL_WORDS = 4,      // total words
+  CTL_WORDS = 4,      // (unused)
   CTL_NREJ = 5,       // rejected pairs appended to rlist
   CTL_LEGACY = 6,     // deferred scatter could not place rejects: re-run with the fix-up path
-  CTL_N = 8
+  CTL_ERR = 7,        // walk item stack outgrew its spill: re-run with a larger spill
+  CTL_CLAIM0 = 16,    // walk topic-claim counters, one per shard, CTL_CLAIM_STRIDE apart
+  CTL_N = 16 + 8 * 32
 };
+
+// diagnostic walk counters: states, slot loads, lane iterations, wave iterations
+constexpr uint32_t CENSUS_N = 4;
+
+// The walk claims topics from WALK_SHARDS counters on separate 128-B lines (one hot counter
+// serialises at ~88 claims/us chip-wide); a wave starts on shard blockIdx % 8 (its XCD under
+// round-robin dispatch) and moves on when that shard's topics are exhausted.
+constexpr uint32_t WALK_SHARDS = 8;
+constexpr uint32_t CTL_CLAIM_STRIDE = 32;
 
 constexpr uint32_t REJ_BIT = 0x80000000u;
 constexpr uint32_t REJ_SCAN_MAX = 4096;  // rejects the deferred scatter handles in-line
-constexpr uint32_t WALK_LDS_STACK = 4;   // walk stack entries per lane kept in LDS (rest spill)
-constexpr uint32_t SPILL_U4 = 3;         // uint4 per spilled walk stack entry
+constexpr uint32_t WALK_LDS_STACK = 8;   // walk probe items per lane kept in LDS (rest spill)
+constexpr uint32_t WALK_SPILL_MIN = 32;  // initial spill items per lane (grown on overflow)
+// spill items per lane that no walk can exceed: a resolved probe pushes <= 4 items spanning
+// 3 levels, and the LIFO holds <= 3 unexplored siblings per level of the current path
+inline uint32_t walk_spill_bound(uint32_t max_depth) { return 4u * (max_depth + 2u) + 8u; }
 
 struct WalkGeom {
   uint32_t blocks = 0;      // persistent workgroups
@@ -84,10 +100,13 @@ WalkGeom walk_geometry(int device, uint32_t wg_per_cu);
 hipError_t launch_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* tmp,
                        uint32_t* total_dst, hipStream_t s);
 uint32_t scan_tmp_words(uint32_t n);
-// tokenise: levels (nw), level tokens (wh), topic records (rec), exact route-key ids; adds the
-// batch's level count to ctl[CTL_WORDS]
+// tokenise: levels (nw), 64-B topic records (rec: first REC_TOKS tokens inline), tokens of
+// deeper levels (wh, at off[t] + t + level), whole-topic hashes (th)
 hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
                       Scratch& sc, hipStream_t s);
+// exact route-key ids (exact_id[t], NONE when absent or when the table is empty)
+hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
+                        Scratch& sc, hipStream_t s);
 // census != nullptr selects the diagnostic walk that adds {states, slot loads} to census[0..1]
 hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGeom& g,
                        hipStream_t s, unsigned long long* census = nullptr);

@@ -256,11 +256,13 @@ class Engine:
                             o.n_words or 0)
 
     def walk_census(self, d_bytes: int, d_off: int, n: int, bytes_len: int) -> dict:
-        """Instrumented pass: {'states': sum S(t), 'slot_loads', 'pairs', 'words'}."""
-        out = (C.c_uint64 * 4)()
+        """Instrumented pass: {'states': sum S(t), 'slot_loads', 'pairs', 'words',
+        'lane_iters', 'wave_iters'}."""
+        out = (C.c_uint64 * 6)()
         self._check(self._lib.emqxgm_walk_census(self._h, C.c_void_p(d_bytes), C.c_void_p(d_off),
                                                  n, bytes_len, out), "walk_census")
-        return {"states": out[0], "slot_loads": out[1], "pairs": out[2], "words": out[3]}
+        return {"states": out[0], "slot_loads": out[1], "pairs": out[2], "words": out[3],
+                "lane_iters": out[4], "wave_iters": out[5]}
 
     def tune(self, key: str, value: int) -> None:
         self._check(self._lib.emqxgm_tune(self._h, key.encode(), int(value)), f"tune({key})")

@@ -137,9 +137,11 @@ int emqxgm_match_device(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_o
 
 /* Diagnostic pass (instrumented walk kernel, not the production launch): runs the device
  * match and returns out[0] = trie states matched (SURVEY 8d S(t) summed over the batch),
- * out[1] = edge slots loaded, out[2] = pairs, out[3] = levels (words) in the batch. */
+ * out[1] = edge slots loaded, out[2] = pairs, out[3] = levels (words) in the batch,
+ * out[4] = walk iterations summed over busy lanes, out[5] = walk iterations summed over
+ * wavefronts (one memory round trip each). */
 int emqxgm_walk_census(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_offsets,
-                       uint32_t n, uint64_t bytes_len, uint64_t out[4]);
+                       uint32_t n, uint64_t bytes_len, uint64_t out[6]);
 
 int emqxgm_set_profiling(emqxgm_t* h, int on);
 /* Runtime tuning knobs: "walk_wg_per_cu" (persistent walk workgroups per CU). */
