@@ -553,7 +553,6 @@ int ensure_scratch(emqxgm* h, uint32_t n, uint64_t words, uint32_t pairs) {
       (rc = dev_alloc(h, (void**)&s.row2, (size_t)(ncap + 1) * 4)) ||
       (rc = dev_alloc(h, (void**)&s.rej, (size_t)ncap * 4)) ||
       (rc = dev_alloc(h, (void**)&s.exact_id, (size_t)ncap * 4)) ||
-      (rc = dev_alloc(h, (void**)&s.th, (size_t)ncap * 8)) ||
       (rc = dev_alloc(h, (void**)&s.pt, (size_t)pcap * 4)) ||
       (rc = dev_alloc(h, (void**)&s.pf, (size_t)pcap * 4)) ||
       (rc = dev_alloc(h, (void**)&s.pr, (size_t)pcap * 4)) ||
@@ -607,7 +606,6 @@ int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_
     HIPCHK(h, hipMemsetAsync(s.ctl, 0, CTL_N * 4, st));
     if (census) HIPCHK(h, hipMemsetAsync(s.census, 0, CENSUS_N * sizeof(unsigned long long), st));
     HIPCHK(h, launch_tok(d_bytes, d_off, n, h->ix, s, st));
-    HIPCHK(h, launch_exact(d_bytes, d_off, n, h->ix, s, st));
     if (h->ix.trie_empty) {
       HIPCHK(h, hipMemsetAsync(s.row, 0, (size_t)(n + 1) * 4, st));
     } else {

@@ -38,7 +38,6 @@ struct Scratch {
   uint32_t* row2 = nullptr;   // [n+1] (legacy fix-up)
   uint32_t* rej = nullptr;    // [n]   rejected pairs per topic
   uint32_t* exact_id = nullptr;  // [n]
-  uint64_t* th = nullptr;        // [n]   whole-topic hash (exact route-key probe)
   uint32_t p_cap = 0;   // pair staging capacity
   uint32_t* pt = nullptr;     // staged pair: topic
   uint32_t* pf = nullptr;     // staged pair: filter
@@ -101,12 +100,10 @@ hipError_t launch_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* 
                        uint32_t* total_dst, hipStream_t s);
 uint32_t scan_tmp_words(uint32_t n);
 // tokenise: levels (nw), 64-B topic records (rec: first REC_TOKS tokens inline), tokens of
-// deeper levels (wh, at off[t] + t + level), whole-topic hashes (th)
+// deeper levels (wh, at off[t] + t + level), exact route-key ids (exact_id, NONE if absent)
 hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
                       Scratch& sc, hipStream_t s);
-// exact route-key ids (exact_id[t], NONE when absent or when the table is empty)
-hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
-                        Scratch& sc, hipStream_t s);
+
 // census != nullptr selects the diagnostic walk that adds {states, slot loads} to census[0..1]
 hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGeom& g,
                        hipStream_t s, unsigned long long* census = nullptr);

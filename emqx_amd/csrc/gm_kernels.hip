@@ -195,30 +195,16 @@ hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, con
   a.nw = sc.nw;
   a.wh = sc.wh;
   a.rec = sc.rec;
-  a.th = sc.th;
-  a.ctl = sc.ctl;
-  a.test_mask = ix.test_mask;
-  a.full_mask = ix.full_mask;
-  hipLaunchKernelGGL(k_tok, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
-                        Scratch& sc, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  if (ix.exact_empty) return hipMemsetAsync(sc.exact_id, 0xFF, (size_t)n * 4, s);
-  ExactArgs a;
-  a.bytes = bytes;
-  a.off = off;
-  a.n = n;
-  a.th = sc.th;
+  a.exact_id = sc.exact_id;
   a.exact = ix.exact;
-  a.bmask = ix.xmask;
+  a.xmask = ix.xmask;
   a.fbytes = ix.fbytes;
   a.foff = ix.foff;
   a.fver = ix.fver;
-  a.exact_id = sc.exact_id;
-  hipLaunchKernelGGL(k_exact, dim3(grid_for(n, 65536)), dim3(WG), 0, s, a);
+  a.test_mask = ix.test_mask;
+  a.full_mask = ix.full_mask;
+  a.exact_empty = ix.exact_empty;
+  hipLaunchKernelGGL(k_tok, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a);
   return hipGetLastError();
 }
 
