@@ -52,6 +52,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--topic-order", choices=["as-is", "xcd", "sorted"], default="as-is",
+                    help="experiment: permute the batch (outside the timed region) so that topics "
+                         "of one first-two-level prefix group share an XCD shard, or fully sorted")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -99,6 +102,8 @@ def main():
         f"keys, {est['n_nodes']} nodes, {est['device_bytes'] / 2**20:.0f} MiB in "
         f"{time.time() - t0:.1f}s")
 
+    if args.topic_order != "as-is":
+        w = _reorder_topics(w, args.topic_order)
     tb = torch.from_numpy(w.tbytes).to(dev)
     to = torch.from_numpy(w.toff.view(np.int32)).to(dev)
     nbytes = int(w.toff[-1])
@@ -215,6 +220,24 @@ def _subset_packed(fbytes, foff, idx):
     pos = np.repeat(starts - np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64), lens) \
         + np.arange(int(lens.sum()), dtype=np.int64)
     return fbytes[pos], off
+
+
+def _reorder_topics(w, how):
+    """Experiment only: a permutation of the batch (same topics, other order)."""
+    import dataclasses
+    topics = [w.topic(i) for i in range(w.nt)]
+    if how == "sorted":
+        order = sorted(range(w.nt), key=lambda i: topics[i])
+    else:  # group by a hash of the first two levels into 8 shards, random order inside
+        import zlib
+        rng = np.random.default_rng(7)
+        grp = np.array([zlib.crc32(b"/".join(t.split(b"/")[:2])) % 8 for t in topics])
+        order = np.concatenate([rng.permutation(np.nonzero(grp == g)[0]) for g in range(8)])
+    lens = np.array([len(topics[i]) for i in order], np.uint32)
+    off = np.zeros(w.nt + 1, np.uint32)
+    np.cumsum(lens, out=off[1:])
+    tbytes = np.frombuffer(b"".join(topics[i] for i in order), np.uint8).copy()
+    return dataclasses.replace(w, tbytes=tbytes, toff=off)
 
 
 def _pmc_traffic(cfg, nt):

@@ -165,6 +165,7 @@ struct emqxgm {
   bool profiling = false;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   uint32_t spill_want = 0;         // walk spill items per lane (grown on overflow)
+  bool walk_spill = false;         // committed index needs the spilling walk variant
   uint32_t reject_cap = 1u << 20;  // cfg.reject_cap overrides (tests force the legacy path)
   uint64_t test_mask = 0;          // != 0: collision-test tokens (cfg.word_hash_bits)
 };
@@ -498,6 +499,7 @@ int commit_locked(emqxgm* h) {
   h->ix_bufs.swap(nbufs);
   for (Filter& f : h->filters) f.trie_committed = f.in_trie;
   h->ix = nx;
+  h->walk_spill = false;
   h->epoch += 1;
   h->dirty = false;
 
@@ -611,7 +613,8 @@ int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_
     } else {
       HIPCHK(h, hipMemsetAsync(s.rej, 0, (size_t)n * 4, st));
       if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[1], st));
-      HIPCHK(h, launch_walk(h->ix, s, n, h->geom, st, census ? s.census : nullptr));
+      HIPCHK(h, launch_walk(h->ix, s, n, h->geom, st, census ? s.census : nullptr,
+                            h->walk_spill));
       if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[2], st));
       if (!legacy) {
         // pairs of filters made of short (exact) tokens need no byte check (gm_verify.inc)
@@ -637,6 +640,13 @@ int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_
       const uint64_t np = std::min<uint64_t>(0xF0000000ull, (uint64_t)top * 2 + (1u << 20));
       rc = ensure_scratch(h, n, words, (uint32_t)np);
       if (rc) return rc;
+      continue;
+    }
+    if (s.ctl_host[CTL_ERR] && !h->walk_spill) {
+      // a walk lane's item stack outgrew LDS: redo with the spilling variant (kept for this
+      // committed index)
+      h->st.reruns += 1;
+      h->walk_spill = true;
       continue;
     }
     if (s.ctl_host[CTL_ERR]) {

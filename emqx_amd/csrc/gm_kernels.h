@@ -104,9 +104,10 @@ uint32_t scan_tmp_words(uint32_t n);
 hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
                       Scratch& sc, hipStream_t s);
 
-// census != nullptr selects the diagnostic walk that adds {states, slot loads} to census[0..1]
+// census != nullptr selects the diagnostic walk (adds to census[0..CENSUS_N)); spill selects
+// the variant whose probe-item stack continues in global memory (after an LDS overflow)
 hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGeom& g,
-                       hipStream_t s, unsigned long long* census = nullptr);
+                       hipStream_t s, unsigned long long* census = nullptr, bool spill = false);
 // production: verify (flags + counts) -> [scan] -> deferred scatter
 hipError_t launch_verify(const uint8_t* bytes, const uint32_t* off, const DevIndex& ix,
                          Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_t s);

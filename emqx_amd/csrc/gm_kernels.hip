@@ -209,7 +209,7 @@ hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, con
 }
 
 hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGeom& g,
-                       hipStream_t s, unsigned long long* census) {
+                       hipStream_t s, unsigned long long* census, bool spill) {
   WalkArgs a;
   a.rec = sc.rec;
   a.wh = sc.wh;
@@ -230,10 +230,14 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   a.spill_items = sc.spill_items;
   a.lanes = g.lanes;
   a.census = census;
-  if (census)
-    hipLaunchKernelGGL(k_walk<true>, dim3(g.blocks), dim3(WG), 0, s, a);
+  if (census && spill)
+    hipLaunchKernelGGL((k_walk<true, true>), dim3(g.blocks), dim3(WG), 0, s, a);
+  else if (census)
+    hipLaunchKernelGGL((k_walk<true, false>), dim3(g.blocks), dim3(WG), 0, s, a);
+  else if (spill)
+    hipLaunchKernelGGL((k_walk<false, true>), dim3(g.blocks), dim3(WG), 0, s, a);
   else
-    hipLaunchKernelGGL(k_walk<false>, dim3(g.blocks), dim3(WG), 0, s, a);
+    hipLaunchKernelGGL((k_walk<false, false>), dim3(g.blocks), dim3(WG), 0, s, a);
   return hipGetLastError();
 }
 
