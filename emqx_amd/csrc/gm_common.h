@@ -46,10 +46,32 @@ GM_HD uint64_t word_token(uint64_t packed, uint64_t fnv, uint32_t len, uint64_t 
   return TOK_HASHED | (fmix64(fnv) >> 1);
 }
 
-// Whole-topic hash (exact route-key table), folded over the level tokens in order.
-GM_HD uint64_t topic_hash_step(uint64_t h, uint64_t tok) { return fmix64(h ^ tok) + FNV_PRIME; }
-GM_HD uint64_t topic_hash_final(uint64_t h, uint32_t n, uint64_t mask) {
-  return fmix64(h ^ ((uint64_t)n * 0x9e3779b97f4a7c15ull)) & mask;
+// Route-key hash (exact table): over the key's bytes taken as little-endian 32-bit words, the
+// last one zero-padded, in two 32-bit multiply-rotate lanes folded through fmix64.  It needs
+// only the bytes (not the level tokens), so the device issues the table probe before it
+// tokenises.  `mask` keeps fewer bits in the collision tests.
+GM_HD void key_hash_init(uint32_t len, uint32_t& a, uint32_t& b) {
+  a = 0x9747b28cu ^ len;
+  b = 0x85ebca6bu + len;
+}
+GM_HD void key_hash_word(uint32_t w, uint32_t& a, uint32_t& b) {
+  a ^= w * 0xcc9e2d51u;
+  a = ((a << 15) | (a >> 17)) * 5u + 0xe6546b64u;
+  b += w * 0x1b873593u;
+  b = ((b << 13) | (b >> 19)) * 0x85ebca6bu ^ 0xc2b2ae35u;
+}
+GM_HD uint64_t key_hash_final(uint32_t a, uint32_t b, uint64_t mask) {
+  return fmix64(((uint64_t)a << 32) | b) & mask;
+}
+GM_HD uint64_t key_hash(const uint8_t* p, uint32_t len, uint64_t mask) {
+  uint32_t a, b;
+  key_hash_init(len, a, b);
+  for (uint32_t i = 0; i < len; i += 4) {
+    uint32_t w = 0;
+    for (uint32_t j = 0; j < 4 && i + j < len; ++j) w |= (uint32_t)p[i + j] << (8 * j);
+    key_hash_word(w, a, b);
+  }
+  return key_hash_final(a, b, mask);
 }
 
 // ---- edge slots -------------------------------------------------------------------------

@@ -434,11 +434,7 @@ int commit_locked(emqxgm* h) {
   for (uint32_t id = 0; id < h->filters.size(); ++id) {
     const Filter& f = h->filters[id];
     if (!f.route_refs) continue;
-    bool hashed;
-    tokenize(h->pool.data() + f.off, f.len, test_mask, toks, is_plus, is_hash, hashed);
-    uint64_t x = FNV_OFF;
-    for (uint64_t tk : toks) x = topic_hash_step(x, tk);
-    const uint64_t fh = topic_hash_final(x, (uint32_t)toks.size(), fmask);
+    const uint64_t fh = key_hash(h->pool.data() + f.off, f.len, fmask);
     uint64_t b = exact_slot(fh, xcap - 1);
     for (;;) {
       uint32_t j = 0;
