@@ -81,7 +81,7 @@ constexpr uint32_t CTL_CLAIM_STRIDE = 32;
 
 constexpr uint32_t REJ_BIT = 0x80000000u;
 constexpr uint32_t REJ_SCAN_MAX = 4096;  // rejects the deferred scatter handles in-line
-constexpr uint32_t WALK_LDS_STACK = 8;   // walk probe items per lane kept in LDS (rest spill)
+constexpr uint32_t WALK_LDS_STACK = 6;   // walk probe items per lane kept in LDS (rest spill)
 constexpr uint32_t WALK_SPILL_MIN = 32;  // initial spill items per lane (grown on overflow)
 // spill items per lane that no walk can exceed: a resolved probe pushes <= 4 items spanning
 // 3 levels, and the LIFO holds <= 3 unexplored siblings per level of the current path
