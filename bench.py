@@ -126,8 +126,6 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    s0 = eng.stats()
-    eng.set_profiling(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -138,6 +136,13 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # kernel timing with HIP events on the engine's stream, in extra passes after the timed
+    # region (the events themselves add gaps between launches)
+    s0 = eng.stats()
+    eng.set_profiling(True)
+    for _ in range(max(3, min(args.steps, 10))):
+        step()
+    torch.cuda.synchronize()
     eng.set_profiling(False)
     s1 = eng.stats()
     if world > 1:
@@ -147,7 +152,7 @@ def main():
 
     launches = s1["walk_launches"] - s0["walk_launches"]
     walk_ms = (s1["walk_ms"] - s0["walk_ms"]) / max(1, launches)
-    pipe_ms = (s1["total_ms"] - s0["total_ms"]) / max(1, args.steps)
+    pipe_ms = (s1["total_ms"] - s0["total_ms"]) / max(1, launches)
     # algorithmic bytes of one k_walk launch (DESIGN.md "Roofline"): per topic a 16-B record,
     # the next-level token hashes (4 B per level), 3 x 16-B edge probes per matched trie state
     # (SURVEY 8d's 48*S(t)), and a 12-B staged (topic, filter, rank) triple per match; plus 4 B

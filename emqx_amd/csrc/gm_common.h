@@ -75,20 +75,18 @@ GM_HD uint64_t key_hash(const uint8_t* p, uint32_t len, uint64_t mask) {
 }
 
 // ---- edge slots -------------------------------------------------------------------------
-// 64 B per slot, 4 x uint4, one slot per trie edge (parent --level token--> child C):
+// 32 B per slot, 2 x uint4, one slot per trie edge (parent --level token--> child C):
 //   s0 = {tok.lo, tok.hi, parent, cf}       key = (parent node id, level token), exact
-//   s1 = {hf, tw, tn, p.cf}
-//   s2 = {p.hf, p.tw, pp.cf, pp.hf}
-//   s3 = {pp.tw, 0, 0, 0}
+//   s1 = {hf, tw, p.cf, p.hf}
 //   cf  = C's node id (27 bits) | C's flags (5 bits)
 //   hf  = filter id of "C_path/#", NONE, or (CF_HFM) index into the multi[] list pool
 //   tw  = wildcard filter(s) ending exactly at C (fid, or LIST_MULTI|multi index)
-//   tn  = non-wildcard trie key(s) ending at C (same encoding)
-//   p   = C's '+' child, pp = p's '+' child: {cf, hf, tw} of each, cf = 0 if there is none
-//         (node 0 is the root, never a child).  Embedding them lets the walk expand '+'
-//         children without a probe; only a third consecutive '+' level probes (C/+, '+').
-// An empty slot has parent == NONE.
-constexpr uint32_t SLOT_U4 = 4;
+//   p   = C's '+' child {cf, hf} (cf = 0 if there is none; node 0 is the root, never a child),
+//         carried so that the walk expands it without a probe.  The rest of p (its terminal
+//         filters, its own '+' child) comes from the (C, '+') slot when the walk needs it.
+// Non-wildcard trie keys ending at a node (only single-level '$' topics read them,
+// emqx_trie.erl:287) live in a per-node side array.  An empty slot has parent == NONE.
+constexpr uint32_t SLOT_U4 = 2;
 constexpr uint32_t CF_ID_BITS = 27;
 constexpr uint32_t CF_ID_MASK = (1u << CF_ID_BITS) - 1;
 constexpr uint32_t MAX_NODES = CF_ID_MASK;

@@ -386,44 +386,26 @@ int commit_locked(emqxgm* h) {
     cfv[i] = (uint32_t)i | flags;
     hfv[i] = hf;
   }
-  // '+' child of every node (0 = none); its info is embedded one and two levels deep in the
-  // slot of the edge that leads to the node, so the walk never probes for most '+' children
+  // '+' child of every node (0 = none); its {cf, hf} is carried in the slot of the edge that
+  // leads to the node, so the walk expands most '+' children without a probe
   std::vector<uint32_t> pchild(n_nodes, 0u);
   for (const Edge& e : edges)
     if (e.tok == PLUS_TOK) pchild[e.parent] = e.child;
-  // 64-B slots (gm_common.h "edge slots"); load factor <= 1/2
+  // 32-B slots (gm_common.h "edge slots"); load factor <= 1/2
   const uint64_t ecap = pow2_at_least(std::max<uint64_t>(64, edges.size() * 2));
   std::vector<uint4> eslots(SLOT_U4 * ecap, make_uint4(0u, 0u, 0u, 0u));
   for (uint64_t i = 0; i < ecap; ++i) eslots[SLOT_U4 * i] = make_uint4(0u, 0u, NONE, 0u);
-  auto pinfo = [&](uint32_t node, uint32_t& cf, uint32_t& hf, uint32_t& tw) {
-    if (node == 0) {
-      cf = 0u;
-      hf = tw = NONE;
-    } else {
-      cf = cfv[node];
-      hf = hfv[node];
-      tw = resolve(ntw[node]);
-    }
-  };
   for (const Edge& e : edges) {
     uint64_t i = edge_slot(e.parent, e.tok, ecap - 1);
     while (eslots[SLOT_U4 * i].z != NONE) i = (i + 1) & (ecap - 1);
-    const uint32_t c = e.child, p = pchild[c], pp = p ? pchild[p] : 0u;
-    uint32_t pcf, phf, ptw, ppcf, pphf, pptw;
-    pinfo(p, pcf, phf, ptw);
-    pinfo(pp, ppcf, pphf, pptw);
+    const uint32_t c = e.child, p = pchild[c];
     uint4* sl = &eslots[SLOT_U4 * i];
     sl[0] = make_uint4((uint32_t)e.tok, (uint32_t)(e.tok >> 32), e.parent, cfv[c]);
-    sl[1] = make_uint4(hfv[c], resolve(ntw[c]), resolve(ntn[c]), pcf);
-    sl[2] = make_uint4(phf, ptw, ppcf, pphf);
-    sl[3] = make_uint4(pptw, 0u, 0u, 0u);
+    sl[1] = make_uint4(hfv[c], resolve(ntw[c]), p ? cfv[p] : 0u, p ? hfv[p] : NONE);
   }
-  uint32_t root_q[6];
-  {
-    const uint32_t p = pchild[0], pp = p ? pchild[p] : 0u;
-    pinfo(p, root_q[0], root_q[1], root_q[2]);
-    pinfo(pp, root_q[3], root_q[4], root_q[5]);
-  }
+  std::vector<uint32_t> tn_of(n_nodes);
+  for (size_t i = 0; i < n_nodes; ++i) tn_of[i] = resolve(ntn[i]);
+  const uint32_t root_p = pchild[0];
 
   // ---- exact route keys ----
   uint64_t n_route = 0;
@@ -472,6 +454,7 @@ int commit_locked(emqxgm* h) {
   DevIndex nx;
   if ((rc = dev_upload(h, nbufs, eslots, &nx.edges)) ||
       (rc = dev_upload(h, nbufs, multi, &nx.multi)) ||
+      (rc = dev_upload(h, nbufs, tn_of, &nx.tn_of)) ||
       (rc = dev_upload(h, nbufs, fvbits, &nx.fvbits)) ||
       (rc = dev_upload(h, nbufs, xslots, &nx.exact))) {
     free_bufs(nbufs);
@@ -481,7 +464,8 @@ int commit_locked(emqxgm* h) {
   nx.xmask = xcap - 1;
   nx.root_cf = cfv[0];
   nx.root_hf = hfv[0];
-  for (int q = 0; q < 6; ++q) nx.root_q[q] = root_q[q];
+  nx.root_pcf = root_p ? cfv[root_p] : 0u;
+  nx.root_phf = root_p ? hfv[root_p] : NONE;
   nx.fbytes = (const uint8_t*)h->d_pool.p;
   nx.foff = (const uint64_t*)h->d_foff.p;
   nx.fver = (const uint4*)h->d_fver.p;
@@ -508,7 +492,8 @@ int commit_locked(emqxgm* h) {
   h->st.edge_slots = ecap;
   h->st.exact_slots = xcap * XBUCKET;
   h->st.max_depth = max_depth;
-  h->st.device_bytes = ecap * SLOT_U4 * 16 + xcap * XBUCKET * 16 + multi.size() * 4 + h->pool.size() +
+  h->st.device_bytes = ecap * SLOT_U4 * 16 + xcap * XBUCKET * 16 + multi.size() * 4 +
+                       n_nodes * 4 + h->pool.size() +
                        (nf + 1) * 8 + nf * VREC;
   return 0;
 }
@@ -551,9 +536,7 @@ int ensure_scratch(emqxgm* h, uint32_t n, uint64_t words, uint32_t pairs) {
       (rc = dev_alloc(h, (void**)&s.row2, (size_t)(ncap + 1) * 4)) ||
       (rc = dev_alloc(h, (void**)&s.rej, (size_t)ncap * 4)) ||
       (rc = dev_alloc(h, (void**)&s.exact_id, (size_t)ncap * 4)) ||
-      (rc = dev_alloc(h, (void**)&s.pt, (size_t)pcap * 4)) ||
-      (rc = dev_alloc(h, (void**)&s.pf, (size_t)pcap * 4)) ||
-      (rc = dev_alloc(h, (void**)&s.pr, (size_t)pcap * 4)) ||
+      (rc = dev_alloc(h, (void**)&s.stg, (size_t)pcap * 16)) ||
       (rc = dev_alloc(h, (void**)&s.out, (size_t)pcap * 4)) ||
       (rc = dev_alloc(h, (void**)&s.out2, (size_t)pcap * 4)) ||
       (rc = dev_alloc(h, (void**)&s.scan_tmp, (size_t)stw * 4)) ||
@@ -607,7 +590,8 @@ int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_
     if (h->ix.trie_empty) {
       HIPCHK(h, hipMemsetAsync(s.row, 0, (size_t)(n + 1) * 4, st));
     } else {
-      HIPCHK(h, hipMemsetAsync(s.rej, 0, (size_t)n * 4, st));
+      // per-topic reject counts: only the verification passes write (and then read) them
+      if (h->ix.needs_verify || legacy) HIPCHK(h, hipMemsetAsync(s.rej, 0, (size_t)n * 4, st));
       if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[1], st));
       HIPCHK(h, launch_walk(h->ix, s, n, h->geom, st, census ? s.census : nullptr,
                             h->walk_spill));

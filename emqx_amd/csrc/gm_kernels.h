@@ -11,7 +11,8 @@ struct DevIndex {
   uint64_t emask = 0;             // slot capacity - 1
   const uint32_t* multi = nullptr;  // [count, fid...] lists
   uint32_t root_cf = 0, root_hf = 0xFFFFFFFFu;
-  uint32_t root_q[6] = {0u, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0xFFFFFFFFu, 0xFFFFFFFFu};  // p, pp
+  uint32_t root_pcf = 0, root_phf = 0xFFFFFFFFu;  // root's '+' child (cf 0: none)
+  const uint32_t* tn_of = nullptr;  // per node: non-wildcard trie keys ending there
   const uint4* exact = nullptr;   // exact buckets of XBUCKET {hash.lo, hash.hi, fid, len}
   uint64_t xmask = 0;             // bucket count - 1
   const uint8_t* fbytes = nullptr;  // filter string pool
@@ -39,9 +40,7 @@ struct Scratch {
   uint32_t* rej = nullptr;    // [n]   rejected pairs per topic
   uint32_t* exact_id = nullptr;  // [n]
   uint32_t p_cap = 0;   // pair staging capacity
-  uint32_t* pt = nullptr;     // staged pair: topic
-  uint32_t* pf = nullptr;     // staged pair: filter
-  uint32_t* pr = nullptr;     // staged pair: rank within topic (bit 31 = rejected)
+  uint4* stg = nullptr;       // staged pairs {topic (NONE: unused), filter, rank | REJ_BIT, 0}
   uint32_t o_cap = 0;
   uint32_t* out = nullptr;    // [pairs] CSR filter ids
   uint32_t* out2 = nullptr;   // legacy fix-up target

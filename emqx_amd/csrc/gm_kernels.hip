@@ -169,7 +169,7 @@ WalkGeom walk_geometry(int device, uint32_t wg_per_cu) {
   // default 3 x 256-thread workgroups per CU: the walk is bounded by the random line rate of
   // HBM/MALL (tools/gather_bench: ~54 G lines/s), and more resident waves only thrash the L2
   // (measured sweep in profiles/r01/sweep_v3.txt)
-  g.blocks = (uint32_t)cus * (wg_per_cu ? wg_per_cu : 3u);
+  g.blocks = (uint32_t)cus * (wg_per_cu ? wg_per_cu : 4u);
   g.lanes = g.blocks * WG;
   return g;
 }
@@ -218,13 +218,13 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   a.multi = ix.multi;
   a.root_cf = ix.root_cf;
   a.root_hf = ix.root_hf;
-  for (int q = 0; q < 6; ++q) a.root_q[q] = ix.root_q[q];
+  a.root_pcf = ix.root_pcf;
+  a.root_phf = ix.root_phf;
+  a.tn_of = ix.tn_of;
   a.n = n;
   a.ctl = sc.ctl;
   a.cnt = sc.cnt;
-  a.pt = sc.pt;
-  a.pf = sc.pf;
-  a.pr = sc.pr;
+  a.stg = sc.stg;
   a.pcap = sc.p_cap;
   a.spill = sc.spill;
   a.spill_items = sc.spill_items;
@@ -251,9 +251,7 @@ hipError_t launch_verify(const uint8_t* bytes, const uint32_t* off, const DevInd
   a.foff = ix.foff;
   a.fver = ix.fver;
   a.fvbits = ix.fvbits;
-  a.pt = sc.pt;
-  a.pf = sc.pf;
-  a.pr = sc.pr;
+  a.stg = sc.stg;
   a.pcap = sc.p_cap;
   a.cnt = sc.cnt;
   a.rej = sc.rej;
@@ -267,9 +265,7 @@ hipError_t launch_verify(const uint8_t* bytes, const uint32_t* off, const DevInd
 hipError_t launch_scatter(Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_t s) {
   (void)n;
   ScatterArgs a;
-  a.pt = sc.pt;
-  a.pf = sc.pf;
-  a.pr = sc.pr;
+  a.stg = sc.stg;
   a.pcap = sc.p_cap;
   a.row = sc.row;
   a.rej = sc.rej;
@@ -291,9 +287,7 @@ hipError_t launch_verify_scatter(const uint8_t* bytes, const uint32_t* off, cons
   a.fbytes = ix.fbytes;
   a.foff = ix.foff;
   a.fvbits = ix.fvbits;
-  a.pt = sc.pt;
-  a.pf = sc.pf;
-  a.pr = sc.pr;
+  a.stg = sc.stg;
   a.pcap = sc.p_cap;
   a.row = sc.row;
   a.out = sc.out;
