@@ -153,11 +153,10 @@ def main():
     launches = s1["walk_launches"] - s0["walk_launches"]
     walk_ms = (s1["walk_ms"] - s0["walk_ms"]) / max(1, launches)
     pipe_ms = (s1["total_ms"] - s0["total_ms"]) / max(1, launches)
-    # algorithmic bytes of one k_walk launch (DESIGN.md "Roofline"): per topic a 16-B record,
-    # the next-level token hashes (4 B per level), 3 x 16-B edge probes per matched trie state
-    # (SURVEY 8d's 48*S(t)), and a 12-B staged (topic, filter, rank) triple per match; plus 4 B
-    # of per-topic count.
-    walk_bytes = (16 + 4) * w.nt + 4 * census["words"] + 48 * census["states"] + 12 * census["pairs"]
+    # algorithmic bytes of one k_walk launch (DESIGN.md "Roofline"): per topic its 64-B record
+    # (header + level tokens) and a 4-B match count, 3 x 16-B edge probes per matched trie
+    # state (SURVEY 8d's 48*S(t)), and a 16-B staged (topic, filter, rank) record per match.
+    walk_bytes = (64 + 4) * w.nt + 48 * census["states"] + 16 * census["pairs"]
     achieved = walk_bytes / (walk_ms * 1e-3) / 1e9 if walk_ms > 0 else 0.0
     topics_total = (w.nt * world) if args.shard == "topics" else w.nt
     value = topics_total / (elapsed / args.steps)

@@ -47,8 +47,11 @@ __global__ __launch_bounds__(256) void k_gather(const uint4* __restrict__ tab, u
 }
 
 int main(int argc, char** argv) {
+  // usage: gather_bench [table_MiB=2048] [wg_per_cu=8] [width_16B_units=0 (all)] [depth=0 (all)]
   const uint64_t mb = argc > 1 ? atoll(argv[1]) : 2048;
   const int wgpc = argc > 2 ? atoi(argv[2]) : 8;
+  const int only_w = argc > 3 ? atoi(argv[3]) : 0;
+  const int only_d = argc > 4 ? atoi(argv[4]) : 0;
   hipDeviceProp_t p;
   CHK(hipGetDeviceProperties(&p, 0));
   const uint64_t bytes = mb << 20;
@@ -64,7 +67,9 @@ int main(int argc, char** argv) {
   const int rounds = 64;
   printf("table %llu MiB, %d CUs x %d WG, %d rounds\n", (unsigned long long)mb, p.multiProcessorCount, wgpc, rounds);
   for (int W : {1, 2, 4}) {
+    if (only_w && W != only_w) continue;
     for (int depth : {1, 2, 4}) {
+      if (only_d && depth != only_d) continue;
       const uint64_t nslots = bytes / (16ull * W);
       for (int rep = 0; rep < 2; ++rep) {
         CHK(hipEventRecord(a));
