@@ -86,7 +86,12 @@ GM_HD uint64_t key_hash(const uint8_t* p, uint32_t len, uint64_t mask) {
 //         filters, its own '+' child) comes from the (C, '+') slot when the walk needs it.
 // Non-wildcard trie keys ending at a node (only single-level '$' topics read them,
 // emqx_trie.erl:287) live in a per-node side array.  An empty slot has parent == NONE.
+// Slots come in 64-B buckets of EBUCKET (one line: a probe loads and checks both slots, so a
+// collision inside the bucket costs no extra round trip); an edge goes to the first free slot
+// of its home bucket (edge_slot) or of the buckets after it, and a lookup stops at a bucket
+// with a free slot.
 constexpr uint32_t SLOT_U4 = 2;
+constexpr uint32_t EBUCKET = 2;
 constexpr uint32_t CF_ID_BITS = 27;
 constexpr uint32_t CF_ID_MASK = (1u << CF_ID_BITS) - 1;
 constexpr uint32_t MAX_NODES = CF_ID_MASK;

@@ -391,13 +391,22 @@ int commit_locked(emqxgm* h) {
   std::vector<uint32_t> pchild(n_nodes, 0u);
   for (const Edge& e : edges)
     if (e.tok == PLUS_TOK) pchild[e.parent] = e.child;
-  // 32-B slots (gm_common.h "edge slots"); load factor <= 1/2
-  const uint64_t ecap = pow2_at_least(std::max<uint64_t>(64, edges.size() * 2));
+  // 32-B slots in 64-B buckets (gm_common.h "edge slots"); load factor <= 1/2
+  const uint64_t ecap = pow2_at_least(std::max<uint64_t>(64, edges.size() * 2));  // slots
+  const uint64_t nbk = ecap / EBUCKET;
   std::vector<uint4> eslots(SLOT_U4 * ecap, make_uint4(0u, 0u, 0u, 0u));
   for (uint64_t i = 0; i < ecap; ++i) eslots[SLOT_U4 * i] = make_uint4(0u, 0u, NONE, 0u);
   for (const Edge& e : edges) {
-    uint64_t i = edge_slot(e.parent, e.tok, ecap - 1);
-    while (eslots[SLOT_U4 * i].z != NONE) i = (i + 1) & (ecap - 1);
+    uint64_t b = edge_slot(e.parent, e.tok, nbk - 1), i;
+    for (;;) {
+      uint32_t j = 0;
+      while (j < EBUCKET && eslots[SLOT_U4 * (b * EBUCKET + j)].z != NONE) ++j;
+      if (j < EBUCKET) {
+        i = b * EBUCKET + j;
+        break;
+      }
+      b = (b + 1) & (nbk - 1);
+    }
     const uint32_t c = e.child, p = pchild[c];
     uint4* sl = &eslots[SLOT_U4 * i];
     sl[0] = make_uint4((uint32_t)e.tok, (uint32_t)(e.tok >> 32), e.parent, cfv[c]);
@@ -460,7 +469,7 @@ int commit_locked(emqxgm* h) {
     free_bufs(nbufs);
     return rc;
   }
-  nx.emask = ecap - 1;
+  nx.emask = nbk - 1;
   nx.xmask = xcap - 1;
   nx.root_cf = cfv[0];
   nx.root_hf = hfv[0];

@@ -8,7 +8,7 @@ namespace gm {
 // Committed device index (all pointers are device memory).
 struct DevIndex {
   const uint4* edges = nullptr;   // SLOT_U4 x uint4 per slot (gm_common.h "edge slots")
-  uint64_t emask = 0;             // slot capacity - 1
+  uint64_t emask = 0;             // bucket count - 1
   const uint32_t* multi = nullptr;  // [count, fid...] lists
   uint32_t root_cf = 0, root_hf = 0xFFFFFFFFu;
   uint32_t root_pcf = 0, root_phf = 0xFFFFFFFFu;  // root's '+' child (cf 0: none)
