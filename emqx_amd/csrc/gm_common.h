@@ -92,6 +92,7 @@ GM_HD uint64_t key_hash(const uint8_t* p, uint32_t len, uint64_t mask) {
 // with a free slot.
 constexpr uint32_t SLOT_U4 = 2;
 constexpr uint32_t EBUCKET = 2;
+constexpr uint32_t EDGE_SLACK = 4;  // slots >= 4 x edges (load <= 1/4): fewer bucket overflows
 constexpr uint32_t CF_ID_BITS = 27;
 constexpr uint32_t CF_ID_MASK = (1u << CF_ID_BITS) - 1;
 constexpr uint32_t MAX_NODES = CF_ID_MASK;

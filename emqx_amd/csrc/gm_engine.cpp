@@ -392,7 +392,7 @@ int commit_locked(emqxgm* h) {
   for (const Edge& e : edges)
     if (e.tok == PLUS_TOK) pchild[e.parent] = e.child;
   // 32-B slots in 64-B buckets (gm_common.h "edge slots"); load factor <= 1/2
-  const uint64_t ecap = pow2_at_least(std::max<uint64_t>(64, edges.size() * 2));  // slots
+  const uint64_t ecap = pow2_at_least(std::max<uint64_t>(64, edges.size() * EDGE_SLACK));  // slots
   const uint64_t nbk = ecap / EBUCKET;
   std::vector<uint4> eslots(SLOT_U4 * ecap, make_uint4(0u, 0u, 0u, 0u));
   for (uint64_t i = 0; i < ecap; ++i) eslots[SLOT_U4 * i] = make_uint4(0u, 0u, NONE, 0u);
