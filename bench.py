@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-route-keys", action="store_true",
+                    help="experiment: trie only (no exact route-key table)")
     ap.add_argument("--topic-order", choices=["as-is", "xcd", "sorted"], default="as-is",
                     help="experiment: permute the batch (outside the timed region) so that topics "
                          "of one first-two-level prefix group share an XCD shard, or fully sorted")
@@ -93,7 +95,8 @@ def main():
         mine = np.arange(w.nf)
     fb, fo = _subset(w, mine)
     wild = w.fwild[mine].astype(bool)
-    eng.route_ref_many(fb, fo)
+    if not args.no_route_keys:
+        eng.route_ref_many(fb, fo)
     wb, wo = _subset_packed(fb, fo, np.nonzero(wild)[0])
     eng.trie_insert_many(wb, wo)
     eng.commit()
