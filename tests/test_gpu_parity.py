@@ -306,6 +306,65 @@ def test_cfg3_sample_at_1m_filters(emqx):
     _assert_engine_equals_ref(eng, ref, None, w.tbytes, w.toff)
 
 
+def _sample_packed(w, idx):
+    """Topics idx of workload w, packed (bytes, u32 offsets)."""
+    lens = (w.toff[idx + 1] - w.toff[idx]).astype(np.int64)
+    off = np.zeros(len(idx) + 1, np.uint32)
+    np.cumsum(lens, out=off[1:])
+    starts = w.toff[idx].astype(np.int64)
+    pos = np.repeat(starts - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(lens.sum())
+    return w.tbytes[pos], off
+
+
+def _rows_unique(res):
+    """No (topic, filter) pair twice in the CSR result (the trie returns sets)."""
+    n = len(res.row_ptr) - 1
+    if res.filter_id.size == 0:
+        return True
+    t = np.repeat(np.arange(n, dtype=np.int64), np.diff(res.row_ptr.astype(np.int64)))
+    key = t * (1 << 32) + res.filter_id.astype(np.int64)
+    key.sort()
+    return bool((np.diff(key) != 0).all())
+
+
+def test_cfg3_full_size(emqx):
+    """BASELINE config 3 at its full size: 10M filters, the bench's 2M-topic batch.  The whole
+    batch runs on the device; every 40th topic (50k) is checked bit-exact against the oracle
+    (C++ restatement of emqx_trie match_compact), the rest by size-independent properties:
+    no duplicate pair in any row, counts consistent with the CSR, S(t) of the sample equal to
+    the oracle's trie-state count."""
+    import workloads
+    w = workloads.generate(3)
+    eng, ref = _load_both(emqx, w)
+    res = eng.match_packed(w.tbytes, w.toff)
+    assert int(res.row_ptr[-1]) == res.filter_id.size > w.nt
+    assert _rows_unique(res)
+    idx = np.arange(0, w.nt, 40)
+    sb, so = _sample_packed(w, idx)
+    row, ids, ex = ref.match(sb, so, threads=16)
+    for j, i in enumerate(idx):
+        got = np.sort(res.filter_id[res.row_ptr[i]:res.row_ptr[i + 1]])
+        assert np.array_equal(got, ids[row[j]:row[j + 1]]), (i, w.topic(int(i)))
+    assert np.array_equal(res.exact_id[idx], ex)
+    import torch
+    tb = torch.from_numpy(sb).cuda()
+    to = torch.from_numpy(so.view(np.int32)).cuda()
+    census = eng.walk_census(tb.data_ptr(), to.data_ptr(), len(idx), int(so[-1]))
+    assert census["pairs"] == int(row[-1])
+    assert census["states"] == int(ref.states(sb, so, threads=16).sum())
+
+
+def test_cfg4_exact_heavy_10m(emqx):
+    """BASELINE config 4's shape at 10M exact per-device keys + 100k wildcards (the full 100M
+    needs ~30 GB of host memory for the ordered-set oracle): the exact route-key table at scale
+    and the long-word (hashed token) verification path, bit-exact on a 100k-topic batch."""
+    import workloads
+    w = workloads.generate(4, 10_100_000, 100_000)
+    eng, ref = _load_both(emqx, w)
+    res = _assert_engine_equals_ref(eng, ref, None, w.tbytes, w.toff)
+    assert (res.exact_id != emqx.NONE).mean() > 0.85
+
+
 def test_cfg4_slice_long_words(emqx):
     """cfg4 shape (dev/{id:09}/state exact keys + wildcards): 9-byte levels get hashed tokens,
     so these pairs go through byte verification in production mode."""
