@@ -98,52 +98,74 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, u
   return woff + x - v;
 }
 
+// Thread-sequential tiles: thread i of a block owns items [16 i, 16 i + 16) of the block's
+// SCAN_TILE, read and written as four 16-B vectors (the arrays are 256-B aligned); a ragged
+// tail falls back to scalar accesses.
+__device__ __forceinline__ void load16(const uint32_t* in, uint64_t i0, uint32_t n, uint32_t v[16]) {
+  if (i0 + 16 <= n) {
+    const uint4* q = (const uint4*)(in + i0);
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint4 x = q[j];
+      v[4 * j] = x.x, v[4 * j + 1] = x.y, v[4 * j + 2] = x.z, v[4 * j + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) v[j] = (i0 + j < n) ? in[i0 + j] : 0u;
+  }
+}
+
 __global__ __launch_bounds__(WG) void k_scan_partials(const uint32_t* __restrict__ in, uint32_t n,
                                                       uint32_t* __restrict__ part) {
   __shared__ uint32_t s_w[WG / 64];
-  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
+  uint32_t v[16];
+  load16(in, (uint64_t)blockIdx.x * SCAN_TILE + 16ull * threadIdx.x, n, v);
   uint32_t acc = 0;
-  for (uint32_t j = 0; j < SCAN_ITEMS; ++j) {
-    const uint64_t i = base + (uint64_t)j * WG + threadIdx.x;
-    acc += (i < n) ? in[i] : 0u;
-  }
+#pragma unroll
+  for (uint32_t j = 0; j < 16; ++j) acc += v[j];
   uint32_t tot;
   block_excl_scan(acc, s_w, tot);
   if (threadIdx.x == 0) part[blockIdx.x] = tot;
 }
 
-__global__ __launch_bounds__(WG) void k_scan_top(uint32_t* __restrict__ part, uint32_t np,
-                                                 uint32_t* __restrict__ out_n,
-                                                 uint32_t* __restrict__ total_dst) {
-  __shared__ uint32_t s_w[WG / 64];
-  uint32_t carry = 0;
-  for (uint32_t b = 0; b < np; b += WG) {
-    const uint32_t i = b + threadIdx.x;
-    const uint32_t v = (i < np) ? part[i] : 0u;
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan(v, s_w, tot);
-    if (i < np) part[i] = carry + ex;
-    carry += tot;
-  }
-  if (threadIdx.x == 0) {
-    *out_n = carry;
-    if (total_dst) *total_dst = carry;
-  }
-}
-
+// Each block adds up the partials of the blocks before it itself (a few hundred words), so the
+// scan is two launches.  The last block writes the grand total to out_n (and total_dst).
 __global__ __launch_bounds__(WG) void k_scan_final(const uint32_t* __restrict__ in, uint32_t n,
-                                                   const uint32_t* __restrict__ part,
-                                                   uint32_t* __restrict__ out) {
+                                                   const uint32_t* __restrict__ part, uint32_t nb,
+                                                   uint32_t* __restrict__ out,
+                                                   uint32_t* __restrict__ out_n,
+                                                   uint32_t* __restrict__ total_dst) {
   __shared__ uint32_t s_w[WG / 64];
-  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
-  uint32_t carry = part[blockIdx.x];
-  for (uint32_t j = 0; j < SCAN_ITEMS; ++j) {
-    const uint64_t i = base + (uint64_t)j * WG + threadIdx.x;
-    const uint32_t v = (i < n) ? in[i] : 0u;
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan(v, s_w, tot);
-    if (i < n) out[i] = carry + ex;
-    carry += tot;
+  uint32_t pre = 0;
+  for (uint32_t i = threadIdx.x; i < blockIdx.x; i += WG) pre += part[i];
+  uint32_t carry;
+  block_excl_scan(pre, s_w, carry);  // carry = sum of part[0 .. blockIdx)
+  const uint64_t i0 = (uint64_t)blockIdx.x * SCAN_TILE + 16ull * threadIdx.x;
+  uint32_t v[16];
+  load16(in, i0, n, v);
+  uint32_t acc = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 16; ++j) acc += v[j];
+  uint32_t tot;
+  uint32_t x = carry + block_excl_scan(acc, s_w, tot);
+#pragma unroll
+  for (uint32_t j = 0; j < 16; ++j) {
+    const uint32_t e = x;
+    x += v[j];
+    v[j] = e;
+  }
+  if (i0 + 16 <= n) {
+    uint4* q = (uint4*)(out + i0);
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) q[j] = make_uint4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+  } else {
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j)
+      if (i0 + j < n) out[i0 + j] = v[j];
+  }
+  if (blockIdx.x == nb - 1 && threadIdx.x == 0) {
+    *out_n = carry + tot;
+    if (total_dst) *total_dst = carry + tot;
   }
 }
 
@@ -179,9 +201,15 @@ uint32_t scan_tmp_words(uint32_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 1
 hipError_t launch_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* tmp,
                        uint32_t* total_dst, hipStream_t s) {
   const uint32_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
-  if (nb > 0) hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(WG), 0, s, in, n, tmp);
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(WG), 0, s, tmp, nb, out + n, total_dst);
-  if (nb > 0) hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(WG), 0, s, in, n, tmp, out);
+  if (nb == 0) {
+    // empty input: out[0] = 0 (and the total) without a kernel
+    hipError_t e = hipMemsetAsync(out, 0, 4, s);
+    if (e == hipSuccess && total_dst) e = hipMemsetAsync(total_dst, 0, 4, s);
+    return e;
+  }
+  hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(WG), 0, s, in, n, tmp);
+  hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(WG), 0, s, in, n, tmp, nb, out, out + n,
+                     total_dst);
   return hipGetLastError();
 }
 
