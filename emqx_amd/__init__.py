@@ -2,12 +2,14 @@
 
 The product is ``libemqx_gpumatch.so`` (gfx950 HIP kernels + host index builder + C-ABI,
 ``include/emqx_gpumatch.h``).  This package is the host-side mirror of the reference's
-``emqx_trie`` / ``emqx_router`` modules over that library:
+``emqx_trie`` / ``emqx_router`` / ``emqx_broker`` (publish fan-out) modules over that library:
 
-    from emqx_amd import Trie, Router, Engine
+    from emqx_amd import Trie, Router, Broker, Engine
 """
-from .engine import NONE, DeviceResult, Engine, EngineError, MatchResult  # noqa: F401
+from .broker import Broker  # noqa: F401
+from .engine import NONE, DeviceResult, Engine, EngineError, MatchResult, PublishResult  # noqa: F401
 from .router import Router  # noqa: F401
 from .trie import Trie  # noqa: F401
 
-__all__ = ["Engine", "EngineError", "MatchResult", "DeviceResult", "Trie", "Router", "NONE"]
+__all__ = ["Engine", "EngineError", "MatchResult", "DeviceResult", "PublishResult", "Trie",
+           "Router", "Broker", "NONE"]

@@ -16,6 +16,8 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "../../include/emqx_gpumatch.h"
@@ -161,6 +163,15 @@ struct emqxgm {
   // ---- host outputs ----
   std::vector<uint64_t> h_row;
   std::vector<uint32_t> h_fid, h_exact, h_row32, h_fid_tmp;
+
+  // ---- publish fan-out state (host registry; device tables built at commit) ----
+  std::unordered_map<uint32_t, std::vector<std::pair<uint32_t, uint32_t>>> rdest;  // (node, group)
+  std::unordered_map<uint32_t, std::vector<uint32_t>> lsubs;  // local subscribers per filter
+  uint32_t local_node = NONE;
+  FanScratch fs;
+  std::vector<DevBuf> fan_bufs, fan_out_bufs;
+  std::vector<uint64_t> h_rp, h_dp;
+  std::vector<uint32_t> h_rf, h_rd, h_df, h_ds, h_tmp32;
 
   bool profiling = false;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -458,9 +469,53 @@ int commit_locked(emqxgm* h) {
                           h->fver_host.size())))
     return rc;
 
+  // ---- publish fan-out tables (gm_fanout.inc): per filter id, its aggre/1 entries (plain
+  // node dests, then each group once: emqx_broker.erl:284-300) and, when it routes to the
+  // local node, its local subscribers (dispatch/2, :326-355) ----
+  std::vector<uint32_t> rt_off, rt_dst, dl_off, dl_sub;
+  const bool fan = !h->rdest.empty() || !h->lsubs.empty();
+  if (fan) {
+    rt_off.assign(nf + 1, 0u);
+    dl_off.assign(nf + 1, 0u);
+    std::vector<uint32_t> groups;
+    for (uint32_t id = 0; id < nf; ++id) {
+      rt_off[id + 1] = rt_off[id];
+      dl_off[id + 1] = dl_off[id];
+      auto it = h->rdest.find(id);
+      if (it == h->rdest.end()) continue;
+      bool local = false;
+      groups.clear();
+      for (const auto& d : it->second) {
+        if (d.second == NONE) {
+          rt_dst.push_back(d.first);
+          local = local || d.first == h->local_node;
+        } else {
+          groups.push_back(EMQXGM_DEST_GROUP | d.second);
+        }
+      }
+      std::sort(groups.begin(), groups.end());
+      groups.erase(std::unique(groups.begin(), groups.end()), groups.end());
+      rt_dst.insert(rt_dst.end(), groups.begin(), groups.end());
+      rt_off[id + 1] = (uint32_t)rt_dst.size();
+      if (local) {
+        auto sit = h->lsubs.find(id);
+        if (sit != h->lsubs.end()) dl_sub.insert(dl_sub.end(), sit->second.begin(), sit->second.end());
+        dl_off[id + 1] = (uint32_t)dl_sub.size();
+      }
+    }
+  }
+
   // ---- upload and swap ----
   std::vector<DevBuf> nbufs;
   DevIndex nx;
+  if (fan && ((rc = dev_upload(h, nbufs, rt_off, &nx.rt_off)) ||
+              (rc = dev_upload(h, nbufs, rt_dst, &nx.rt_dst)) ||
+              (rc = dev_upload(h, nbufs, dl_off, &nx.dl_off)) ||
+              (rc = dev_upload(h, nbufs, dl_sub, &nx.dl_sub)))) {
+    free_bufs(nbufs);
+    return rc;
+  }
+  nx.fan_nf = fan ? (uint32_t)nf : 0u;
   if ((rc = dev_upload(h, nbufs, eslots, &nx.edges)) ||
       (rc = dev_upload(h, nbufs, multi, &nx.multi)) ||
       (rc = dev_upload(h, nbufs, tn_of, &nx.tn_of)) ||
@@ -698,6 +753,59 @@ int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_
   return 0;
 }
 
+int fan_alloc(emqxgm* h, std::vector<DevBuf>& keep, uint32_t** p, size_t words) {
+  HIPCHK(h, hipMalloc((void**)p, std::max<size_t>(words * 4, 16)));
+  DevBuf b;
+  b.p = *p;
+  b.bytes = words * 4;
+  keep.push_back(b);
+  return 0;
+}
+
+// Publish fan-out over the match result of the last run_device pass (n topics): counts, two
+// scans, then (outputs grown to the totals) the fill.  Leaves the results in h->fs.
+int run_fanout(emqxgm* h, uint32_t n, uint32_t* n_routes, uint32_t* n_deliv) {
+  FanScratch& f = h->fs;
+  Scratch& s = h->sc;
+  hipStream_t st = h->stream;
+  int rc = 0;
+  if (n > f.n_cap || !f.cr) {
+    HIPCHK(h, hipStreamSynchronize(st));
+    free_bufs(h->fan_bufs);
+    const uint32_t cap = std::max(n, f.n_cap);
+    if ((rc = fan_alloc(h, h->fan_bufs, &f.cr, cap)) || (rc = fan_alloc(h, h->fan_bufs, &f.cd, cap)) ||
+        (rc = fan_alloc(h, h->fan_bufs, &f.rp, (size_t)cap + 1)) ||
+        (rc = fan_alloc(h, h->fan_bufs, &f.dp, (size_t)cap + 1)))
+      return rc;
+    f.n_cap = cap;
+  }
+  if (n == 0) {
+    *n_routes = *n_deliv = 0;
+    return 0;
+  }
+  HIPCHK(h, launch_fanout(h->ix, s, f, n, false, st));
+  HIPCHK(h, launch_scan(f.cr, f.rp, n, s.scan_tmp, s.ctl + CTL_FAN_R, st));
+  HIPCHK(h, launch_scan(f.cd, f.dp, n, s.scan_tmp, s.ctl + CTL_FAN_D, st));
+  HIPCHK(h, hipMemcpyAsync(s.ctl_host + CTL_FAN_R, s.ctl + CTL_FAN_R, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(h, hipStreamSynchronize(st));
+  const uint32_t nr = s.ctl_host[CTL_FAN_R], nd = s.ctl_host[CTL_FAN_D];
+  if (nr > f.r_cap || nd > f.d_cap || !f.o_rf) {
+    free_bufs(h->fan_out_bufs);
+    const uint32_t rc_ = std::max(nr, f.r_cap), dc = std::max(nd, f.d_cap);
+    if ((rc = fan_alloc(h, h->fan_out_bufs, &f.o_rf, rc_)) ||
+        (rc = fan_alloc(h, h->fan_out_bufs, &f.o_rd, rc_)) ||
+        (rc = fan_alloc(h, h->fan_out_bufs, &f.o_df, dc)) ||
+        (rc = fan_alloc(h, h->fan_out_bufs, &f.o_ds, dc)))
+      return rc;
+    f.r_cap = rc_;
+    f.d_cap = dc;
+  }
+  HIPCHK(h, launch_fanout(h->ix, s, f, n, true, st));
+  *n_routes = nr;
+  *n_deliv = nd;
+  return 0;
+}
+
 int ensure_input(emqxgm* h, uint64_t bytes, uint64_t offs) {
   if (bytes > h->in_bytes_cap) {
     if (h->d_in_bytes) (void)hipFree(h->d_in_bytes);
@@ -767,6 +875,8 @@ void emqxgm_destroy(emqxgm_t* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   free_bufs(h->ix_bufs);
   free_bufs(h->sc_bufs);
+  free_bufs(h->fan_bufs);
+  free_bufs(h->fan_out_bufs);
   if (h->sc.ctl_host) (void)hipHostFree(h->sc.ctl_host);
   if (h->d_pool.p) (void)hipFree(h->d_pool.p);
   if (h->d_foff.p) (void)hipFree(h->d_foff.p);
@@ -837,6 +947,95 @@ int emqxgm_route_unref(emqxgm_t* h, const uint8_t* filter, uint32_t len) {
     --h->n_route_pending;
     h->dirty = true;
   }
+  return 0;
+}
+
+// ---- publish fan-out registry ----
+
+int emqxgm_route_add(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t node,
+                     uint32_t group) {
+  if (!h || (!filter && len) || len > 65535 || node == NONE ||
+      (group != NONE && (group & EMQXGM_DEST_GROUP)))
+    return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (h->filters.size() >= 0x7FFFFFFFu) return -E2BIG;
+  const uint32_t i = find_id(h, filter, len, true);
+  auto& v = h->rdest[i];
+  const std::pair<uint32_t, uint32_t> d(node, group);
+  if (std::find(v.begin(), v.end(), d) != v.end()) return 0;  // already routed
+  v.push_back(d);
+  if (h->filters[i].route_refs++ == 0) {
+    ++h->n_route_pending;
+    // insert_trie_route: the first route of a wildcard filter (emqx_router_utils.erl:34-39)
+    if (is_wild(filter, len) && !h->filters[i].in_trie) {
+      h->filters[i].in_trie = 1;
+      ++h->n_trie_pending;
+    }
+  }
+  h->dirty = true;
+  return 0;
+}
+
+int emqxgm_route_delete(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t node,
+                        uint32_t group) {
+  if (!h || (!filter && len)) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  const uint32_t i = find_id(h, filter, len, false);
+  if (i == NONE) return 0;
+  auto it = h->rdest.find(i);
+  if (it == h->rdest.end()) return 0;
+  auto& v = it->second;
+  auto p = std::find(v.begin(), v.end(), std::make_pair(node, group));
+  if (p == v.end()) return 0;  // absent route: no-op
+  v.erase(p);
+  if (v.empty()) h->rdest.erase(it);
+  if (h->filters[i].route_refs && --h->filters[i].route_refs == 0) {
+    --h->n_route_pending;
+    // delete_trie_route: the last route of a wildcard filter (emqx_router_utils.erl:57-71)
+    if (is_wild(filter, len) && h->filters[i].in_trie) {
+      h->filters[i].in_trie = 0;
+      --h->n_trie_pending;
+    }
+  }
+  h->dirty = true;
+  return 0;
+}
+
+int emqxgm_set_local_node(emqxgm_t* h, uint32_t node) {
+  if (!h) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (h->local_node != node) {
+    h->local_node = node;
+    h->dirty = true;
+  }
+  return 0;
+}
+
+int emqxgm_subscriber_add(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t sub) {
+  if (!h || (!filter && len) || len > 65535) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (h->filters.size() >= 0x7FFFFFFFu) return -E2BIG;
+  const uint32_t i = find_id(h, filter, len, true);
+  auto& v = h->lsubs[i];
+  if (std::find(v.begin(), v.end(), sub) == v.end()) {
+    v.push_back(sub);
+    h->dirty = true;
+  }
+  return 0;
+}
+
+int emqxgm_subscriber_delete(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t sub) {
+  if (!h || (!filter && len)) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  const uint32_t i = find_id(h, filter, len, false);
+  if (i == NONE) return 0;
+  auto it = h->lsubs.find(i);
+  if (it == h->lsubs.end()) return 0;
+  auto p = std::find(it->second.begin(), it->second.end(), sub);
+  if (p == it->second.end()) return 0;
+  it->second.erase(p);
+  if (it->second.empty()) h->lsubs.erase(it);
+  h->dirty = true;
   return 0;
 }
 
@@ -973,6 +1172,73 @@ int emqxgm_match_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offset
   out->row_ptr = h->h_row.data();
   out->filter_id = h->h_fid.data();
   out->exact_id = h->h_exact.data();
+  return 0;
+}
+
+int emqxgm_publish_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets, uint32_t n,
+                         emqxgm_publish_out* out) {
+  if (!h || !out || (!offsets && n)) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
+  h->h_rp.assign((size_t)n + 1, 0);
+  h->h_dp.assign((size_t)n + 1, 0);
+  h->h_rf.clear();
+  h->h_rd.clear();
+  h->h_df.clear();
+  h->h_ds.clear();
+  std::vector<uint32_t> loff;
+  for (uint32_t i0 = 0; i0 < n; i0 += h->cfg.batch_max) {
+    const uint32_t i1 = std::min<uint64_t>((uint64_t)i0 + h->cfg.batch_max, n);
+    const uint32_t m = i1 - i0;
+    const uint64_t b0 = offsets[i0], b1 = offsets[i1];
+    if (b1 < b0) return -EINVAL;
+    loff.resize((size_t)m + 1);
+    for (uint32_t i = 0; i <= m; ++i) {
+      if (offsets[i0 + i] < b0 || (i && offsets[i0 + i] < offsets[i0 + i - 1])) return -EINVAL;
+      loff[i] = (uint32_t)(offsets[i0 + i] - b0);
+    }
+    int rc = ensure_input(h, std::max<uint64_t>(b1 - b0, 1), (uint64_t)m + 1);
+    if (rc) return rc;
+    if (b1 > b0)
+      HIPCHK(h, hipMemcpyAsync(h->d_in_bytes, bytes + b0, b1 - b0, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->d_in_off, loff.data(), ((size_t)m + 1) * 4, hipMemcpyHostToDevice,
+                             h->stream));
+    uint32_t pairs = 0, nr = 0, nd = 0;
+    if ((rc = run_device(h, h->d_in_bytes, h->d_in_off, m, b1 - b0, &pairs)) ||
+        (rc = run_fanout(h, m, &nr, &nd)))
+      return rc;
+    const FanScratch& f = h->fs;
+    const uint64_t rbase = h->h_rf.size(), dbase = h->h_df.size();
+    h->h_rf.resize(rbase + nr);
+    h->h_rd.resize(rbase + nr);
+    h->h_df.resize(dbase + nd);
+    h->h_ds.resize(dbase + nd);
+    std::vector<uint32_t> rp(m + 1), dp(m + 1);
+    HIPCHK(h, hipMemcpyAsync(rp.data(), f.rp, ((size_t)m + 1) * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipMemcpyAsync(dp.data(), f.dp, ((size_t)m + 1) * 4, hipMemcpyDeviceToHost, h->stream));
+    if (nr) {
+      HIPCHK(h, hipMemcpyAsync(h->h_rf.data() + rbase, f.o_rf, (size_t)nr * 4, hipMemcpyDeviceToHost, h->stream));
+      HIPCHK(h, hipMemcpyAsync(h->h_rd.data() + rbase, f.o_rd, (size_t)nr * 4, hipMemcpyDeviceToHost, h->stream));
+    }
+    if (nd) {
+      HIPCHK(h, hipMemcpyAsync(h->h_df.data() + dbase, f.o_df, (size_t)nd * 4, hipMemcpyDeviceToHost, h->stream));
+      HIPCHK(h, hipMemcpyAsync(h->h_ds.data() + dbase, f.o_ds, (size_t)nd * 4, hipMemcpyDeviceToHost, h->stream));
+    }
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    for (uint32_t i = 0; i <= m; ++i) {
+      h->h_rp[i0 + i] = rbase + rp[i];
+      h->h_dp[i0 + i] = dbase + dp[i];
+    }
+  }
+  out->n = n;
+  out->n_routes = h->h_rf.size();
+  out->n_deliveries = h->h_df.size();
+  out->route_ptr = h->h_rp.data();
+  out->route_filter = h->h_rf.data();
+  out->route_dest = h->h_rd.data();
+  out->deliver_ptr = h->h_dp.data();
+  out->deliver_filter = h->h_df.data();
+  out->deliver_sub = h->h_ds.data();
   return 0;
 }
 

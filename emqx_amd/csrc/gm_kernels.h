@@ -13,6 +13,12 @@ struct DevIndex {
   uint32_t root_cf = 0, root_hf = 0xFFFFFFFFu;
   uint32_t root_pcf = 0, root_phf = 0xFFFFFFFFu;  // root's '+' child (cf 0: none)
   const uint32_t* tn_of = nullptr;  // per node: non-wildcard trie keys ending there
+  // publish fan-out tables (gm_fanout.inc), per filter id < fan_nf
+  const uint32_t* rt_off = nullptr;  // [fan_nf+1] aggre entries
+  const uint32_t* rt_dst = nullptr;
+  const uint32_t* dl_off = nullptr;  // [fan_nf+1] local deliveries
+  const uint32_t* dl_sub = nullptr;
+  uint32_t fan_nf = 0;
   const uint4* exact = nullptr;   // exact buckets of XBUCKET {hash.lo, hash.hi, fid, len}
   uint64_t xmask = 0;             // bucket count - 1
   const uint8_t* fbytes = nullptr;  // filter string pool
@@ -65,6 +71,8 @@ enum : int {
   CTL_NREJ = 5,       // rejected pairs appended to rlist
   CTL_LEGACY = 6,     // deferred scatter could not place rejects: re-run with the fix-up path
   CTL_ERR = 7,        // walk item stack outgrew its spill: re-run with a larger spill
+  CTL_FAN_R = 9,      // publish fan-out: aggre entries of the batch
+  CTL_FAN_D = 10,     //   local deliveries of the batch
   CTL_CLAIM0 = 16,    // walk topic-claim counters, one per shard, CTL_CLAIM_STRIDE apart
   CTL_N = 16 + 8 * 32
 };
@@ -102,6 +110,16 @@ uint32_t scan_tmp_words(uint32_t n);
 // deeper levels (wh, at off[t] + t + level), exact route-key ids (exact_id, NONE if absent)
 hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
                       Scratch& sc, hipStream_t s);
+
+// Per-batch scratch of the publish fan-out (gm_fanout.inc).
+struct FanScratch {
+  uint32_t n_cap = 0, r_cap = 0, d_cap = 0;
+  uint32_t *cr = nullptr, *cd = nullptr, *rp = nullptr, *dp = nullptr;
+  uint32_t *o_rf = nullptr, *o_rd = nullptr, *o_df = nullptr, *o_ds = nullptr;
+};
+// count pass (fill = false) or fill pass over the match result in sc (row, out, exact_id)
+hipError_t launch_fanout(const DevIndex& ix, const Scratch& sc, FanScratch& fs, uint32_t n,
+                         bool fill, hipStream_t s);
 
 // census != nullptr selects the diagnostic walk (adds to census[0..CENSUS_N)); spill selects
 // the variant whose probe-item stack continues in global memory (after an LDS overflow)

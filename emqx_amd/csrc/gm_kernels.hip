@@ -172,6 +172,7 @@ __global__ __launch_bounds__(WG) void k_scan_final(const uint32_t* __restrict__ 
 #include "gm_tok.inc"
 #include "gm_walk.inc"
 #include "gm_verify.inc"
+#include "gm_fanout.inc"
 
 uint32_t grid_for(uint64_t items, uint32_t cap_blocks) {
   uint64_t b = (items + WG - 1) / WG;
@@ -332,6 +333,34 @@ hipError_t launch_fixup(Scratch& sc, uint32_t n, hipStream_t s) {
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_compact_rows, dim3(grid_for(n, 4096)), dim3(WG), 0, s, sc.row, sc.out,
                      sc.row2, sc.out2, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_fanout(const DevIndex& ix, const Scratch& sc, FanScratch& fs, uint32_t n, bool fill,
+                         hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  FanArgs a;
+  a.n = n;
+  a.row = sc.row;
+  a.fid = sc.out;
+  a.exact_id = sc.exact_id;
+  a.rt_off = ix.rt_off;
+  a.rt_dst = ix.rt_dst;
+  a.dl_off = ix.dl_off;
+  a.dl_sub = ix.dl_sub;
+  a.nf = ix.fan_nf;
+  a.cr = fs.cr;
+  a.cd = fs.cd;
+  a.rp = fs.rp;
+  a.dp = fs.dp;
+  a.o_rf = fs.o_rf;
+  a.o_rd = fs.o_rd;
+  a.o_df = fs.o_df;
+  a.o_ds = fs.o_ds;
+  if (fill)
+    hipLaunchKernelGGL(k_fanout<true>, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_fanout<false>, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a);
   return hipGetLastError();
 }
 

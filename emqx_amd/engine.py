@@ -41,6 +41,14 @@ class _DevOut(C.Structure):
                 ("filter_id", C.c_void_p), ("exact_id", C.c_void_p), ("n_words", C.c_void_p)]
 
 
+class _PubOut(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("n_routes", C.c_uint64), ("n_deliveries", C.c_uint64),
+                ("route_ptr", C.POINTER(C.c_uint64)), ("route_filter", C.POINTER(C.c_uint32)),
+                ("route_dest", C.POINTER(C.c_uint32)), ("deliver_ptr", C.POINTER(C.c_uint64)),
+                ("deliver_filter", C.POINTER(C.c_uint32)),
+                ("deliver_sub", C.POINTER(C.c_uint32))]
+
+
 class _Stats(C.Structure):
     _fields_ = [("epoch", C.c_uint64), ("n_filters", C.c_uint64), ("n_trie_filters", C.c_uint64),
                 ("n_route_keys", C.c_uint64), ("n_nodes", C.c_uint64), ("n_edges", C.c_uint64),
@@ -75,6 +83,12 @@ SYMBOLS = {
     "emqxgm_match_batch": (C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(_Out)]),
     "emqxgm_match_device": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, C.POINTER(_DevOut)]),
     "emqxgm_walk_census": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, _U64P]),
+    "emqxgm_route_add": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "emqxgm_route_delete": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "emqxgm_set_local_node": (C.c_int, [_P, C.c_uint32]),
+    "emqxgm_subscriber_add": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint32]),
+    "emqxgm_subscriber_delete": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint32]),
+    "emqxgm_publish_batch": (C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(_PubOut)]),
     "emqxgm_set_profiling": (C.c_int, [_P, C.c_int]),
     "emqxgm_tune": (C.c_int, [_P, C.c_char_p, C.c_int64]),
     "emqxgm_get_stats": (C.c_int, [_P, C.POINTER(_Stats)]),
@@ -118,6 +132,30 @@ def pack(items: Sequence[bytes], off_dtype=np.uint64) -> Tuple[np.ndarray, np.nd
 
 def _ptr(a: np.ndarray):
     return a.ctypes.data_as(C.c_void_p) if a.size else C.c_void_p(0)
+
+
+DEST_GROUP = 0x80000000
+
+
+@dataclass
+class PublishResult:
+    """Host-resident result of publish_batch (emqx_broker:publish/1 over a batch): per topic
+    the aggre/1 entries (filter id, dest handle; DEST_GROUP bit = shared group) and the local
+    dispatches (filter id, subscriber handle)."""
+    route_ptr: np.ndarray      # uint64 [n+1]
+    route_filter: np.ndarray   # uint32
+    route_dest: np.ndarray     # uint32
+    deliver_ptr: np.ndarray    # uint64 [n+1]
+    deliver_filter: np.ndarray
+    deliver_sub: np.ndarray
+
+    def routes(self, i: int):
+        a, b = int(self.route_ptr[i]), int(self.route_ptr[i + 1])
+        return list(zip(self.route_filter[a:b].tolist(), self.route_dest[a:b].tolist()))
+
+    def deliveries(self, i: int):
+        a, b = int(self.deliver_ptr[i]), int(self.deliver_ptr[i + 1])
+        return list(zip(self.deliver_filter[a:b].tolist(), self.deliver_sub[a:b].tolist()))
 
 
 @dataclass
@@ -187,6 +225,40 @@ class Engine:
 
     def route_unref(self, f: bytes) -> None:
         self._check(self._lib.emqxgm_route_unref(self._h, f, len(f)), "route_unref")
+
+    # ---- publish fan-out registry (emqx_router do_add_route/do_delete_route, subscribers) ----
+    def route_add(self, f: bytes, node: int, group: int = NONE) -> None:
+        self._check(self._lib.emqxgm_route_add(self._h, f, len(f), node, group), "route_add")
+
+    def route_delete(self, f: bytes, node: int, group: int = NONE) -> None:
+        self._check(self._lib.emqxgm_route_delete(self._h, f, len(f), node, group), "route_delete")
+
+    def set_local_node(self, node: int) -> None:
+        self._check(self._lib.emqxgm_set_local_node(self._h, node), "set_local_node")
+
+    def subscriber_add(self, f: bytes, sub: int) -> None:
+        self._check(self._lib.emqxgm_subscriber_add(self._h, f, len(f), sub), "subscriber_add")
+
+    def subscriber_delete(self, f: bytes, sub: int) -> None:
+        self._check(self._lib.emqxgm_subscriber_delete(self._h, f, len(f), sub),
+                    "subscriber_delete")
+
+    def publish(self, topics: Sequence[bytes]) -> PublishResult:
+        buf, off = pack(list(topics), np.uint64)
+        off32 = np.ascontiguousarray(off, dtype=np.uint32)
+        n = len(off32) - 1
+        o = _PubOut()
+        self._check(self._lib.emqxgm_publish_batch(self._h, _ptr(buf), _ptr(off32), n,
+                                                   C.byref(o)), "publish_batch")
+
+        def arr(p, k, dt):
+            return np.ctypeslib.as_array(p, shape=(k,)).copy() if k else np.zeros(0, dt)
+        return PublishResult(arr(o.route_ptr, n + 1, np.uint64),
+                             arr(o.route_filter, o.n_routes, np.uint32),
+                             arr(o.route_dest, o.n_routes, np.uint32),
+                             arr(o.deliver_ptr, n + 1, np.uint64),
+                             arr(o.deliver_filter, o.n_deliveries, np.uint32),
+                             arr(o.deliver_sub, o.n_deliveries, np.uint32))
 
     def trie_insert_many(self, buf: np.ndarray, off: np.ndarray) -> np.ndarray:
         off = np.ascontiguousarray(off, dtype=np.uint64)

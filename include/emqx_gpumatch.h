@@ -19,6 +19,11 @@
  *                           tokenising per emqx_topic:words/1 (emqx_topic.erl:155-169)
  *   emqxgm_match_device  <- the same with topic bytes / results resident in HBM
  *   emqxgm_filter_bytes  <- filter id -> filter binary (the trie returns binaries)
+ *   emqxgm_route_add     <- emqx_router:do_add_route/2    apps/emqx/src/emqx_router.erl:124-138
+ *   emqxgm_route_delete  <- emqx_router:do_delete_route/2 apps/emqx/src/emqx_router.erl:171-179
+ *   emqxgm_subscriber_add/delete <- the local emqx_subscriber bag (emqx_broker.erl:150-214)
+ *   emqxgm_publish_batch <- emqx_broker:publish/1 -> route(aggre(match_routes(Topic)))
+ *                           apps/emqx/src/emqx_broker.erl:218-300, dispatch/2 :326-355
  *
  * Result semantics (bit-exact with the reference, SURVEY.md 8a/8a'):
  *   for topic t, trie row = { f in trie : emqx_trie:match(t) returns f }  (no duplicates;
@@ -50,6 +55,7 @@ extern "C" {
 #endif
 
 #define EMQXGM_NONE 0xFFFFFFFFu
+#define EMQXGM_DEST_GROUP 0x80000000u /* dest handle bit: a shared-subscription group */
 #define EMQXGM_ABI_VERSION 1
 
 typedef struct emqxgm emqxgm_t;
@@ -134,6 +140,43 @@ int emqxgm_match_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offset
  * bytes_len = offsets[n] (passed so the engine never has to read it back). */
 int emqxgm_match_device(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_offsets,
                         uint32_t n, uint64_t bytes_len, emqxgm_dev_out* out);
+
+/* ---- publish fan-out (emqx_broker.erl:218-355) -------------------------------------------
+ * Routes with dest identity: a plain route {Filter, Node} passes group = EMQXGM_NONE; a shared-
+ * subscription route {Filter, {Group, Node}} passes both (handles < 2^31, chosen by the caller).
+ * Like emqx_router:do_add_route/do_delete_route, the first route of a wildcard filter inserts it
+ * into the trie and its last one removes it, the route key exists while the filter has a route
+ * (the same refcount as emqxgm_route_ref), and adding an existing route or deleting an absent
+ * one is a no-op.  Visible after emqxgm_commit, like every mutation. */
+int emqxgm_route_add(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t node,
+                     uint32_t group);
+int emqxgm_route_delete(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t node,
+                        uint32_t group);
+/* node() of this broker: aggre entries {To, local_node} are dispatched to local subscribers. */
+int emqxgm_set_local_node(emqxgm_t* h, uint32_t node);
+/* The local subscriber bag (filter -> subscriber handle); duplicates / absent deletes: no-op. */
+int emqxgm_subscriber_add(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t sub);
+int emqxgm_subscriber_delete(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t sub);
+
+typedef struct emqxgm_publish_out { /* host-resident result of emqxgm_publish_batch */
+  uint32_t n;
+  uint64_t n_routes;              /* aggre entries of the whole batch */
+  uint64_t n_deliveries;          /* local dispatches of the whole batch */
+  const uint64_t* route_ptr;      /* [n+1] topic i's entries: [route_ptr[i], route_ptr[i+1]) */
+  const uint32_t* route_filter;   /* To of each entry (filter id) */
+  const uint32_t* route_dest;     /* node handle, or EMQXGM_DEST_GROUP | group handle */
+  const uint64_t* deliver_ptr;    /* [n+1] topic i's local dispatches */
+  const uint32_t* deliver_filter; /* the filter (To) a dispatch goes through */
+  const uint32_t* deliver_sub;    /* the subscriber it reaches */
+} emqxgm_publish_out;
+
+/* emqx_broker:publish/1 for a batch of topics: the aggre/1 entries of match_routes(Topic)
+ * (node dests as {To, Node}, shared dests as {To, Group} with each group once per filter) and
+ * the local dispatches of the entries {To, local_node} (every subscriber of To).  Entries of a
+ * topic come in match_routes order (exact key first, then the trie row); callers treat them as
+ * the set the reference's route/2 folds over. */
+int emqxgm_publish_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets, uint32_t n,
+                         emqxgm_publish_out* out);
 
 /* Diagnostic pass (instrumented walk kernel, not the production launch): runs the device
  * match and returns out[0] = trie states matched (SURVEY 8d S(t) summed over the batch),

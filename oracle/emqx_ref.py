@@ -448,3 +448,18 @@ def _erl_order(entry):
     (node, str here) sorts before a binary (group)."""
     to, x = entry
     return (to, (0, x.encode()) if isinstance(x, str) else (1, bytes(x)))
+
+
+def publish(router: "Router", topic: bytes, local_node: object,
+            subscribers: Dict[bytes, List[object]]) -> Tuple[list, list]:
+    """emqx_broker:publish/1 (emqx_broker.erl:218-232) as far as routing goes:
+    ``route(aggre(match_routes(Topic)), Delivery)`` (:262-282).  Returns the aggre/1 entries
+    and the local dispatches: every ``{To, Node}`` entry with ``Node =:= node()`` goes to
+    dispatch(To) = each subscriber of To (subscribers/1, :546-552); other nodes are forwarded to
+    and groups go to emqx_shared_sub (outside the node's own fan-out)."""
+    entries = aggre(router.match_routes(topic))
+    deliveries = []
+    for to, dest in entries:
+        if dest == local_node:
+            deliveries += [(to, s) for s in subscribers.get(to, [])]
+    return entries, deliveries

@@ -219,3 +219,23 @@ def test_aggre():
     assert R.aggre([(b"a", "n1")]) == [(b"a", "n1")]
     assert R.aggre([(b"a", ("g", "n1"))]) == [(b"a", "g")]
     assert R.aggre(routes) == [(b"a", "n1"), (b"b", "g")]
+
+
+def test_publish_oracle_fanout():
+    """oracle publish = route(aggre(match_routes(T))) with local dispatch
+    (emqx_broker.erl:218-300, 326-355): group dests collapse per filter, only {To, node()}
+    entries dispatch, a wildcard topic name keeps only its own exact routes."""
+    r = R.Router()
+    r.add_route(b"a/+", "n1")
+    r.add_route(b"a/+", "n2")
+    r.add_route(b"a/b", "n1")
+    r.add_route(b"a/#", (b"g", "n2"))
+    r.add_route(b"a/#", (b"g", "n3"))
+    subs = {b"a/+": ["s1", "s2"], b"a/b": ["s3"], b"a/#": ["x"]}
+    entries, deliv = R.publish(r, b"a/b", "n1", subs)
+    assert sorted(entries, key=repr) == sorted([(b"a/#", b"g"), (b"a/+", "n1"), (b"a/+", "n2"),
+                                               (b"a/b", "n1")], key=repr)
+    assert deliv == [(b"a/+", "s1"), (b"a/+", "s2"), (b"a/b", "s3")]
+    entries, deliv = R.publish(r, b"a/+", "n1", subs)
+    assert sorted(entries, key=repr) == sorted([(b"a/+", "n1"), (b"a/+", "n2")], key=repr)
+    assert R.publish(r, b"zz", "n1", subs) == ([], [])
