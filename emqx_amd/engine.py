@@ -185,6 +185,7 @@ class Engine:
     def __init__(self, device: int = 0, word_hash_bits: int = 0, full_hash_bits: int = 64,
                  batch_max: int = 0, walk_wg_per_cu: int = 0, reject_cap: int = 0):
         self._lib = lib()
+        self.device = device
         cfg = _Cfg(device, word_hash_bits, full_hash_bits, batch_max, walk_wg_per_cu, reject_cap)
         h = C.c_void_p()
         rc = self._lib.emqxgm_create(C.byref(cfg), C.byref(h))

@@ -75,6 +75,32 @@ class Trie:
         self._maybe_commit()
         return self.engine.match(topics)
 
+    # ---- the session trie (emqx_trie.erl:84-100, 117-119, 135-137, 151-153, 175-176): the same
+    # operations on a second table, used when persistent sessions are enabled
+    # (emqx_session_router.erl:147-159).  Here: a second engine index on the same device,
+    # created on first use. ----
+    def _session(self) -> "Trie":
+        s = getattr(self, "_session_trie", None)
+        if s is None:
+            s = self._session_trie = Trie(device=self.engine.device)
+            s._compact = self._compact
+        return s
+
+    def insert_session(self, topic: bytes) -> str:
+        return self._session().insert(topic)
+
+    def delete_session(self, topic: bytes) -> str:
+        return self._session().delete(topic)
+
+    def match_session(self, topic: bytes) -> List[bytes]:
+        return self._session().match(topic)
+
+    def match_session_batch(self, topics: Sequence[bytes]) -> List[List[bytes]]:
+        return self._session().match_batch(topics)
+
+    def empty_session(self) -> bool:
+        return self._session().empty()
+
     def lookup_topic(self, topic: bytes) -> List[bytes]:
         """emqx_trie.erl:267-271 -- whether the committed trie holds the key {Topic, 1}."""
         self._maybe_commit()

@@ -74,6 +74,21 @@ def test_trie_suite_on_device(emqx, golden, compact):
         trie.engine.close()
 
 
+def test_session_trie_is_a_second_table(emqx):
+    """insert_session/match_session/delete_session/empty_session work on their own table
+    (emqx_trie.erl:117-176): the two tries never see each other's filters."""
+    trie = emqx.Trie()
+    trie.insert(b"a/+")
+    trie.insert_session(b"a/#")
+    trie.insert_session(b"b/+")
+    assert trie.match(b"a/b") == [b"a/+"]
+    assert sorted(trie.match_session(b"a/b")) == [b"a/#"]
+    assert trie.match_session(b"b/x") == [b"b/+"] and trie.match(b"b/x") == []
+    trie.delete_session(b"a/#")
+    trie.delete_session(b"b/+")
+    assert trie.empty_session() and not trie.empty()
+
+
 def test_router_suite_on_device(emqx, golden):
     for case, steps in golden["router_cases"].items():
         r = emqx.Router()
