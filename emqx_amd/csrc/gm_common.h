@@ -12,6 +12,7 @@
 namespace gm {
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint32_t TOMB = 0xFFFFFFFEu;  // deleted slot / exact entry (delta commits)
 
 // ---- level tokens ---------------------------------------------------------------------
 // A level token identifies one topic level (emqx_topic:words/1 element).  A word of at most
@@ -85,7 +86,8 @@ GM_HD uint64_t key_hash(const uint8_t* p, uint32_t len, uint64_t mask) {
 //         carried so that the walk expands it without a probe.  The rest of p (its terminal
 //         filters, its own '+' child) comes from the (C, '+') slot when the walk needs it.
 // Non-wildcard trie keys ending at a node (only single-level '$' topics read them,
-// emqx_trie.erl:287) live in a per-node side array.  An empty slot has parent == NONE.
+// emqx_trie.erl:287) live in a per-node side array.  An empty slot has parent == NONE; a slot
+// freed by a delta commit has parent == TOMB (never a node id, not empty: lookups go on).
 // Slots come in 64-B buckets of EBUCKET (one line: a probe loads and checks both slots, so a
 // collision inside the bucket costs no extra round trip); an edge goes to the first free slot
 // of its home bucket (edge_slot) or of the buckets after it, and a lookup stops at a bucket
@@ -107,7 +109,8 @@ GM_HD uint64_t edge_slot(uint32_t parent, uint64_t tok, uint64_t mask) {
   return fmix64(tok ^ ((uint64_t)parent * 0x9e3779b97f4a7c15ull)) & mask;
 }
 // Exact route-key table: buckets of XBUCKET 16-B entries {hash.lo, hash.hi, fid, len}, filled
-// in order (linear probing over buckets); exact_slot gives the home bucket.
+// in order (linear probing over buckets); exact_slot gives the home bucket.  An empty entry has
+// fid == NONE; a deleted one {0, 0, TOMB, 0xFFFFFFFF} (a length no key has) never matches.
 constexpr uint32_t XBUCKET = 4;
 GM_HD uint64_t exact_slot(uint64_t fh, uint64_t mask) { return fmix64(fh + 0x632be59bd9b4e019ull) & mask; }
 

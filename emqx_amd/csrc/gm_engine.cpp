@@ -9,6 +9,7 @@
 //     the pending registry and becomes visible atomically at emqxgm_commit.
 #include <errno.h>
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <string.h>
 
 #include <algorithm>
@@ -34,15 +35,16 @@ uint64_t pow2_at_least(uint64_t x) {
   return p;
 }
 
-// Open-addressing map (parent node, level token) -> child node (host-side trie builder).
+// Open-addressing map (parent node, level token) -> child node (host-side trie; kept between
+// commits for delta commits, so it also erases: a freed entry becomes a TOMB that lookups pass).
 struct EdgeMap {
   struct Ent {
     uint64_t tok;
-    uint32_t parent;  // NONE = empty
+    uint32_t parent;  // NONE = empty, TOMB = erased
     uint32_t child;
   };
   std::vector<Ent> ents;
-  uint64_t mask = 0, used = 0;
+  uint64_t mask = 0, used = 0;  // used counts erased entries too
   void init(uint64_t expect) {
     const uint64_t cap = pow2_at_least(std::max<uint64_t>(16, expect * 2));
     ents.assign(cap, Ent{0, NONE, 0});
@@ -57,27 +59,47 @@ struct EdgeMap {
     used = 0;
     bool ins;
     for (const Ent& e : old)
-      if (e.parent != NONE) *get_or_insert(e.parent, e.tok, ins) = e.child;
+      if (e.parent != NONE && e.parent != TOMB) *get_or_insert(e.parent, e.tok, ins) = e.child;
   }
   // returns pointer to the child slot; inserted=true if new
   uint32_t* get_or_insert(uint32_t parent, uint64_t tok, bool& inserted) {
     if ((used + 1) * 2 > mask + 1) grow();
-    uint64_t i = edge_slot(parent, tok, mask);
+    uint64_t i = edge_slot(parent, tok, mask), free_at = ~0ull;
     for (;;) {
       Ent& e = ents[i];
       if (e.parent == parent && e.tok == tok) {
         inserted = false;
         return &e.child;
       }
+      if (e.parent == TOMB && free_at == ~0ull) free_at = i;
       if (e.parent == NONE) {
-        e.parent = parent;
-        e.tok = tok;
-        ++used;
+        if (free_at == ~0ull) {
+          free_at = i;
+          ++used;
+        }
+        Ent& f = ents[free_at];
+        f.parent = parent;
+        f.tok = tok;
         inserted = true;
-        return &e.child;
+        return &f.child;
       }
       i = (i + 1) & mask;
     }
+  }
+  uint32_t* find(uint32_t parent, uint64_t tok) {
+    if (ents.empty()) return nullptr;
+    for (uint64_t i = edge_slot(parent, tok, mask);; i = (i + 1) & mask) {
+      Ent& e = ents[i];
+      if (e.parent == parent && e.tok == tok) return &e.child;
+      if (e.parent == NONE) return nullptr;
+    }
+  }
+  bool erase(uint32_t parent, uint64_t tok) {
+    uint32_t* c = find(parent, tok);
+    if (!c) return false;
+    Ent* e = (Ent*)((uint8_t*)c - offsetof(Ent, child));
+    e->parent = TOMB;
+    return true;
   }
 };
 
@@ -117,6 +139,7 @@ struct Filter {
   uint8_t in_trie;
   uint8_t wild;
   uint8_t trie_committed;
+  uint8_t route_committed;
   uint32_t route_refs;
 };
 
@@ -124,6 +147,65 @@ struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
 };
+
+constexpr uint64_t DEAD = ~0ull;  // TrieModel::slot of the root and of removed nodes
+
+// Host model of the committed trie and exact table, kept so that a commit with a small delta
+// patches the device tables in place (commit_delta) instead of rebuilding them.  A slot's 32 B
+// are a function of its node's state (node_slot), so only positions and occupancy are mirrored.
+struct TrieModel {
+  bool valid = false;  // false: the next commit is a full build
+  EdgeMap emap;
+  // per node (root = 0): hf/tw/tn are NONE, a filter id, or LIST_MULTI | multi[] position
+  std::vector<uint32_t> parent, ref, nlit, pchild, hf, tw, tn;
+  std::vector<uint64_t> tok;
+  std::vector<uint64_t> slot;       // edge slot of the node's incoming edge (DEAD: root/removed)
+  std::vector<uint64_t> occ, tomb;  // bitmaps over edge slots: used (live or TOMB), TOMB
+  uint64_t nbk = 0, ecap = 0, n_occ = 0, n_edges = 0, tn_cap = 0, fv_cap = 0;
+  std::vector<uint32_t> fvbits;
+  bool needs_verify = false;
+  uint32_t max_depth = 0;
+  uint64_t n_trie = 0, n_route = 0;
+  // exact route keys: entry per committed key, bitmaps over entries
+  std::vector<uint32_t> xpos;
+  std::vector<uint64_t> xocc, xtomb;
+  uint64_t xcap = 0, x_occ = 0;
+  // device tables patched in place (owned by emqxgm::ix_bufs)
+  uint32_t *d_edges = nullptr, *d_exact = nullptr, *d_tn = nullptr, *d_fv = nullptr;
+
+  uint32_t cf(uint32_t i) const {  // gm_common.h cf: id | flags
+    uint32_t f = i;
+    if (nlit[i]) f |= CF_LIT;
+    if (pchild[i]) f |= CF_PLUS;
+    if (hf[i] != NONE && (hf[i] & LIST_MULTI)) f |= CF_HFM;
+    if (tw[i] != NONE) f |= CF_TW;
+    if (tn[i] != NONE) f |= CF_TN;
+    return f;
+  }
+  uint32_t hfd(uint32_t i) const { return hf[i] == NONE ? NONE : (hf[i] & ~LIST_MULTI); }
+  void node_slot(uint32_t c, uint4* sl) const {  // the 2 x uint4 of c's incoming edge
+    const uint32_t p = pchild[c];
+    sl[0] = make_uint4((uint32_t)tok[c], (uint32_t)(tok[c] >> 32), parent[c], cf(c));
+    sl[1] = make_uint4(hfd(c), tw[c], p ? cf(p) : 0u, p ? hfd(p) : NONE);
+  }
+  uint32_t new_node(uint32_t par, uint64_t t) {
+    const uint32_t c = (uint32_t)parent.size();
+    parent.push_back(par);
+    tok.push_back(t);
+    ref.push_back(0);
+    nlit.push_back(0);
+    pchild.push_back(0);
+    hf.push_back(NONE);
+    tw.push_back(NONE);
+    tn.push_back(NONE);
+    slot.push_back(DEAD);
+    return c;
+  }
+};
+
+inline bool bit(const std::vector<uint64_t>& b, uint64_t i) { return (b[i >> 6] >> (i & 63)) & 1; }
+inline void bset(std::vector<uint64_t>& b, uint64_t i) { b[i >> 6] |= 1ull << (i & 63); }
+inline void bclr(std::vector<uint64_t>& b, uint64_t i) { b[i >> 6] &= ~(1ull << (i & 63)); }
 
 }  // namespace
 
@@ -179,6 +261,14 @@ struct emqxgm {
   bool walk_spill = false;         // committed index needs the spilling walk variant
   uint32_t reject_cap = 1u << 20;  // cfg.reject_cap overrides (tests force the legacy path)
   uint64_t test_mask = 0;          // != 0: collision-test tokens (cfg.word_hash_bits)
+
+  // ---- delta commits ----
+  TrieModel tm;
+  std::vector<uint32_t> changed;  // filter ids whose trie / route-key membership may differ
+  bool fan_dirty = true;          // fan-out registry changed since the fan tables were built
+  std::vector<DevBuf> fan_tab_bufs;
+  DevBuf d_patch;
+  uint32_t delta_mode = 1;        // 0: always rebuild, 1: delta when small, 2: delta if possible
 };
 
 namespace {
@@ -246,6 +336,7 @@ uint32_t find_id(emqxgm* h, const uint8_t* p, uint32_t len, bool create) {
   f.len = len;
   f.in_trie = 0;
   f.trie_committed = 0;
+  f.route_committed = 0;
   f.wild = is_wild(p, len) ? 1 : 0;
   f.route_refs = 0;
   h->pool.insert(h->pool.end(), p, p + len);
@@ -304,153 +395,9 @@ int append_upload(emqxgm* h, DevBuf& buf, uint64_t& uploaded, const void* src, u
   return 0;
 }
 
-// Build the device index from the pending registry and swap it in.
-int commit_locked(emqxgm* h) {
-  const uint64_t test_mask = h->test_mask;
-  const uint64_t fmask =
-      h->cfg.full_hash_bits >= 64 ? ~0ull : ((1ull << h->cfg.full_hash_bits) - 1ull);
+// Filter string pool, offsets and 64-B verification records: append-only device mirrors.
+int upload_pool(emqxgm* h) {
   const uint64_t nf = h->filters.size();
-
-  // ---- trie: nodes keyed by (parent, level token); root = node 0 ----
-  std::vector<uint32_t> nflags(1, 0), nhf(1, NONE), ntw(1, NONE), ntn(1, NONE);
-  EdgeMap emap;
-  emap.init(std::max<uint64_t>(1024, h->n_trie_pending * 2));
-  ListBuild lb;
-  struct Edge {
-    uint64_t tok;
-    uint32_t parent, child;
-  };
-  std::vector<Edge> edges;
-  edges.reserve(h->n_trie_pending * 2 + 16);
-  std::vector<uint32_t> fvbits((nf + 31) / 32 + 1, 0u);
-  bool needs_verify = false;
-  uint32_t max_depth = 0;
-  uint64_t n_trie = 0;
-  std::vector<uint64_t> toks;
-  std::vector<uint8_t> is_plus, is_hash;
-  for (uint32_t id = 0; id < h->filters.size(); ++id) {
-    const Filter& f = h->filters[id];
-    if (!f.in_trie) continue;
-    ++n_trie;
-    bool hashed;
-    tokenize(h->pool.data() + f.off, f.len, test_mask, toks, is_plus, is_hash, hashed);
-    if (hashed) {
-      fvbits[id >> 5] |= 1u << (id & 31);
-      needs_verify = true;
-    }
-    const size_t nw = toks.size();
-    const bool hash_last = is_hash[nw - 1];
-    const size_t path_len = hash_last ? nw - 1 : nw;  // '#' last: attach to the parent node
-    uint32_t cur = 0;
-    for (size_t w = 0; w < path_len; ++w) {
-      const uint64_t tok = is_plus[w] ? PLUS_TOK : toks[w];
-      bool ins;
-      uint32_t* v = emap.get_or_insert(cur, tok, ins);
-      if (ins) {
-        const uint32_t child = (uint32_t)nflags.size();
-        if (child >= MAX_NODES) {
-          h->err = "trie exceeds 2^27-1 nodes";
-          return -E2BIG;
-        }
-        *v = child;
-        nflags.push_back(0);
-        nhf.push_back(NONE);
-        ntw.push_back(NONE);
-        ntn.push_back(NONE);
-        edges.push_back(Edge{tok, cur, child});
-        nflags[cur] |= is_plus[w] ? CF_PLUS : CF_LIT;
-      }
-      cur = *v;
-    }
-    max_depth = std::max<uint32_t>(max_depth, (uint32_t)path_len);
-    if (hash_last) {
-      lb.add(nhf[cur], id);
-    } else if (f.wild) {
-      lb.add(ntw[cur], id);
-      nflags[cur] |= CF_TW;
-    } else {
-      lb.add(ntn[cur], id);
-      nflags[cur] |= CF_TN;
-    }
-  }
-  // flatten multi lists
-  std::vector<uint32_t> multi(1, 0);
-  std::vector<uint32_t> list_pos(lb.lists.size());
-  for (size_t i = 0; i < lb.lists.size(); ++i) {
-    list_pos[i] = (uint32_t)multi.size();
-    multi.push_back((uint32_t)lb.lists[i].size());
-    multi.insert(multi.end(), lb.lists[i].begin(), lb.lists[i].end());
-  }
-  auto resolve = [&](uint32_t v) -> uint32_t {
-    if (v == NONE || !(v & LIST_MULTI)) return v;
-    return LIST_MULTI | list_pos[v & ~LIST_MULTI];
-  };
-  const size_t n_nodes = nflags.size();
-  std::vector<uint32_t> cfv(n_nodes), hfv(n_nodes);
-  for (size_t i = 0; i < n_nodes; ++i) {
-    uint32_t hf = resolve(nhf[i]);
-    uint32_t flags = nflags[i];
-    if (hf != NONE && (hf & LIST_MULTI)) {
-      flags |= CF_HFM;
-      hf &= ~LIST_MULTI;
-    }
-    cfv[i] = (uint32_t)i | flags;
-    hfv[i] = hf;
-  }
-  // '+' child of every node (0 = none); its {cf, hf} is carried in the slot of the edge that
-  // leads to the node, so the walk expands most '+' children without a probe
-  std::vector<uint32_t> pchild(n_nodes, 0u);
-  for (const Edge& e : edges)
-    if (e.tok == PLUS_TOK) pchild[e.parent] = e.child;
-  // 32-B slots in 64-B buckets (gm_common.h "edge slots"); load factor <= 1/2
-  const uint64_t ecap = pow2_at_least(std::max<uint64_t>(64, edges.size() * EDGE_SLACK));  // slots
-  const uint64_t nbk = ecap / EBUCKET;
-  std::vector<uint4> eslots(SLOT_U4 * ecap, make_uint4(0u, 0u, 0u, 0u));
-  for (uint64_t i = 0; i < ecap; ++i) eslots[SLOT_U4 * i] = make_uint4(0u, 0u, NONE, 0u);
-  for (const Edge& e : edges) {
-    uint64_t b = edge_slot(e.parent, e.tok, nbk - 1), i;
-    for (;;) {
-      uint32_t j = 0;
-      while (j < EBUCKET && eslots[SLOT_U4 * (b * EBUCKET + j)].z != NONE) ++j;
-      if (j < EBUCKET) {
-        i = b * EBUCKET + j;
-        break;
-      }
-      b = (b + 1) & (nbk - 1);
-    }
-    const uint32_t c = e.child, p = pchild[c];
-    uint4* sl = &eslots[SLOT_U4 * i];
-    sl[0] = make_uint4((uint32_t)e.tok, (uint32_t)(e.tok >> 32), e.parent, cfv[c]);
-    sl[1] = make_uint4(hfv[c], resolve(ntw[c]), p ? cfv[p] : 0u, p ? hfv[p] : NONE);
-  }
-  std::vector<uint32_t> tn_of(n_nodes);
-  for (size_t i = 0; i < n_nodes; ++i) tn_of[i] = resolve(ntn[i]);
-  const uint32_t root_p = pchild[0];
-
-  // ---- exact route keys ----
-  uint64_t n_route = 0;
-  for (const Filter& f : h->filters) n_route += f.route_refs > 0;
-  // buckets of XBUCKET entries, load factor <= 1/2, filled in order (gm_common.h)
-  const uint64_t xcap = pow2_at_least(std::max<uint64_t>(16, (n_route * 2 + XBUCKET - 1) / XBUCKET));
-  std::vector<uint4> xslots(xcap * XBUCKET, make_uint4(0u, 0u, NONE, 0u));
-  for (uint32_t id = 0; id < h->filters.size(); ++id) {
-    const Filter& f = h->filters[id];
-    if (!f.route_refs) continue;
-    const uint64_t fh = key_hash(h->pool.data() + f.off, f.len, fmask);
-    uint64_t b = exact_slot(fh, xcap - 1);
-    for (;;) {
-      uint32_t j = 0;
-      while (j < XBUCKET && xslots[b * XBUCKET + j].z != NONE) ++j;
-      if (j < XBUCKET) {
-        xslots[b * XBUCKET + j] = make_uint4((uint32_t)fh, (uint32_t)(fh >> 32), id, f.len);
-        break;
-      }
-      b = (b + 1) & (xcap - 1);
-    }
-  }
-
-  // ---- filter string pool, offsets and 64-B verification records (append-only) ----
-  if (hipSetDevice(h->cfg.device) != hipSuccess) return fail(h, hipErrorInvalidDevice, "hipSetDevice");
   if (h->foff_host.empty()) h->foff_host.push_back(0);
   for (uint64_t i = h->foff_host.size() - 1; i < nf; ++i)  // pool is append-only
     h->foff_host.push_back(h->filters[i].off + h->filters[i].len);
@@ -468,12 +415,21 @@ int commit_locked(emqxgm* h) {
       (rc = append_upload(h, h->d_fver, h->fver_uploaded, h->fver_host.data(),
                           h->fver_host.size())))
     return rc;
+  h->ix.fbytes = (const uint8_t*)h->d_pool.p;
+  h->ix.foff = (const uint64_t*)h->d_foff.p;
+  h->ix.fver = (const uint4*)h->d_fver.p;
+  return 0;
+}
 
-  // ---- publish fan-out tables (gm_fanout.inc): per filter id, its aggre/1 entries (plain
-  // node dests, then each group once: emqx_broker.erl:284-300) and, when it routes to the
-  // local node, its local subscribers (dispatch/2, :326-355) ----
+// Publish fan-out tables (gm_fanout.inc): per filter id, its aggre/1 entries (plain node dests,
+// then each group once: emqx_broker.erl:284-300) and, when it routes to the local node, its
+// local subscribers (dispatch/2, :326-355).  Rebuilt whenever the fan-out registry changed.
+int build_fan(emqxgm* h) {
+  const uint64_t nf = h->filters.size();
   std::vector<uint32_t> rt_off, rt_dst, dl_off, dl_sub;
   const bool fan = !h->rdest.empty() || !h->lsubs.empty();
+  std::vector<DevBuf> nb;
+  DevIndex& ix = h->ix;
   if (fan) {
     rt_off.assign(nf + 1, 0u);
     dl_off.assign(nf + 1, 0u);
@@ -503,62 +459,482 @@ int commit_locked(emqxgm* h) {
         dl_off[id + 1] = (uint32_t)dl_sub.size();
       }
     }
+    DevIndex t;
+    int rc = 0;
+    if ((rc = dev_upload(h, nb, rt_off, &t.rt_off)) || (rc = dev_upload(h, nb, rt_dst, &t.rt_dst)) ||
+        (rc = dev_upload(h, nb, dl_off, &t.dl_off)) || (rc = dev_upload(h, nb, dl_sub, &t.dl_sub))) {
+      free_bufs(nb);
+      return rc;
+    }
+    ix.rt_off = t.rt_off;
+    ix.rt_dst = t.rt_dst;
+    ix.dl_off = t.dl_off;
+    ix.dl_sub = t.dl_sub;
+  } else {
+    ix.rt_off = ix.rt_dst = ix.dl_off = ix.dl_sub = nullptr;
   }
+  ix.fan_nf = fan ? (uint32_t)nf : 0u;
+  free_bufs(h->fan_tab_bufs);
+  h->fan_tab_bufs.swap(nb);
+  h->fan_dirty = false;
+  return 0;
+}
+
+void commit_stats(emqxgm* h, double ms, bool delta) {
+  const TrieModel& m = h->tm;
+  h->st.epoch = h->epoch;
+  h->st.n_filters = h->filters.size();
+  h->st.n_trie_filters = m.n_trie;
+  h->st.n_route_keys = m.n_route;
+  h->st.n_nodes = m.n_edges + 1;
+  h->st.n_edges = m.n_edges;
+  h->st.edge_slots = m.ecap;
+  h->st.exact_slots = m.xcap * XBUCKET;
+  h->st.max_depth = m.max_depth;
+  h->st.device_bytes = m.ecap * SLOT_U4 * 16 + m.xcap * XBUCKET * 16 + m.tn_cap * 4 +
+                       m.fv_cap * 4 + h->pool.size() + (h->filters.size() + 1) * 8 +
+                       h->filters.size() * VREC;
+  h->st.last_commit_ms = ms;
+  (delta ? h->st.delta_commits : h->st.full_commits) += 1;
+}
+
+// Full build of the device index from the pending registry; swaps it in and rebuilds the host
+// model (TrieModel) that later delta commits patch.
+int commit_full(emqxgm* h) {
+  const uint64_t test_mask = h->test_mask;
+  const uint64_t fmask =
+      h->cfg.full_hash_bits >= 64 ? ~0ull : ((1ull << h->cfg.full_hash_bits) - 1ull);
+  const uint64_t nf = h->filters.size();
+  h->tm = TrieModel();  // frees the old model before the new one is built
+  TrieModel m;
+
+  // ---- trie: nodes keyed by (parent, level token); root = node 0 ----
+  m.new_node(NONE, 0);
+  m.emap.init(std::max<uint64_t>(1024, h->n_trie_pending * 2));
+  ListBuild lb;
+  m.fvbits.assign((nf + 31) / 32 + 1, 0u);
+  std::vector<uint64_t> toks;
+  std::vector<uint8_t> is_plus, is_hash;
+  for (uint32_t id = 0; id < h->filters.size(); ++id) {
+    const Filter& f = h->filters[id];
+    if (!f.in_trie) continue;
+    ++m.n_trie;
+    bool hashed;
+    tokenize(h->pool.data() + f.off, f.len, test_mask, toks, is_plus, is_hash, hashed);
+    if (hashed) {
+      m.fvbits[id >> 5] |= 1u << (id & 31);
+      m.needs_verify = true;
+    }
+    const size_t nw = toks.size();
+    const bool hash_last = is_hash[nw - 1];
+    const size_t path_len = hash_last ? nw - 1 : nw;  // '#' last: attach to the parent node
+    uint32_t cur = 0;
+    for (size_t w = 0; w < path_len; ++w) {
+      const uint64_t tok = is_plus[w] ? PLUS_TOK : toks[w];
+      bool ins;
+      uint32_t* v = m.emap.get_or_insert(cur, tok, ins);
+      if (ins) {
+        if (m.parent.size() >= MAX_NODES) {
+          h->err = "trie exceeds 2^27-1 nodes";
+          return -E2BIG;
+        }
+        const uint32_t child = m.new_node(cur, tok);
+        *v = child;
+        if (is_plus[w])
+          m.pchild[cur] = child;
+        else
+          m.nlit[cur] += 1;
+      }
+      cur = *v;
+      m.ref[cur] += 1;
+    }
+    m.max_depth = std::max<uint32_t>(m.max_depth, (uint32_t)path_len);
+    lb.add(hash_last ? m.hf[cur] : f.wild ? m.tw[cur] : m.tn[cur], id);
+  }
+  // flatten multi lists
+  std::vector<uint32_t> multi(1, 0);
+  std::vector<uint32_t> list_pos(lb.lists.size());
+  for (size_t i = 0; i < lb.lists.size(); ++i) {
+    list_pos[i] = (uint32_t)multi.size();
+    multi.push_back((uint32_t)lb.lists[i].size());
+    multi.insert(multi.end(), lb.lists[i].begin(), lb.lists[i].end());
+  }
+  auto resolve = [&](uint32_t& v) {
+    if (v != NONE && (v & LIST_MULTI)) v = LIST_MULTI | list_pos[v & ~LIST_MULTI];
+  };
+  const size_t n_nodes = m.parent.size();
+  for (size_t i = 0; i < n_nodes; ++i) {
+    resolve(m.hf[i]);
+    resolve(m.tw[i]);
+    resolve(m.tn[i]);
+  }
+  m.n_edges = n_nodes - 1;
+  // 32-B slots in 64-B buckets (gm_common.h "edge slots"); load factor <= 1/EDGE_SLACK.  Each
+  // slot carries its child's '+' child {cf, hf}, so the walk expands most '+' children
+  // without a probe.
+  m.ecap = pow2_at_least(std::max<uint64_t>(64, m.n_edges * EDGE_SLACK));
+  m.nbk = m.ecap / EBUCKET;
+  m.occ.assign(m.ecap / 64 + 1, 0ull);
+  m.tomb.assign(m.ecap / 64 + 1, 0ull);
+  std::vector<uint4> eslots(SLOT_U4 * m.ecap, make_uint4(0u, 0u, 0u, 0u));
+  for (uint64_t i = 0; i < m.ecap; ++i) eslots[SLOT_U4 * i] = make_uint4(0u, 0u, NONE, 0u);
+  for (uint32_t c = 1; c < n_nodes; ++c) {
+    uint64_t b = edge_slot(m.parent[c], m.tok[c], m.nbk - 1), i;
+    for (;;) {
+      uint32_t j = 0;
+      while (j < EBUCKET && bit(m.occ, b * EBUCKET + j)) ++j;
+      if (j < EBUCKET) {
+        i = b * EBUCKET + j;
+        break;
+      }
+      b = (b + 1) & (m.nbk - 1);
+    }
+    bset(m.occ, i);
+    m.slot[c] = i;
+    m.node_slot(c, &eslots[SLOT_U4 * i]);
+  }
+  m.n_occ = m.n_edges;
+  // node side array with headroom for delta-commit growth
+  m.tn_cap = n_nodes + std::max<uint64_t>(4096, n_nodes / 4);
+  std::vector<uint32_t> tn_of(m.tn_cap, NONE);
+  for (size_t i = 0; i < n_nodes; ++i) tn_of[i] = m.tn[i];
+  m.fv_cap = m.fvbits.size() + std::max<uint64_t>(1024, m.fvbits.size() / 4);
+  m.fvbits.resize(m.fv_cap, 0u);
+
+  // ---- exact route keys: buckets of XBUCKET entries, load factor <= 1/2, filled in order ----
+  for (const Filter& f : h->filters) m.n_route += f.route_refs > 0;
+  m.xcap = pow2_at_least(std::max<uint64_t>(16, (m.n_route * 2 + XBUCKET - 1) / XBUCKET));
+  m.xocc.assign(m.xcap * XBUCKET / 64 + 1, 0ull);
+  m.xtomb.assign(m.xcap * XBUCKET / 64 + 1, 0ull);
+  m.xpos.assign(nf, NONE);
+  std::vector<uint4> xslots(m.xcap * XBUCKET, make_uint4(0u, 0u, NONE, 0u));
+  for (uint32_t id = 0; id < h->filters.size(); ++id) {
+    const Filter& f = h->filters[id];
+    if (!f.route_refs) continue;
+    const uint64_t fh = key_hash(h->pool.data() + f.off, f.len, fmask);
+    uint64_t b = exact_slot(fh, m.xcap - 1);
+    for (;;) {
+      uint32_t j = 0;
+      while (j < XBUCKET && xslots[b * XBUCKET + j].z != NONE) ++j;
+      if (j < XBUCKET) {
+        const uint64_t e = b * XBUCKET + j;
+        xslots[e] = make_uint4((uint32_t)fh, (uint32_t)(fh >> 32), id, f.len);
+        bset(m.xocc, e);
+        m.xpos[id] = (uint32_t)e;
+        break;
+      }
+      b = (b + 1) & (m.xcap - 1);
+    }
+  }
+  m.x_occ = m.n_route;
 
   // ---- upload and swap ----
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return fail(h, hipErrorInvalidDevice, "hipSetDevice");
+  int rc = 0;
+  if ((rc = upload_pool(h)) || (rc = build_fan(h))) return rc;
   std::vector<DevBuf> nbufs;
-  DevIndex nx;
-  if (fan && ((rc = dev_upload(h, nbufs, rt_off, &nx.rt_off)) ||
-              (rc = dev_upload(h, nbufs, rt_dst, &nx.rt_dst)) ||
-              (rc = dev_upload(h, nbufs, dl_off, &nx.dl_off)) ||
-              (rc = dev_upload(h, nbufs, dl_sub, &nx.dl_sub)))) {
-    free_bufs(nbufs);
-    return rc;
-  }
-  nx.fan_nf = fan ? (uint32_t)nf : 0u;
+  DevIndex nx = h->ix;  // pool and fan-out pointers just set
   if ((rc = dev_upload(h, nbufs, eslots, &nx.edges)) ||
       (rc = dev_upload(h, nbufs, multi, &nx.multi)) ||
       (rc = dev_upload(h, nbufs, tn_of, &nx.tn_of)) ||
-      (rc = dev_upload(h, nbufs, fvbits, &nx.fvbits)) ||
+      (rc = dev_upload(h, nbufs, m.fvbits, &nx.fvbits)) ||
       (rc = dev_upload(h, nbufs, xslots, &nx.exact))) {
     free_bufs(nbufs);
     return rc;
   }
-  nx.emask = nbk - 1;
-  nx.xmask = xcap - 1;
-  nx.root_cf = cfv[0];
-  nx.root_hf = hfv[0];
-  nx.root_pcf = root_p ? cfv[root_p] : 0u;
-  nx.root_phf = root_p ? hfv[root_p] : NONE;
-  nx.fbytes = (const uint8_t*)h->d_pool.p;
-  nx.foff = (const uint64_t*)h->d_foff.p;
-  nx.fver = (const uint4*)h->d_fver.p;
+  m.d_edges = (uint32_t*)nx.edges;
+  m.d_exact = (uint32_t*)nx.exact;
+  m.d_tn = (uint32_t*)nx.tn_of;
+  m.d_fv = (uint32_t*)nx.fvbits;
+  nx.emask = m.nbk - 1;
+  nx.xmask = m.xcap - 1;
+  const uint32_t root_p = m.pchild[0];
+  nx.root_cf = m.cf(0);
+  nx.root_hf = m.hfd(0);
+  nx.root_pcf = root_p ? m.cf(root_p) : 0u;
+  nx.root_phf = root_p ? m.hfd(root_p) : NONE;
   nx.test_mask = test_mask;
-  nx.needs_verify = needs_verify;
+  nx.needs_verify = m.needs_verify;
   nx.full_mask = fmask;
-  nx.max_depth = max_depth;
-  nx.trie_empty = (n_trie == 0);
-  nx.exact_empty = (n_route == 0);
+  nx.max_depth = m.max_depth;
+  nx.trie_empty = (m.n_trie == 0);
+  nx.exact_empty = (m.n_route == 0);
   free_bufs(h->ix_bufs);
   h->ix_bufs.swap(nbufs);
-  for (Filter& f : h->filters) f.trie_committed = f.in_trie;
+  for (Filter& f : h->filters) {
+    f.trie_committed = f.in_trie;
+    f.route_committed = f.route_refs > 0;
+  }
   h->ix = nx;
+  m.valid = true;
+  h->tm = std::move(m);
+  h->changed.clear();
   h->walk_spill = false;
+  return 0;
+}
+
+// Delta commit: apply the membership changes since the last commit to the host model and patch
+// the device tables in place (k_patch).  Returns 0 when applied, 1 when the delta does not fit
+// (too large, a table would pass its load bound, a node list would need a multi[] list, ...):
+// the caller then runs the full build, which also rebuilds the model.  Readers are stream-
+// ordered behind the patches, and a commit holds the handle lock, so no match sees a half-
+// applied delta.
+int commit_delta(emqxgm* h) {
+  TrieModel& m = h->tm;
+  if (!m.valid || h->delta_mode == 0) return 1;
+  const uint64_t nf = h->filters.size();
+  auto& ch = h->changed;
+  std::sort(ch.begin(), ch.end());
+  ch.erase(std::unique(ch.begin(), ch.end()), ch.end());
+  std::vector<uint32_t> tadd, tdel, radd, rdel;
+  for (uint32_t id : ch) {
+    const Filter& f = h->filters[id];
+    if (f.in_trie != f.trie_committed) (f.in_trie ? tadd : tdel).push_back(id);
+    const bool r = f.route_refs > 0;
+    if (r != (bool)f.route_committed) (r ? radd : rdel).push_back(id);
+  }
+  const uint64_t nchg = tadd.size() + tdel.size() + radd.size() + rdel.size();
+  if (h->delta_mode == 1 && nchg > std::max<uint64_t>(4096, (m.n_trie + m.n_route) / 8)) return 1;
+  if ((nf + 31) / 32 + 1 > m.fv_cap) return 1;
+  m.valid = false;  // from here a declined delta leaves the model to the full build
+
+  const uint64_t test_mask = h->test_mask;
+  const uint64_t fmask =
+      h->cfg.full_hash_bits >= 64 ? ~0ull : ((1ull << h->cfg.full_hash_bits) - 1ull);
+  std::unordered_map<uint64_t, uint32_t> epatch;  // edge slot -> node (NONE: TOMB)
+  std::unordered_map<uint64_t, uint4> xpatch;     // exact entry -> content
+  std::vector<uint32_t> dirty;                    // nodes whose slot / side entry changed
+  bool fv_changed = false;
+  std::vector<uint64_t> toks;
+  std::vector<uint8_t> is_plus, is_hash;
+  std::vector<uint32_t> path;
+
+  // ---- trie deletes: drop the key from its end node, free nodes no filter passes any more ----
+  for (uint32_t id : tdel) {
+    const Filter& f = h->filters[id];
+    bool hashed;
+    tokenize(h->pool.data() + f.off, f.len, test_mask, toks, is_plus, is_hash, hashed);
+    const size_t nw = toks.size();
+    const bool hash_last = is_hash[nw - 1];
+    const size_t path_len = hash_last ? nw - 1 : nw;
+    path.clear();
+    uint32_t cur = 0;
+    for (size_t w = 0; w < path_len; ++w) {
+      const uint32_t* v = m.emap.find(cur, is_plus[w] ? PLUS_TOK : toks[w]);
+      if (!v) return 1;
+      cur = *v;
+      path.push_back(cur);
+    }
+    uint32_t& fld = hash_last ? m.hf[cur] : f.wild ? m.tw[cur] : m.tn[cur];
+    if (fld != id) return 1;  // part of a multi[] list
+    fld = NONE;
+    dirty.push_back(cur);
+    for (size_t k = path.size(); k-- > 0;) {
+      const uint32_t n = path[k];
+      if (--m.ref[n] != 0) continue;
+      const uint32_t par = m.parent[n];
+      m.emap.erase(par, m.tok[n]);
+      if (m.tok[n] == PLUS_TOK)
+        m.pchild[par] = 0;
+      else
+        m.nlit[par] -= 1;
+      bset(m.tomb, m.slot[n]);
+      epatch[m.slot[n]] = NONE;
+      m.slot[n] = DEAD;
+      m.n_edges -= 1;
+      dirty.push_back(par);
+    }
+    m.n_trie -= 1;
+  }
+
+  // ---- trie inserts: new nodes take the first free or TOMB slot of their bucket chain ----
+  for (uint32_t id : tadd) {
+    const Filter& f = h->filters[id];
+    bool hashed;
+    tokenize(h->pool.data() + f.off, f.len, test_mask, toks, is_plus, is_hash, hashed);
+    if (hashed) {
+      m.fvbits[id >> 5] |= 1u << (id & 31);
+      m.needs_verify = true;
+      fv_changed = true;
+    }
+    const size_t nw = toks.size();
+    const bool hash_last = is_hash[nw - 1];
+    const size_t path_len = hash_last ? nw - 1 : nw;
+    uint32_t cur = 0;
+    for (size_t w = 0; w < path_len; ++w) {
+      const uint64_t tok = is_plus[w] ? PLUS_TOK : toks[w];
+      bool ins;
+      uint32_t* v = m.emap.get_or_insert(cur, tok, ins);
+      if (ins) {
+        if (m.parent.size() >= std::min<uint64_t>(MAX_NODES, m.tn_cap)) return 1;
+        if ((m.n_occ + 1) * 2 > m.ecap) return 1;  // load bound of a delta-patched table
+        const uint32_t c = m.new_node(cur, tok);
+        *v = c;
+        uint64_t b = edge_slot(cur, tok, m.nbk - 1), i = DEAD;
+        while (i == DEAD) {
+          for (uint32_t j = 0; j < EBUCKET && i == DEAD; ++j) {
+            const uint64_t q = b * EBUCKET + j;
+            if (!bit(m.occ, q)) {
+              bset(m.occ, q);
+              m.n_occ += 1;
+              i = q;
+            } else if (bit(m.tomb, q)) {
+              bclr(m.tomb, q);
+              i = q;
+            }
+          }
+          b = (b + 1) & (m.nbk - 1);
+        }
+        m.slot[c] = i;
+        epatch[i] = c;
+        m.n_edges += 1;
+        if (is_plus[w])
+          m.pchild[cur] = c;
+        else
+          m.nlit[cur] += 1;
+        dirty.push_back(cur);
+        dirty.push_back(c);
+      }
+      cur = *v;
+      m.ref[cur] += 1;
+    }
+    m.max_depth = std::max<uint32_t>(m.max_depth, (uint32_t)path_len);
+    uint32_t& fld = hash_last ? m.hf[cur] : f.wild ? m.tw[cur] : m.tn[cur];
+    if (fld != NONE) return 1;  // a second key at one node needs a multi[] list
+    fld = id;
+    dirty.push_back(cur);
+    m.n_trie += 1;
+  }
+
+  // ---- exact route keys ----
+  m.xpos.resize(nf, NONE);
+  for (uint32_t id : rdel) {
+    const uint32_t e = m.xpos[id];
+    if (e == NONE) return 1;
+    bset(m.xtomb, e);
+    xpatch[e] = make_uint4(0u, 0u, TOMB, 0xFFFFFFFFu);
+    m.xpos[id] = NONE;
+    m.n_route -= 1;
+  }
+  for (uint32_t id : radd) {
+    if ((m.x_occ + 1) * 4 > m.xcap * XBUCKET * 3) return 1;
+    const Filter& f = h->filters[id];
+    const uint64_t fh = key_hash(h->pool.data() + f.off, f.len, fmask);
+    uint64_t b = exact_slot(fh, m.xcap - 1), e = DEAD;
+    while (e == DEAD) {
+      for (uint32_t j = 0; j < XBUCKET && e == DEAD; ++j) {
+        const uint64_t q = b * XBUCKET + j;
+        if (!bit(m.xocc, q)) {
+          bset(m.xocc, q);
+          m.x_occ += 1;
+          e = q;
+        } else if (bit(m.xtomb, q)) {
+          bclr(m.xtomb, q);
+          e = q;
+        }
+      }
+      b = (b + 1) & (m.xcap - 1);
+    }
+    xpatch[e] = make_uint4((uint32_t)fh, (uint32_t)(fh >> 32), id, f.len);
+    m.xpos[id] = (uint32_t)e;
+    m.n_route += 1;
+  }
+
+  // ---- patch lists: a dirty node rewrites its own slot, and its parent's slot when it is the
+  // parent's '+' child (the parent's slot carries its {cf, hf}) ----
+  std::sort(dirty.begin(), dirty.end());
+  dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
+  std::vector<uint32_t> tn_nodes;
+  for (uint32_t n : dirty) {
+    if (n != 0 && m.slot[n] == DEAD) continue;  // removed
+    if (n != 0) epatch[m.slot[n]] = n;
+    tn_nodes.push_back(n);
+    const uint32_t par = n ? m.parent[n] : NONE;
+    if (par != NONE && par != 0 && m.pchild[par] == n) epatch[m.slot[par]] = par;
+  }
+  const uint32_t ne = (uint32_t)epatch.size(), nx = (uint32_t)xpatch.size();
+  const uint32_t nt = (uint32_t)tn_nodes.size();
+  const uint64_t words = (uint64_t)ne * 8 + (uint64_t)nx * 4 + nt;
+  std::vector<uint32_t> src(words);
+  std::vector<uint64_t> idx((uint64_t)ne + nx + nt);
+  {
+    uint64_t k = 0;
+    uint32_t* w = src.data();
+    for (const auto& p : epatch) {
+      idx[k++] = p.first;
+      uint4 sl[2] = {make_uint4(0u, 0u, TOMB, 0u), make_uint4(0u, 0u, 0u, 0u)};
+      if (p.second != NONE) m.node_slot(p.second, sl);
+      memcpy(w, sl, 32);
+      w += 8;
+    }
+    for (const auto& p : xpatch) {
+      idx[k++] = p.first;
+      memcpy(w, &p.second, 16);
+      w += 4;
+    }
+    for (uint32_t n : tn_nodes) {
+      idx[k++] = n;
+      *w++ = m.tn[n];
+    }
+  }
+
+  // ---- upload ----
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return fail(h, hipErrorInvalidDevice, "hipSetDevice");
+  int rc = 0;
+  if ((rc = upload_pool(h)) || (h->fan_dirty && (rc = build_fan(h)))) return rc;
+  const uint64_t need = words * 4 + idx.size() * 8 + 16;
+  if (need > h->d_patch.bytes) {
+    if (h->d_patch.p) (void)hipFree(h->d_patch.p);
+    h->d_patch = DevBuf();
+    const uint64_t bytes = std::max<uint64_t>(need, 1u << 20);
+    HIPCHK(h, hipMalloc(&h->d_patch.p, bytes));
+    h->d_patch.bytes = bytes;
+  }
+  uint32_t* d_src = (uint32_t*)h->d_patch.p;
+  uint64_t* d_idx = (uint64_t*)((uint8_t*)h->d_patch.p + ((words * 4 + 15) & ~15ull));
+  if (words) HIPCHK(h, hipMemcpyAsync(d_src, src.data(), words * 4, hipMemcpyHostToDevice, h->stream));
+  if (!idx.empty())
+    HIPCHK(h, hipMemcpyAsync(d_idx, idx.data(), idx.size() * 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, launch_patch(m.d_edges, d_src, d_idx, ne, 8, h->stream));
+  HIPCHK(h, launch_patch(m.d_exact, d_src + (uint64_t)ne * 8, d_idx + ne, nx, 4, h->stream));
+  HIPCHK(h, launch_patch(m.d_tn, d_src + (uint64_t)ne * 8 + (uint64_t)nx * 4, d_idx + ne + nx, nt, 1,
+                         h->stream));
+  if (fv_changed)
+    HIPCHK(h, hipMemcpyAsync(m.d_fv, m.fvbits.data(), ((nf + 31) / 32 + 1) * 4,
+                             hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+
+  DevIndex& ix = h->ix;
+  const uint32_t root_p = m.pchild[0];
+  ix.root_cf = m.cf(0);
+  ix.root_hf = m.hfd(0);
+  ix.root_pcf = root_p ? m.cf(root_p) : 0u;
+  ix.root_phf = root_p ? m.hfd(root_p) : NONE;
+  ix.needs_verify = m.needs_verify;
+  ix.max_depth = m.max_depth;
+  ix.trie_empty = (m.n_trie == 0);
+  ix.exact_empty = (m.n_route == 0);
+  for (uint32_t id : ch) {
+    Filter& f = h->filters[id];
+    f.trie_committed = f.in_trie;
+    f.route_committed = f.route_refs > 0;
+  }
+  ch.clear();
+  m.valid = true;
+  return 0;
+}
+
+// Make the pending registry the committed index: a delta commit when it fits, else a full build.
+int commit_locked(emqxgm* h) {
+  const auto t0 = std::chrono::steady_clock::now();
+  int rc = commit_delta(h);
+  const bool delta = rc == 0;
+  if (rc > 0) rc = commit_full(h);
+  if (rc) return rc;
   h->epoch += 1;
   h->dirty = false;
-
-  h->st.epoch = h->epoch;
-  h->st.n_filters = nf;
-  h->st.n_trie_filters = n_trie;
-  h->st.n_route_keys = n_route;
-  h->st.n_nodes = n_nodes;
-  h->st.n_edges = edges.size();
-  h->st.edge_slots = ecap;
-  h->st.exact_slots = xcap * XBUCKET;
-  h->st.max_depth = max_depth;
-  h->st.device_bytes = ecap * SLOT_U4 * 16 + xcap * XBUCKET * 16 + multi.size() * 4 +
-                       n_nodes * 4 + h->pool.size() +
-                       (nf + 1) * 8 + nf * VREC;
+  commit_stats(h, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
+               delta);
   return 0;
 }
 
@@ -877,6 +1253,8 @@ void emqxgm_destroy(emqxgm_t* h) {
   free_bufs(h->sc_bufs);
   free_bufs(h->fan_bufs);
   free_bufs(h->fan_out_bufs);
+  free_bufs(h->fan_tab_bufs);
+  if (h->d_patch.p) (void)hipFree(h->d_patch.p);
   if (h->sc.ctl_host) (void)hipHostFree(h->sc.ctl_host);
   if (h->d_pool.p) (void)hipFree(h->d_pool.p);
   if (h->d_foff.p) (void)hipFree(h->d_foff.p);
@@ -896,6 +1274,7 @@ static int trie_insert_locked(emqxgm* h, const uint8_t* p, uint32_t len, uint32_
   if (!h->filters[i].in_trie) {
     h->filters[i].in_trie = 1;
     ++h->n_trie_pending;
+    h->changed.push_back(i);
     h->dirty = true;
   }
   if (id) *id = i;
@@ -908,6 +1287,7 @@ static int route_ref_locked(emqxgm* h, const uint8_t* p, uint32_t len, uint32_t*
   const uint32_t i = find_id(h, p, len, true);
   if (h->filters[i].route_refs++ == 0) {
     ++h->n_route_pending;
+    h->changed.push_back(i);
     h->dirty = true;
   }
   if (id) *id = i;
@@ -927,6 +1307,7 @@ int emqxgm_trie_delete(emqxgm_t* h, const uint8_t* filter, uint32_t len) {
   if (i != NONE && h->filters[i].in_trie) {  // absent filter: no-op (emqx_trie.erl:139-144)
     h->filters[i].in_trie = 0;
     --h->n_trie_pending;
+    h->changed.push_back(i);
     h->dirty = true;
   }
   return 0;
@@ -945,6 +1326,7 @@ int emqxgm_route_unref(emqxgm_t* h, const uint8_t* filter, uint32_t len) {
   if (i == NONE || h->filters[i].route_refs == 0) return -ENOENT;
   if (--h->filters[i].route_refs == 0) {
     --h->n_route_pending;
+    h->changed.push_back(i);
     h->dirty = true;
   }
   return 0;
@@ -964,8 +1346,10 @@ int emqxgm_route_add(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t 
   const std::pair<uint32_t, uint32_t> d(node, group);
   if (std::find(v.begin(), v.end(), d) != v.end()) return 0;  // already routed
   v.push_back(d);
+  h->fan_dirty = true;
   if (h->filters[i].route_refs++ == 0) {
     ++h->n_route_pending;
+    h->changed.push_back(i);
     // insert_trie_route: the first route of a wildcard filter (emqx_router_utils.erl:34-39)
     if (is_wild(filter, len) && !h->filters[i].in_trie) {
       h->filters[i].in_trie = 1;
@@ -989,8 +1373,10 @@ int emqxgm_route_delete(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32
   if (p == v.end()) return 0;  // absent route: no-op
   v.erase(p);
   if (v.empty()) h->rdest.erase(it);
+  h->fan_dirty = true;
   if (h->filters[i].route_refs && --h->filters[i].route_refs == 0) {
     --h->n_route_pending;
+    h->changed.push_back(i);
     // delete_trie_route: the last route of a wildcard filter (emqx_router_utils.erl:57-71)
     if (is_wild(filter, len) && h->filters[i].in_trie) {
       h->filters[i].in_trie = 0;
@@ -1006,6 +1392,7 @@ int emqxgm_set_local_node(emqxgm_t* h, uint32_t node) {
   std::lock_guard<std::mutex> g(h->mu);
   if (h->local_node != node) {
     h->local_node = node;
+    h->fan_dirty = true;
     h->dirty = true;
   }
   return 0;
@@ -1019,6 +1406,7 @@ int emqxgm_subscriber_add(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint
   auto& v = h->lsubs[i];
   if (std::find(v.begin(), v.end(), sub) == v.end()) {
     v.push_back(sub);
+    h->fan_dirty = true;
     h->dirty = true;
   }
   return 0;
@@ -1035,6 +1423,7 @@ int emqxgm_subscriber_delete(emqxgm_t* h, const uint8_t* filter, uint32_t len, u
   if (p == it->second.end()) return 0;
   it->second.erase(p);
   if (it->second.empty()) h->lsubs.erase(it);
+  h->fan_dirty = true;
   h->dirty = true;
   return 0;
 }
@@ -1267,6 +1656,11 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
     h->cfg.walk_wg_per_cu = (uint32_t)value;
     h->geom = walk_geometry(h->cfg.device, h->cfg.walk_wg_per_cu);
     return 0;  // spill scratch is re-sized by the next match (ensure_scratch)
+  }
+  if (strcmp(key, "delta_commit") == 0) {
+    if (value < 0 || value > 2) return -EINVAL;
+    h->delta_mode = (uint32_t)value;
+    return 0;
   }
   return -EINVAL;
 }

@@ -364,4 +364,23 @@ hipError_t launch_fanout(const DevIndex& ix, const Scratch& sc, FanScratch& fs, 
   return hipGetLastError();
 }
 
+// Delta commit (gm_engine.cpp commit_delta): entry e of `src` (w dwords) replaces entry idx[e]
+// of the table at dst.  One lane per dword; patches are a few thousand entries at most.
+__global__ void k_patch(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src,
+                        const uint64_t* __restrict__ idx, uint32_t n, uint32_t w) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint64_t)n * w) return;
+  const uint64_t e = i / w, j = i - e * w;
+  dst[idx[e] * w + j] = src[i];
+}
+
+hipError_t launch_patch(uint32_t* dst, const uint32_t* src, const uint64_t* idx, uint32_t n,
+                        uint32_t w, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint64_t lanes = (uint64_t)n * w;
+  hipLaunchKernelGGL(k_patch, dim3((uint32_t)((lanes + WG - 1) / WG)), dim3(WG), 0, s, dst, src,
+                     idx, n, w);
+  return hipGetLastError();
+}
+
 }  // namespace gm

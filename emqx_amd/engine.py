@@ -57,7 +57,8 @@ class _Stats(C.Structure):
                 ("legacy_batches", C.c_uint32), ("batches", C.c_uint64),
                 ("topics", C.c_uint64), ("pairs", C.c_uint64), ("rejected_pairs", C.c_uint64),
                 ("reruns", C.c_uint64), ("walk_ms", C.c_double), ("walk_launches", C.c_uint64),
-                ("total_ms", C.c_double)]
+                ("total_ms", C.c_double), ("full_commits", C.c_uint64),
+                ("delta_commits", C.c_uint64), ("last_commit_ms", C.c_double)]
 
 
 # name -> (restype, argtypes): exactly the entry points declared in include/emqx_gpumatch.h

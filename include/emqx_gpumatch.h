@@ -107,6 +107,9 @@ typedef struct emqxgm_stats {
   double walk_ms;           /* summed walk-kernel time (HIP events), if profiling is on */
   uint64_t walk_launches;
   double total_ms;          /* summed device time of whole match passes, if profiling is on */
+  uint64_t full_commits;    /* commits that rebuilt the device index */
+  uint64_t delta_commits;   /* commits that patched it in place (small deltas) */
+  double last_commit_ms;    /* host wall time of the last commit (build/patch + upload) */
 } emqxgm_stats;
 
 int emqxgm_abi_version(void);
@@ -187,7 +190,9 @@ int emqxgm_walk_census(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_of
                        uint32_t n, uint64_t bytes_len, uint64_t out[6]);
 
 int emqxgm_set_profiling(emqxgm_t* h, int on);
-/* Runtime tuning knobs: "walk_wg_per_cu" (persistent walk workgroups per CU). */
+/* Runtime tuning knobs: "walk_wg_per_cu" (persistent walk workgroups per CU);
+ * "delta_commit": 0 = every commit rebuilds the index, 1 = small deltas are patched in place
+ * (default), 2 = every delta that fits the tables' load bounds is patched in place. */
 int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value);
 int emqxgm_get_stats(emqxgm_t* h, emqxgm_stats* st);
 /* Last HIP error string seen by the handle (for diagnostics). */
