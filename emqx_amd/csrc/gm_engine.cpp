@@ -203,6 +203,16 @@ struct TrieModel {
   }
 };
 
+// Host side of the publish fan-out tables (gm_fanout.inc): entries per filter id and the used
+// and reserved sizes of the two append-only pools.
+struct FanModel {
+  bool valid = false;
+  uint64_t cap = 0;  // filter ids with an entry (0: no tables)
+  uint64_t rt_used = 0, rt_cap = 0, dl_used = 0, dl_cap = 0, garbage = 0;
+  std::vector<uint4> ent;
+  uint32_t *d_ent = nullptr, *d_rt = nullptr, *d_dl = nullptr;  // owned by emqxgm::fan_tab_bufs
+};
+
 inline bool bit(const std::vector<uint64_t>& b, uint64_t i) { return (b[i >> 6] >> (i & 63)) & 1; }
 inline void bset(std::vector<uint64_t>& b, uint64_t i) { b[i >> 6] |= 1ull << (i & 63); }
 inline void bclr(std::vector<uint64_t>& b, uint64_t i) { b[i >> 6] &= ~(1ull << (i & 63)); }
@@ -265,7 +275,9 @@ struct emqxgm {
   // ---- delta commits ----
   TrieModel tm;
   std::vector<uint32_t> changed;  // filter ids whose trie / route-key membership may differ
-  bool fan_dirty = true;          // fan-out registry changed since the fan tables were built
+  FanModel fm;
+  std::vector<uint32_t> fan_changed;  // filter ids whose fan-out lists may differ
+  bool fan_rebuild = false;           // every filter's lists may differ (local node changed)
   std::vector<DevBuf> fan_tab_bufs;
   DevBuf d_patch;
   uint32_t delta_mode = 1;        // 0: always rebuild, 1: delta when small, 2: delta if possible
@@ -421,62 +433,138 @@ int upload_pool(emqxgm* h) {
   return 0;
 }
 
-// Publish fan-out tables (gm_fanout.inc): per filter id, its aggre/1 entries (plain node dests,
-// then each group once: emqx_broker.erl:284-300) and, when it routes to the local node, its
-// local subscribers (dispatch/2, :326-355).  Rebuilt whenever the fan-out registry changed.
-int build_fan(emqxgm* h) {
-  const uint64_t nf = h->filters.size();
-  std::vector<uint32_t> rt_off, rt_dst, dl_off, dl_sub;
-  const bool fan = !h->rdest.empty() || !h->lsubs.empty();
-  std::vector<DevBuf> nb;
-  DevIndex& ix = h->ix;
-  if (fan) {
-    rt_off.assign(nf + 1, 0u);
-    dl_off.assign(nf + 1, 0u);
-    std::vector<uint32_t> groups;
-    for (uint32_t id = 0; id < nf; ++id) {
-      rt_off[id + 1] = rt_off[id];
-      dl_off[id + 1] = dl_off[id];
-      auto it = h->rdest.find(id);
-      if (it == h->rdest.end()) continue;
-      bool local = false;
-      groups.clear();
-      for (const auto& d : it->second) {
-        if (d.second == NONE) {
-          rt_dst.push_back(d.first);
-          local = local || d.first == h->local_node;
-        } else {
-          groups.push_back(EMQXGM_DEST_GROUP | d.second);
-        }
-      }
-      std::sort(groups.begin(), groups.end());
-      groups.erase(std::unique(groups.begin(), groups.end()), groups.end());
-      rt_dst.insert(rt_dst.end(), groups.begin(), groups.end());
-      rt_off[id + 1] = (uint32_t)rt_dst.size();
-      if (local) {
-        auto sit = h->lsubs.find(id);
-        if (sit != h->lsubs.end()) dl_sub.insert(dl_sub.end(), sit->second.begin(), sit->second.end());
-        dl_off[id + 1] = (uint32_t)dl_sub.size();
-      }
+// Publish fan-out lists of one filter id (gm_fanout.inc): its aggre/1 entries (plain node
+// dests, then each group once: emqx_broker.erl:284-300) and, when it routes to the local node,
+// its local subscribers (dispatch/2, :326-355).
+void fan_lists(emqxgm* h, uint32_t id, std::vector<uint32_t>& rt, std::vector<uint32_t>& dl,
+               std::vector<uint32_t>& groups) {
+  auto it = h->rdest.find(id);
+  if (it == h->rdest.end()) return;
+  bool local = false;
+  groups.clear();
+  for (const auto& d : it->second) {
+    if (d.second == NONE) {
+      rt.push_back(d.first);
+      local = local || d.first == h->local_node;
+    } else {
+      groups.push_back(EMQXGM_DEST_GROUP | d.second);
     }
+  }
+  std::sort(groups.begin(), groups.end());
+  groups.erase(std::unique(groups.begin(), groups.end()), groups.end());
+  rt.insert(rt.end(), groups.begin(), groups.end());
+  if (local) {
+    auto sit = h->lsubs.find(id);
+    if (sit != h->lsubs.end()) dl.insert(dl.end(), sit->second.begin(), sit->second.end());
+  }
+}
+
+// Full build of the fan-out tables: entries for every filter id (with headroom for new ids)
+// and both pools packed (with headroom for delta appends).
+int fan_full(emqxgm* h) {
+  const uint64_t nf = h->filters.size();
+  FanModel& m = h->fm;
+  m = FanModel();
+  DevIndex& ix = h->ix;
+  std::vector<DevBuf> nb;
+  if (!h->rdest.empty() || !h->lsubs.empty()) {
+    m.cap = nf + std::max<uint64_t>(4096, nf / 4);
+    m.ent.assign(m.cap, make_uint4(0u, 0u, 0u, 0u));
+    std::vector<uint32_t> rt, dl, groups;
+    for (uint32_t id = 0; id < nf; ++id) {
+      const uint32_t r0 = (uint32_t)rt.size(), d0 = (uint32_t)dl.size();
+      fan_lists(h, id, rt, dl, groups);
+      m.ent[id] = make_uint4(r0, (uint32_t)rt.size() - r0, d0, (uint32_t)dl.size() - d0);
+    }
+    m.rt_used = rt.size();
+    m.dl_used = dl.size();
+    m.rt_cap = m.rt_used + std::max<uint64_t>(16384, m.rt_used / 4);
+    m.dl_cap = m.dl_used + std::max<uint64_t>(16384, m.dl_used / 4);
+    if (m.rt_cap >= 0xFFFFFFFFull || m.dl_cap >= 0xFFFFFFFFull) {
+      h->err = "fan-out pools exceed 2^32 entries";
+      return -E2BIG;
+    }
+    rt.resize(m.rt_cap, 0u);
+    dl.resize(m.dl_cap, 0u);
     DevIndex t;
     int rc = 0;
-    if ((rc = dev_upload(h, nb, rt_off, &t.rt_off)) || (rc = dev_upload(h, nb, rt_dst, &t.rt_dst)) ||
-        (rc = dev_upload(h, nb, dl_off, &t.dl_off)) || (rc = dev_upload(h, nb, dl_sub, &t.dl_sub))) {
+    if ((rc = dev_upload(h, nb, m.ent, &t.fan)) || (rc = dev_upload(h, nb, rt, &t.rt_dst)) ||
+        (rc = dev_upload(h, nb, dl, &t.dl_sub))) {
       free_bufs(nb);
       return rc;
     }
-    ix.rt_off = t.rt_off;
+    ix.fan = t.fan;
     ix.rt_dst = t.rt_dst;
-    ix.dl_off = t.dl_off;
     ix.dl_sub = t.dl_sub;
+    m.d_ent = (uint32_t*)t.fan;
+    m.d_rt = (uint32_t*)t.rt_dst;
+    m.d_dl = (uint32_t*)t.dl_sub;
   } else {
-    ix.rt_off = ix.rt_dst = ix.dl_off = ix.dl_sub = nullptr;
+    ix.fan = nullptr;
+    ix.rt_dst = ix.dl_sub = nullptr;
   }
-  ix.fan_nf = fan ? (uint32_t)nf : 0u;
+  ix.fan_nf = (uint32_t)m.cap;
   free_bufs(h->fan_tab_bufs);
   h->fan_tab_bufs.swap(nb);
-  h->fan_dirty = false;
+  h->fan_changed.clear();
+  h->fan_rebuild = false;
+  m.valid = true;
+  return 0;
+}
+
+// Fan-out tables after a registry change: a changed filter's lists are appended to the pools
+// and its entry re-pointed (k_patch); a full build when the tables are absent, an id or a pool
+// passes its headroom, stale entries pass half the pools, or the local node changed.
+int fan_commit(emqxgm* h) {
+  FanModel& m = h->fm;
+  auto& ch = h->fan_changed;
+  if (!m.valid || h->fan_rebuild || (m.cap == 0 && !ch.empty())) return fan_full(h);
+  if (ch.empty()) return 0;
+  std::sort(ch.begin(), ch.end());
+  ch.erase(std::unique(ch.begin(), ch.end()), ch.end());
+  std::vector<uint32_t> rt, dl, groups, src;
+  std::vector<uint64_t> idx;
+  uint64_t garbage = m.garbage;
+  for (uint32_t id : ch) {
+    if (id >= m.cap) return fan_full(h);
+    const uint32_t r0 = (uint32_t)rt.size(), d0 = (uint32_t)dl.size();
+    fan_lists(h, id, rt, dl, groups);
+    const uint4 old = m.ent[id];
+    garbage += old.y + old.w;
+    const uint4 e = make_uint4((uint32_t)(m.rt_used + r0), (uint32_t)rt.size() - r0,
+                               (uint32_t)(m.dl_used + d0), (uint32_t)dl.size() - d0);
+    m.ent[id] = e;
+    idx.push_back(id);
+    src.insert(src.end(), {e.x, e.y, e.z, e.w});
+  }
+  if (m.rt_used + rt.size() > m.rt_cap || m.dl_used + dl.size() > m.dl_cap ||
+      garbage * 2 > m.rt_used + m.dl_used + 65536)
+    return fan_full(h);
+  const uint64_t words = src.size();
+  const uint64_t need = words * 4 + idx.size() * 8 + 16;
+  if (need > h->d_patch.bytes) {
+    if (h->d_patch.p) (void)hipFree(h->d_patch.p);
+    h->d_patch = DevBuf();
+    const uint64_t bytes = std::max<uint64_t>(need, 1u << 20);
+    HIPCHK(h, hipMalloc(&h->d_patch.p, bytes));
+    h->d_patch.bytes = bytes;
+  }
+  uint32_t* d_src = (uint32_t*)h->d_patch.p;
+  uint64_t* d_idx = (uint64_t*)((uint8_t*)h->d_patch.p + ((words * 4 + 15) & ~15ull));
+  if (!rt.empty())
+    HIPCHK(h, hipMemcpyAsync(m.d_rt + m.rt_used, rt.data(), rt.size() * 4, hipMemcpyHostToDevice,
+                             h->stream));
+  if (!dl.empty())
+    HIPCHK(h, hipMemcpyAsync(m.d_dl + m.dl_used, dl.data(), dl.size() * 4, hipMemcpyHostToDevice,
+                             h->stream));
+  HIPCHK(h, hipMemcpyAsync(d_src, src.data(), words * 4, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(d_idx, idx.data(), idx.size() * 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, launch_patch(m.d_ent, d_src, d_idx, (uint32_t)idx.size(), 4, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  m.rt_used += rt.size();
+  m.dl_used += dl.size();
+  m.garbage = garbage;
+  ch.clear();
   return 0;
 }
 
@@ -631,7 +719,7 @@ int commit_full(emqxgm* h) {
   // ---- upload and swap ----
   if (hipSetDevice(h->cfg.device) != hipSuccess) return fail(h, hipErrorInvalidDevice, "hipSetDevice");
   int rc = 0;
-  if ((rc = upload_pool(h)) || (rc = build_fan(h))) return rc;
+  if ((rc = upload_pool(h)) || (rc = fan_full(h))) return rc;
   std::vector<DevBuf> nbufs;
   DevIndex nx = h->ix;  // pool and fan-out pointers just set
   if ((rc = dev_upload(h, nbufs, eslots, &nx.edges)) ||
@@ -881,7 +969,7 @@ int commit_delta(emqxgm* h) {
   // ---- upload ----
   if (hipSetDevice(h->cfg.device) != hipSuccess) return fail(h, hipErrorInvalidDevice, "hipSetDevice");
   int rc = 0;
-  if ((rc = upload_pool(h)) || (h->fan_dirty && (rc = build_fan(h)))) return rc;
+  if ((rc = upload_pool(h))) return rc;
   const uint64_t need = words * 4 + idx.size() * 8 + 16;
   if (need > h->d_patch.bytes) {
     if (h->d_patch.p) (void)hipFree(h->d_patch.p);
@@ -903,6 +991,7 @@ int commit_delta(emqxgm* h) {
     HIPCHK(h, hipMemcpyAsync(m.d_fv, m.fvbits.data(), ((nf + 31) / 32 + 1) * 4,
                              hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
+  if ((rc = fan_commit(h))) return rc;
 
   DevIndex& ix = h->ix;
   const uint32_t root_p = m.pchild[0];
@@ -1346,7 +1435,7 @@ int emqxgm_route_add(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t 
   const std::pair<uint32_t, uint32_t> d(node, group);
   if (std::find(v.begin(), v.end(), d) != v.end()) return 0;  // already routed
   v.push_back(d);
-  h->fan_dirty = true;
+  h->fan_changed.push_back(i);
   if (h->filters[i].route_refs++ == 0) {
     ++h->n_route_pending;
     h->changed.push_back(i);
@@ -1373,7 +1462,7 @@ int emqxgm_route_delete(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32
   if (p == v.end()) return 0;  // absent route: no-op
   v.erase(p);
   if (v.empty()) h->rdest.erase(it);
-  h->fan_dirty = true;
+  h->fan_changed.push_back(i);
   if (h->filters[i].route_refs && --h->filters[i].route_refs == 0) {
     --h->n_route_pending;
     h->changed.push_back(i);
@@ -1392,7 +1481,7 @@ int emqxgm_set_local_node(emqxgm_t* h, uint32_t node) {
   std::lock_guard<std::mutex> g(h->mu);
   if (h->local_node != node) {
     h->local_node = node;
-    h->fan_dirty = true;
+    h->fan_rebuild = true;
     h->dirty = true;
   }
   return 0;
@@ -1406,7 +1495,7 @@ int emqxgm_subscriber_add(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint
   auto& v = h->lsubs[i];
   if (std::find(v.begin(), v.end(), sub) == v.end()) {
     v.push_back(sub);
-    h->fan_dirty = true;
+    h->fan_changed.push_back(i);
     h->dirty = true;
   }
   return 0;
@@ -1423,7 +1512,7 @@ int emqxgm_subscriber_delete(emqxgm_t* h, const uint8_t* filter, uint32_t len, u
   if (p == it->second.end()) return 0;
   it->second.erase(p);
   if (it->second.empty()) h->lsubs.erase(it);
-  h->fan_dirty = true;
+  h->fan_changed.push_back(i);
   h->dirty = true;
   return 0;
 }

@@ -14,10 +14,9 @@ struct DevIndex {
   uint32_t root_pcf = 0, root_phf = 0xFFFFFFFFu;  // root's '+' child (cf 0: none)
   const uint32_t* tn_of = nullptr;  // per node: non-wildcard trie keys ending there
   // publish fan-out tables (gm_fanout.inc), per filter id < fan_nf
-  const uint32_t* rt_off = nullptr;  // [fan_nf+1] aggre entries
-  const uint32_t* rt_dst = nullptr;
-  const uint32_t* dl_off = nullptr;  // [fan_nf+1] local deliveries
-  const uint32_t* dl_sub = nullptr;
+  const uint4* fan = nullptr;        // [fan_nf] {rt off, rt count, dl off, dl count}
+  const uint32_t* rt_dst = nullptr;  // aggre entries (dest handles)
+  const uint32_t* dl_sub = nullptr;  // local deliveries (subscriber ids)
   uint32_t fan_nf = 0;
   const uint4* exact = nullptr;   // exact buckets of XBUCKET {hash.lo, hash.hi, fid, len}
   uint64_t xmask = 0;             // bucket count - 1

@@ -344,9 +344,8 @@ hipError_t launch_fanout(const DevIndex& ix, const Scratch& sc, FanScratch& fs, 
   a.row = sc.row;
   a.fid = sc.out;
   a.exact_id = sc.exact_id;
-  a.rt_off = ix.rt_off;
+  a.fan = ix.fan;
   a.rt_dst = ix.rt_dst;
-  a.dl_off = ix.dl_off;
   a.dl_sub = ix.dl_sub;
   a.nf = ix.fan_nf;
   a.cr = fs.cr;

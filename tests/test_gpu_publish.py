@@ -116,3 +116,36 @@ def test_publish_random(emqx):
         x.unsubscribe(f, f"s{rng.randrange(40)}")
         x.delete_route(f, "n2")
     x.check(topics[:3000])
+
+
+def test_publish_churn_delta_commits(emqx):
+    """Rounds of subscribe / unsubscribe / route churn, each committed as a delta: the fan-out
+    entries of changed filters are re-pointed at appended lists (gm_engine.cpp fan_commit),
+    and every round's publish fan-out equals the oracle's."""
+    rng = random.Random(17)
+    x = _Both(emqx)
+    vocab = ["a", "b", "c", "+", "dd"]
+    filters = sorted({"/".join(rng.choice(vocab) for _ in range(rng.randint(1, 4))).encode()
+                      for _ in range(400)} | {b"#", b"a/#", b"+/#"})
+    topics = ["/".join(rng.choice(["a", "b", "c", "dd", "e"]) for _ in range(rng.randint(1, 5)))
+              .encode() for _ in range(1500)]
+    for f in filters[:200]:
+        x.subscribe(f, f"s{rng.randrange(20)}")
+    x.check(topics)
+    for _ in range(12):
+        for _ in range(rng.randint(5, 60)):
+            f = rng.choice(filters)
+            r = rng.random()
+            if r < 0.35:
+                x.subscribe(f, f"s{rng.randrange(20)}")
+            elif r < 0.6:
+                x.unsubscribe(f, rng.choice(x.subs.get(f, ["none"])))
+            elif r < 0.75:
+                x.add_route(f, rng.choice(["n2", "n3"]))
+            elif r < 0.85:
+                x.add_route(f, (rng.choice([b"g1", b"g2"]), rng.choice(["n1", "n2"])))
+            else:
+                x.delete_route(f, rng.choice(["n2", "n3", (b"g1", "n1"), (b"g2", "n2")]))
+        x.check(topics)
+    st = x.b.engine.stats()
+    assert st["delta_commits"] >= 10, st
