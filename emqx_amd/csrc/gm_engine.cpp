@@ -150,6 +150,29 @@ struct DevBuf {
 
 constexpr uint64_t DEAD = ~0ull;  // TrieModel::slot of the root and of removed nodes
 
+// Device writes staged by one commit (k_patch): dword runs to device addresses, uploaded in
+// one copy and applied by one launch on the engine stream.
+struct PatchList {
+  std::vector<PatchEnt> ents;
+  std::vector<uint32_t> src;
+  void add(void* dst, const void* vals, uint64_t words) {
+    const uint32_t* v = (const uint32_t*)vals;
+    uint8_t* d = (uint8_t*)dst;
+    while (words) {
+      const uint32_t w = (uint32_t)std::min<uint64_t>(words, 64);
+      ents.push_back(PatchEnt{(uint64_t)(uintptr_t)d, (uint32_t)src.size(), w});
+      src.insert(src.end(), v, v + w);
+      v += w;
+      d += 4ull * w;
+      words -= w;
+    }
+  }
+  void clear() {
+    ents.clear();
+    src.clear();
+  }
+};
+
 // Host model of the committed trie and exact table, kept so that a commit with a small delta
 // patches the device tables in place (commit_delta) instead of rebuilding them.  A slot's 32 B
 // are a function of its node's state (node_slot), so only positions and occupancy are mirrored.
@@ -279,7 +302,11 @@ struct emqxgm {
   std::vector<uint32_t> fan_changed;  // filter ids whose fan-out lists may differ
   bool fan_rebuild = false;           // every filter's lists may differ (local node changed)
   std::vector<DevBuf> fan_tab_bufs;
-  DevBuf d_patch;
+  PatchList patches;
+  DevBuf d_patch;                   // device copy of the staged patch list
+  uint8_t* h_stage = nullptr;       // pinned host staging of the patch list
+  uint64_t h_stage_bytes = 0;
+  hipEvent_t patch_ev = nullptr;    // the last patch upload + launch
   uint32_t delta_mode = 1;        // 0: always rebuild, 1: delta when small, 2: delta if possible
 };
 
@@ -390,25 +417,78 @@ struct ListBuild {
 };
 
 // Grow-and-append a device mirror of an append-only host array (bytes [uploaded, total)).
-int append_upload(emqxgm* h, DevBuf& buf, uint64_t& uploaded, const void* src, uint64_t total) {
-  const uint64_t need = std::max<uint64_t>(16, total);
+// Without growth and with a patch list, the new tail (whole dwords) goes into the list.
+int append_upload(emqxgm* h, DevBuf& buf, uint64_t& uploaded, const void* src, uint64_t total,
+                  PatchList* pl) {
+  const uint64_t need = std::max<uint64_t>(16, (total + 3) & ~3ull);
   if (need > buf.bytes) {
+    HIPCHK(h, hipStreamSynchronize(h->stream));
     DevBuf nb;
     nb.bytes = std::max<uint64_t>(need, buf.bytes * 2);
     HIPCHK(h, hipMalloc(&nb.p, nb.bytes));
     if (uploaded) HIPCHK(h, hipMemcpy(nb.p, buf.p, uploaded, hipMemcpyDeviceToDevice));
     if (buf.p) (void)hipFree(buf.p);
     buf = nb;
+    pl = nullptr;
   }
-  if (total > uploaded)
-    HIPCHK(h, hipMemcpy((uint8_t*)buf.p + uploaded, (const uint8_t*)src + uploaded,
-                        total - uploaded, hipMemcpyHostToDevice));
+  if (total > uploaded) {
+    if (pl) {
+      const uint64_t a = uploaded & ~3ull;
+      std::vector<uint32_t> tmp((total - a + 3) / 4, 0u);
+      memcpy(tmp.data(), (const uint8_t*)src + a, total - a);
+      pl->add((uint8_t*)buf.p + a, tmp.data(), tmp.size());
+    } else {
+      HIPCHK(h, hipMemcpy((uint8_t*)buf.p + uploaded, (const uint8_t*)src + uploaded,
+                          total - uploaded, hipMemcpyHostToDevice));
+    }
+  }
   uploaded = total;
   return 0;
 }
 
-// Filter string pool, offsets and 64-B verification records: append-only device mirrors.
-int upload_pool(emqxgm* h) {
+// Upload the staged patch list: one copy through pinned memory and one k_patch launch on the
+// engine stream (matches are ordered behind it).  patch_wait() before the staging is reused
+// or a patched buffer is freed.
+int patch_wait(emqxgm* h) {
+  if (h->patch_ev) HIPCHK(h, hipEventSynchronize(h->patch_ev));
+  return 0;
+}
+
+int patch_flush(emqxgm* h) {
+  PatchList& pl = h->patches;
+  if (pl.ents.empty()) return 0;
+  int rc = patch_wait(h);
+  if (rc) return rc;
+  const uint64_t eb = pl.ents.size() * sizeof(PatchEnt), total = eb + pl.src.size() * 4;
+  if (total > h->h_stage_bytes) {
+    if (h->h_stage) (void)hipHostFree(h->h_stage);
+    h->h_stage = nullptr;
+    h->h_stage_bytes = 0;
+    const uint64_t bytes = std::max<uint64_t>(total * 2, 1u << 16);
+    HIPCHK(h, hipHostMalloc((void**)&h->h_stage, bytes, hipHostMallocDefault));
+    h->h_stage_bytes = bytes;
+  }
+  if (total > h->d_patch.bytes) {
+    if (h->d_patch.p) (void)hipFree(h->d_patch.p);
+    h->d_patch = DevBuf();
+    const uint64_t bytes = std::max<uint64_t>(total * 2, 1u << 16);
+    HIPCHK(h, hipMalloc(&h->d_patch.p, bytes));
+    h->d_patch.bytes = bytes;
+  }
+  memcpy(h->h_stage, pl.ents.data(), eb);
+  memcpy(h->h_stage + eb, pl.src.data(), pl.src.size() * 4);
+  HIPCHK(h, hipMemcpyAsync(h->d_patch.p, h->h_stage, total, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, launch_patch((const PatchEnt*)h->d_patch.p, (uint32_t)pl.ents.size(),
+                         (const uint32_t*)((uint8_t*)h->d_patch.p + eb), h->stream));
+  if (!h->patch_ev) HIPCHK(h, hipEventCreateWithFlags(&h->patch_ev, hipEventDisableTiming));
+  HIPCHK(h, hipEventRecord(h->patch_ev, h->stream));
+  pl.clear();
+  return 0;
+}
+
+// Filter string pool, offsets and 64-B verification records: append-only device mirrors
+// (pl: stage the appended tails in a delta commit's patch list).
+int upload_pool(emqxgm* h, PatchList* pl) {
   const uint64_t nf = h->filters.size();
   if (h->foff_host.empty()) h->foff_host.push_back(0);
   for (uint64_t i = h->foff_host.size() - 1; i < nf; ++i)  // pool is append-only
@@ -421,11 +501,11 @@ int upload_pool(emqxgm* h) {
     h->fver_host.insert(h->fver_host.end(), r, r + VREC);
   }
   int rc = 0;
-  if ((rc = append_upload(h, h->d_pool, h->pool_uploaded, h->pool.data(), h->pool.size())) ||
+  if ((rc = append_upload(h, h->d_pool, h->pool_uploaded, h->pool.data(), h->pool.size(), pl)) ||
       (rc = append_upload(h, h->d_foff, h->foff_uploaded, h->foff_host.data(),
-                          h->foff_host.size() * sizeof(uint64_t))) ||
+                          h->foff_host.size() * sizeof(uint64_t), pl)) ||
       (rc = append_upload(h, h->d_fver, h->fver_uploaded, h->fver_host.data(),
-                          h->fver_host.size())))
+                          h->fver_host.size(), pl)))
     return rc;
   h->ix.fbytes = (const uint8_t*)h->d_pool.p;
   h->ix.foff = (const uint64_t*)h->d_foff.p;
@@ -522,8 +602,7 @@ int fan_commit(emqxgm* h) {
   if (ch.empty()) return 0;
   std::sort(ch.begin(), ch.end());
   ch.erase(std::unique(ch.begin(), ch.end()), ch.end());
-  std::vector<uint32_t> rt, dl, groups, src;
-  std::vector<uint64_t> idx;
+  std::vector<uint32_t> rt, dl, groups, changed;
   uint64_t garbage = m.garbage;
   for (uint32_t id : ch) {
     if (id >= m.cap) return fan_full(h);
@@ -534,33 +613,15 @@ int fan_commit(emqxgm* h) {
     const uint4 e = make_uint4((uint32_t)(m.rt_used + r0), (uint32_t)rt.size() - r0,
                                (uint32_t)(m.dl_used + d0), (uint32_t)dl.size() - d0);
     m.ent[id] = e;
-    idx.push_back(id);
-    src.insert(src.end(), {e.x, e.y, e.z, e.w});
+    changed.push_back(id);
   }
   if (m.rt_used + rt.size() > m.rt_cap || m.dl_used + dl.size() > m.dl_cap ||
       garbage * 2 > m.rt_used + m.dl_used + 65536)
     return fan_full(h);
-  const uint64_t words = src.size();
-  const uint64_t need = words * 4 + idx.size() * 8 + 16;
-  if (need > h->d_patch.bytes) {
-    if (h->d_patch.p) (void)hipFree(h->d_patch.p);
-    h->d_patch = DevBuf();
-    const uint64_t bytes = std::max<uint64_t>(need, 1u << 20);
-    HIPCHK(h, hipMalloc(&h->d_patch.p, bytes));
-    h->d_patch.bytes = bytes;
-  }
-  uint32_t* d_src = (uint32_t*)h->d_patch.p;
-  uint64_t* d_idx = (uint64_t*)((uint8_t*)h->d_patch.p + ((words * 4 + 15) & ~15ull));
-  if (!rt.empty())
-    HIPCHK(h, hipMemcpyAsync(m.d_rt + m.rt_used, rt.data(), rt.size() * 4, hipMemcpyHostToDevice,
-                             h->stream));
-  if (!dl.empty())
-    HIPCHK(h, hipMemcpyAsync(m.d_dl + m.dl_used, dl.data(), dl.size() * 4, hipMemcpyHostToDevice,
-                             h->stream));
-  HIPCHK(h, hipMemcpyAsync(d_src, src.data(), words * 4, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, hipMemcpyAsync(d_idx, idx.data(), idx.size() * 8, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, launch_patch(m.d_ent, d_src, d_idx, (uint32_t)idx.size(), 4, h->stream));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  PatchList& pl = h->patches;
+  pl.add(m.d_rt + m.rt_used, rt.data(), rt.size());
+  pl.add(m.d_dl + m.dl_used, dl.data(), dl.size());
+  for (uint32_t id : changed) pl.add(m.d_ent + 4ull * id, &m.ent[id], 4);
   m.rt_used += rt.size();
   m.dl_used += dl.size();
   m.garbage = garbage;
@@ -719,7 +780,7 @@ int commit_full(emqxgm* h) {
   // ---- upload and swap ----
   if (hipSetDevice(h->cfg.device) != hipSuccess) return fail(h, hipErrorInvalidDevice, "hipSetDevice");
   int rc = 0;
-  if ((rc = upload_pool(h)) || (rc = fan_full(h))) return rc;
+  if ((rc = upload_pool(h, nullptr)) || (rc = fan_full(h))) return rc;
   std::vector<DevBuf> nbufs;
   DevIndex nx = h->ix;  // pool and fan-out pointers just set
   if ((rc = dev_upload(h, nbufs, eslots, &nx.edges)) ||
@@ -792,7 +853,7 @@ int commit_delta(emqxgm* h) {
   std::unordered_map<uint64_t, uint32_t> epatch;  // edge slot -> node (NONE: TOMB)
   std::unordered_map<uint64_t, uint4> xpatch;     // exact entry -> content
   std::vector<uint32_t> dirty;                    // nodes whose slot / side entry changed
-  bool fv_changed = false;
+  std::vector<uint32_t> fv_words;  // changed words of the verify bitmap
   std::vector<uint64_t> toks;
   std::vector<uint8_t> is_plus, is_hash;
   std::vector<uint32_t> path;
@@ -843,7 +904,7 @@ int commit_delta(emqxgm* h) {
     if (hashed) {
       m.fvbits[id >> 5] |= 1u << (id & 31);
       m.needs_verify = true;
-      fv_changed = true;
+      fv_words.push_back(id >> 5);
     }
     const size_t nw = toks.size();
     const bool hash_last = is_hash[nw - 1];
@@ -940,58 +1001,21 @@ int commit_delta(emqxgm* h) {
     const uint32_t par = n ? m.parent[n] : NONE;
     if (par != NONE && par != 0 && m.pchild[par] == n) epatch[m.slot[par]] = par;
   }
-  const uint32_t ne = (uint32_t)epatch.size(), nx = (uint32_t)xpatch.size();
-  const uint32_t nt = (uint32_t)tn_nodes.size();
-  const uint64_t words = (uint64_t)ne * 8 + (uint64_t)nx * 4 + nt;
-  std::vector<uint32_t> src(words);
-  std::vector<uint64_t> idx((uint64_t)ne + nx + nt);
-  {
-    uint64_t k = 0;
-    uint32_t* w = src.data();
-    for (const auto& p : epatch) {
-      idx[k++] = p.first;
-      uint4 sl[2] = {make_uint4(0u, 0u, TOMB, 0u), make_uint4(0u, 0u, 0u, 0u)};
-      if (p.second != NONE) m.node_slot(p.second, sl);
-      memcpy(w, sl, 32);
-      w += 8;
-    }
-    for (const auto& p : xpatch) {
-      idx[k++] = p.first;
-      memcpy(w, &p.second, 16);
-      w += 4;
-    }
-    for (uint32_t n : tn_nodes) {
-      idx[k++] = n;
-      *w++ = m.tn[n];
-    }
-  }
-
-  // ---- upload ----
+  // ---- stage the patches, upload them in one copy, apply them in one launch ----
   if (hipSetDevice(h->cfg.device) != hipSuccess) return fail(h, hipErrorInvalidDevice, "hipSetDevice");
-  int rc = 0;
-  if ((rc = upload_pool(h))) return rc;
-  const uint64_t need = words * 4 + idx.size() * 8 + 16;
-  if (need > h->d_patch.bytes) {
-    if (h->d_patch.p) (void)hipFree(h->d_patch.p);
-    h->d_patch = DevBuf();
-    const uint64_t bytes = std::max<uint64_t>(need, 1u << 20);
-    HIPCHK(h, hipMalloc(&h->d_patch.p, bytes));
-    h->d_patch.bytes = bytes;
+  PatchList& pl = h->patches;
+  for (const auto& p : epatch) {
+    uint4 sl[2] = {make_uint4(0u, 0u, TOMB, 0u), make_uint4(0u, 0u, 0u, 0u)};
+    if (p.second != NONE) m.node_slot(p.second, sl);
+    pl.add(m.d_edges + 8 * p.first, sl, 8);
   }
-  uint32_t* d_src = (uint32_t*)h->d_patch.p;
-  uint64_t* d_idx = (uint64_t*)((uint8_t*)h->d_patch.p + ((words * 4 + 15) & ~15ull));
-  if (words) HIPCHK(h, hipMemcpyAsync(d_src, src.data(), words * 4, hipMemcpyHostToDevice, h->stream));
-  if (!idx.empty())
-    HIPCHK(h, hipMemcpyAsync(d_idx, idx.data(), idx.size() * 8, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, launch_patch(m.d_edges, d_src, d_idx, ne, 8, h->stream));
-  HIPCHK(h, launch_patch(m.d_exact, d_src + (uint64_t)ne * 8, d_idx + ne, nx, 4, h->stream));
-  HIPCHK(h, launch_patch(m.d_tn, d_src + (uint64_t)ne * 8 + (uint64_t)nx * 4, d_idx + ne + nx, nt, 1,
-                         h->stream));
-  if (fv_changed)
-    HIPCHK(h, hipMemcpyAsync(m.d_fv, m.fvbits.data(), ((nf + 31) / 32 + 1) * 4,
-                             hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
-  if ((rc = fan_commit(h))) return rc;
+  for (const auto& p : xpatch) pl.add(m.d_exact + 4 * p.first, &p.second, 4);
+  for (uint32_t n : tn_nodes) pl.add(m.d_tn + n, &m.tn[n], 1);
+  std::sort(fv_words.begin(), fv_words.end());
+  fv_words.erase(std::unique(fv_words.begin(), fv_words.end()), fv_words.end());
+  for (uint32_t w : fv_words) pl.add(m.d_fv + w, &m.fvbits[w], 1);
+  int rc = 0;
+  if ((rc = upload_pool(h, &pl)) || (rc = fan_commit(h)) || (rc = patch_flush(h))) return rc;
 
   DevIndex& ix = h->ix;
   const uint32_t root_p = m.pchild[0];
@@ -1016,7 +1040,10 @@ int commit_delta(emqxgm* h) {
 // Make the pending registry the committed index: a delta commit when it fits, else a full build.
 int commit_locked(emqxgm* h) {
   const auto t0 = std::chrono::steady_clock::now();
-  int rc = commit_delta(h);
+  h->patches.clear();
+  int rc = patch_wait(h);  // the previous commit's patches are applied before buffers change
+  if (rc) return rc;
+  rc = commit_delta(h);
   const bool delta = rc == 0;
   if (rc > 0) rc = commit_full(h);
   if (rc) return rc;
@@ -1344,6 +1371,8 @@ void emqxgm_destroy(emqxgm_t* h) {
   free_bufs(h->fan_out_bufs);
   free_bufs(h->fan_tab_bufs);
   if (h->d_patch.p) (void)hipFree(h->d_patch.p);
+  if (h->h_stage) (void)hipHostFree(h->h_stage);
+  if (h->patch_ev) (void)hipEventDestroy(h->patch_ev);
   if (h->sc.ctl_host) (void)hipHostFree(h->sc.ctl_host);
   if (h->d_pool.p) (void)hipFree(h->d_pool.p);
   if (h->d_foff.p) (void)hipFree(h->d_foff.p);

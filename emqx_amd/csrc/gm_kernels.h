@@ -116,9 +116,12 @@ struct FanScratch {
   uint32_t *cr = nullptr, *cd = nullptr, *rp = nullptr, *dp = nullptr;
   uint32_t *o_rf = nullptr, *o_rd = nullptr, *o_df = nullptr, *o_ds = nullptr;
 };
-// dst[idx[e] * w + j] = src[e * w + j] for e < n, j < w (dword entries; delta commits)
-hipError_t launch_patch(uint32_t* dst, const uint32_t* src, const uint64_t* idx, uint32_t n,
-                        uint32_t w, hipStream_t s);
+// One patch of a delta commit: w (1..64) dwords from src[s..] to the device address dst.
+struct PatchEnt {
+  uint64_t dst;
+  uint32_t s, w;
+};
+hipError_t launch_patch(const PatchEnt* ents, uint32_t n, const uint32_t* src, hipStream_t s);
 // count pass (fill = false) or fill pass over the match result in sc (row, out, exact_id)
 hipError_t launch_fanout(const DevIndex& ix, const Scratch& sc, FanScratch& fs, uint32_t n,
                          bool fill, hipStream_t s);

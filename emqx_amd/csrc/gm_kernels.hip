@@ -363,22 +363,25 @@ hipError_t launch_fanout(const DevIndex& ix, const Scratch& sc, FanScratch& fs, 
   return hipGetLastError();
 }
 
-// Delta commit (gm_engine.cpp commit_delta): entry e of `src` (w dwords) replaces entry idx[e]
-// of the table at dst.  One lane per dword; patches are a few thousand entries at most.
-__global__ void k_patch(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src,
-                        const uint64_t* __restrict__ idx, uint32_t n, uint32_t w) {
+// Delta commit (gm_engine.cpp PatchList): entry e copies ents[e].w (<= 64) dwords from
+// src + ents[e].s to the device address ents[e].dst, lane j of wave e copying dword j.  Every
+// table a commit touches (edge slots, exact entries, node side array, verify bits, pools,
+// fan-out entries) goes in one list: one upload and one launch per commit.
+__global__ void k_patch(const PatchEnt* __restrict__ ents, uint32_t n,
+                        const uint32_t* __restrict__ src) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (uint64_t)n * w) return;
-  const uint64_t e = i / w, j = i - e * w;
-  dst[idx[e] * w + j] = src[i];
+  const uint64_t e = i >> 6;
+  const uint32_t j = (uint32_t)(i & 63);
+  if (e >= n) return;
+  const PatchEnt p = ents[e];
+  if (j < p.w) ((uint32_t*)p.dst)[j] = src[p.s + j];
 }
 
-hipError_t launch_patch(uint32_t* dst, const uint32_t* src, const uint64_t* idx, uint32_t n,
-                        uint32_t w, hipStream_t s) {
+hipError_t launch_patch(const PatchEnt* ents, uint32_t n, const uint32_t* src, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const uint64_t lanes = (uint64_t)n * w;
-  hipLaunchKernelGGL(k_patch, dim3((uint32_t)((lanes + WG - 1) / WG)), dim3(WG), 0, s, dst, src,
-                     idx, n, w);
+  const uint64_t lanes = (uint64_t)n * 64;
+  hipLaunchKernelGGL(k_patch, dim3((uint32_t)((lanes + WG - 1) / WG)), dim3(WG), 0, s, ents, n,
+                     src);
   return hipGetLastError();
 }
 
