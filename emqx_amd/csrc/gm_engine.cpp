@@ -304,6 +304,7 @@ struct emqxgm {
   std::vector<DevBuf> fan_tab_bufs;
   PatchList patches;
   DevBuf d_patch;                   // device copy of the staged patch list
+  DevBuf d_rules;                   // emqxgm_match_rules inputs and output
   uint8_t* h_stage = nullptr;       // pinned host staging of the patch list
   uint64_t h_stage_bytes = 0;
   hipEvent_t patch_ev = nullptr;    // the last patch upload + launch
@@ -1373,6 +1374,7 @@ void emqxgm_destroy(emqxgm_t* h) {
   if (h->d_patch.p) (void)hipFree(h->d_patch.p);
   if (h->h_stage) (void)hipHostFree(h->h_stage);
   if (h->patch_ev) (void)hipEventDestroy(h->patch_ev);
+  if (h->d_rules.p) (void)hipFree(h->d_rules.p);
   if (h->sc.ctl_host) (void)hipHostFree(h->sc.ctl_host);
   if (h->d_pool.p) (void)hipFree(h->d_pool.p);
   if (h->d_foff.p) (void)hipFree(h->d_foff.p);
@@ -1757,6 +1759,55 @@ int emqxgm_walk_census(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_of
   uint32_t pairs = 0;
   memset(out, 0, 6 * sizeof(uint64_t));
   return run_device(h, d_bytes, d_offsets, n, bytes_len, &pairs, out);
+}
+
+static int grow_buf(emqxgm* h, DevBuf& b, uint64_t bytes) {
+  if (bytes <= b.bytes && b.p) return 0;
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (b.p) (void)hipFree(b.p);
+  b = DevBuf();
+  const uint64_t cap = std::max<uint64_t>(bytes + bytes / 2, 4096);
+  HIPCHK(h, hipMalloc(&b.p, cap));
+  b.bytes = cap;
+  return 0;
+}
+
+int emqxgm_match_rules(emqxgm_t* h, const uint8_t* name_bytes, const uint32_t* name_offsets,
+                       uint32_t n, const uint8_t* rule_bytes, const uint32_t* rule_offsets,
+                       const uint32_t* rule_flags, uint32_t n_rules, uint32_t* out) {
+  if (!h || !name_offsets || !rule_offsets || (n && !out) || (n_rules && !rule_flags))
+    return -EINVAL;
+  const uint64_t nb = name_offsets[n], rb = rule_offsets[n_rules];
+  if ((nb && !name_bytes) || (rb && !rule_bytes)) return -EINVAL;
+  for (uint32_t i = 0; i < n; ++i)
+    if (name_offsets[i + 1] < name_offsets[i]) return -EINVAL;
+  for (uint32_t i = 0; i < n_rules; ++i)
+    if (rule_offsets[i + 1] < rule_offsets[i]) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (n == 0) return 0;
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
+  // one device buffer: [names | name offsets | rules | rule offsets | flags | out]
+  auto al = [](uint64_t x) { return (x + 15) & ~15ull; };
+  const uint64_t o_no = al(nb), o_rb = o_no + al(((uint64_t)n + 1) * 4), o_ro = o_rb + al(rb);
+  const uint64_t o_rf = o_ro + al(((uint64_t)n_rules + 1) * 4);
+  const uint64_t o_out = o_rf + al((uint64_t)n_rules * 4 + 4);
+  const uint64_t total = o_out + (uint64_t)n * 4;
+  int rc = grow_buf(h, h->d_rules, total);
+  if (rc) return rc;
+  uint8_t* d = (uint8_t*)h->d_rules.p;
+  hipStream_t s = h->stream;
+  if (nb) HIPCHK(h, hipMemcpyAsync(d, name_bytes, nb, hipMemcpyHostToDevice, s));
+  HIPCHK(h, hipMemcpyAsync(d + o_no, name_offsets, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s));
+  if (rb) HIPCHK(h, hipMemcpyAsync(d + o_rb, rule_bytes, rb, hipMemcpyHostToDevice, s));
+  HIPCHK(h, hipMemcpyAsync(d + o_ro, rule_offsets, ((size_t)n_rules + 1) * 4,
+                           hipMemcpyHostToDevice, s));
+  if (n_rules)
+    HIPCHK(h, hipMemcpyAsync(d + o_rf, rule_flags, (size_t)n_rules * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(h, launch_rules(d, (const uint32_t*)(d + o_no), n, d + o_rb, (const uint32_t*)(d + o_ro),
+                         (const uint32_t*)(d + o_rf), n_rules, rb, (uint32_t*)(d + o_out), s));
+  HIPCHK(h, hipMemcpyAsync(out, d + o_out, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(h, hipStreamSynchronize(s));
+  return 0;
 }
 
 int emqxgm_set_profiling(emqxgm_t* h, int on) {

@@ -116,6 +116,10 @@ struct FanScratch {
   uint32_t *cr = nullptr, *cd = nullptr, *rp = nullptr, *dp = nullptr;
   uint32_t *o_rf = nullptr, *o_rd = nullptr, *o_df = nullptr, *o_ds = nullptr;
 };
+// first rule (emqx_topic:match/2, or equality for RULE_EQ) matching each name, NONE if none
+hipError_t launch_rules(const uint8_t* nb, const uint32_t* no, uint32_t n, const uint8_t* rb,
+                        const uint32_t* ro, const uint32_t* rf, uint32_t nr, uint64_t rbytes,
+                        uint32_t* out, hipStream_t s);
 // One patch of a delta commit: w (1..64) dwords from src[s..] to the device address dst.
 struct PatchEnt {
   uint64_t dst;

@@ -38,12 +38,13 @@ __device__ __forceinline__ bool bytes_equal(PA a, PB b, uint32_t len) {
   return true;
 }
 
-// emqx_topic:match/2 (emqx_topic.erl:67-89) on raw bytes, for a NON-wildcard topic name T
-// (the trie never returns anything for wildcard names, emqx_trie.erl:157-166).  T and F are
-// byte accessors over LDS or global memory.
-template <class PT, class PF>
+// emqx_topic:match/2 (emqx_topic.erl:67-89) on raw bytes.  T and F are byte accessors over LDS
+// or global memory.  A '+'/'#' word of T is compared literally, as match/2 does for wildcard
+// names.  DOLLAR: the binary clauses (:70-73, a '$' name never matches a root wildcard); false
+// for match/2 called on word lists, which skips them (emqx_authz_rule.erl:213-214).
+template <bool DOLLAR = true, class PT, class PF>
 __device__ __forceinline__ bool mqtt_match(PT T, uint32_t tl, PF F, uint32_t fl) {
-  if (tl > 0 && T[0] == '$' && fl > 0 && (F[0] == '+' || F[0] == '#')) return false;  // :70-73
+  if (DOLLAR && tl > 0 && T[0] == '$' && fl > 0 && (F[0] == '+' || F[0] == '#')) return false;
   uint32_t i = 0, j = 0;  // start of the current topic / filter word
   for (;;) {
     uint32_t je = j;
@@ -173,6 +174,7 @@ __global__ __launch_bounds__(WG) void k_scan_final(const uint32_t* __restrict__ 
 #include "gm_walk.inc"
 #include "gm_verify.inc"
 #include "gm_fanout.inc"
+#include "gm_rules.inc"
 
 uint32_t grid_for(uint64_t items, uint32_t cap_blocks) {
   uint64_t b = (items + WG - 1) / WG;
@@ -382,6 +384,19 @@ hipError_t launch_patch(const PatchEnt* ents, uint32_t n, const uint32_t* src, h
   const uint64_t lanes = (uint64_t)n * 64;
   hipLaunchKernelGGL(k_patch, dim3((uint32_t)((lanes + WG - 1) / WG)), dim3(WG), 0, s, ents, n,
                      src);
+  return hipGetLastError();
+}
+
+hipError_t launch_rules(const uint8_t* nb, const uint32_t* no, uint32_t n, const uint8_t* rb,
+                        const uint32_t* ro, const uint32_t* rf, uint32_t nr, uint64_t rbytes,
+                        uint32_t* out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  RuleArgs a{nb, no, n, rb, ro, rf, nr, out};
+  const dim3 grid(grid_for(n, 8192));
+  if (rbytes <= RULE_LDS && nr <= RULE_LDS_N)
+    hipLaunchKernelGGL(k_rules<true>, grid, dim3(WG), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_rules<false>, grid, dim3(WG), 0, s, a);
   return hipGetLastError();
 }
 

@@ -90,6 +90,7 @@ SYMBOLS = {
     "emqxgm_subscriber_add": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint32]),
     "emqxgm_subscriber_delete": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint32]),
     "emqxgm_publish_batch": (C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(_PubOut)]),
+    "emqxgm_match_rules": (C.c_int, [_P, _P, _P, C.c_uint32, _P, _P, _P, C.c_uint32, _P]),
     "emqxgm_set_profiling": (C.c_int, [_P, C.c_int]),
     "emqxgm_tune": (C.c_int, [_P, C.c_char_p, C.c_int64]),
     "emqxgm_get_stats": (C.c_int, [_P, C.POINTER(_Stats)]),
@@ -136,6 +137,8 @@ def _ptr(a: np.ndarray):
 
 
 DEST_GROUP = 0x80000000
+RULE_EQ = 1     # include/emqx_gpumatch.h EMQXGM_RULE_EQ
+RULE_WORDS = 2  # EMQXGM_RULE_WORDS
 
 
 @dataclass
@@ -337,6 +340,19 @@ class Engine:
                                                  n, bytes_len, out), "walk_census")
         return {"states": out[0], "slot_loads": out[1], "pairs": out[2], "words": out[3],
                 "lane_iters": out[4], "wave_iters": out[5]}
+
+    def match_rules(self, names: Sequence[bytes], rules: Sequence[bytes],
+                    flags: Sequence[int]) -> np.ndarray:
+        """emqxgm_match_rules: index of the first rule matching each name (NONE if none)."""
+        nb, no = pack(list(names), np.uint32)
+        rb, ro = pack(list(rules), np.uint32)
+        fl = np.asarray(flags, dtype=np.uint32)
+        assert len(fl) == len(rules)
+        out = np.empty(len(names), np.uint32)
+        self._check(self._lib.emqxgm_match_rules(self._h, _ptr(nb), _ptr(no), len(names), _ptr(rb),
+                                                 _ptr(ro), _ptr(fl), len(rules), _ptr(out)),
+                    "match_rules")
+        return out
 
     def tune(self, key: str, value: int) -> None:
         self._check(self._lib.emqxgm_tune(self._h, key.encode(), int(value)), f"tune({key})")

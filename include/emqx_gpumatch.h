@@ -56,6 +56,8 @@ extern "C" {
 
 #define EMQXGM_NONE 0xFFFFFFFFu
 #define EMQXGM_DEST_GROUP 0x80000000u /* dest handle bit: a shared-subscription group */
+#define EMQXGM_RULE_EQ 1u    /* rule flag: {eq, Filter} -- the name must equal the filter */
+#define EMQXGM_RULE_WORDS 2u /* rule flag: match/2 on word lists (no '$' clauses) */
 #define EMQXGM_ABI_VERSION 1
 
 typedef struct emqxgm emqxgm_t;
@@ -180,6 +182,16 @@ typedef struct emqxgm_publish_out { /* host-resident result of emqxgm_publish_ba
  * the set the reference's route/2 folds over. */
 int emqxgm_publish_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets, uint32_t n,
                          emqxgm_publish_out* out);
+
+/* First rule matching each name, for the scalar emqx_topic:match/2 loops outside the router:
+ * emqx_authz_rule:match_topics/3 (apps/emqx_authz/src/emqx_authz_rule.erl:201-214: rules in
+ * order, {eq, F} by equality, others by match/2 on word lists -> EMQXGM_RULE_WORDS) and
+ * emqx_rewrite:match_and_rewrite/3 (apps/emqx_modules/src/emqx_rewrite.erl:145-150: match/2 on
+ * binaries, flags 0).  names / rules: packed bytes + [n+1] / [n_rules+1] offsets on the host;
+ * out[i] = index of the first matching rule, or EMQXGM_NONE.  Independent of the index. */
+int emqxgm_match_rules(emqxgm_t* h, const uint8_t* name_bytes, const uint32_t* name_offsets,
+                       uint32_t n, const uint8_t* rule_bytes, const uint32_t* rule_offsets,
+                       const uint32_t* rule_flags, uint32_t n_rules, uint32_t* out);
 
 /* Diagnostic pass (instrumented walk kernel, not the production launch): runs the device
  * match and returns out[0] = trie states matched (SURVEY 8d S(t) summed over the batch),
