@@ -463,3 +463,216 @@ def publish(router: "Router", topic: bytes, local_node: object,
         if dest == local_node:
             deliveries += [(to, s) for s in subscribers.get(to, [])]
     return entries, deliveries
+
+
+# ----------------------------------------------------------------------------------------
+# emqx_retainer_index / emqx_retainer_mnesia: the reverse match (a subscription filter ->
+# the stored retained topics it selects), an ETS match-spec search over word lists
+# ----------------------------------------------------------------------------------------
+
+ANY = "_"  # the match-spec wildcard '_' (a str, never equal to a binary word)
+
+
+class Improper:
+    """An improper list pattern ``[P1, ..., Pk | '_']`` (``L ++ '_'`` in the reference)."""
+
+    def __init__(self, items):
+        self.items = list(items)
+
+    def __eq__(self, other):
+        return isinstance(other, Improper) and self.items == other.items
+
+    def __repr__(self):
+        return f"Improper({self.items!r})"
+
+
+def _app_any(items: list):
+    """``L ++ '_'``: '_' itself for an empty L."""
+    return ANY if not items else Improper(items)
+
+
+def _concat(items: list, pat):
+    """``L ++ Pattern`` for a proper list L."""
+    if pat == ANY:
+        return _app_any(items)
+    if isinstance(pat, Improper):
+        return Improper(items + pat.items)
+    return items + list(pat)
+
+
+def retainer_condition(toks: Sequence[Word]):
+    """emqx_retainer_index.erl:97-112 condition/1: '+' -> '_', a last '#' -> an any tail."""
+    t1 = [ANY if w == PLUS else w for w in toks]
+    if not (len(t1) > 0 and t1[-1] == HASH):
+        return t1
+    rest = list(t1)
+    rest.remove(HASH)  # Tokens1 -- ['#'] drops the first '#'
+    return _app_any(rest)
+
+
+def retainer_condition_index(index: Sequence[int], toks: Sequence[Word]):
+    """emqx_retainer_index.erl:93-95, 174-200 condition/2: the index-key pattern."""
+    def go(ix, ts, n, im, om):
+        if ix and ts and ts[0] == HASH:  # :174-175
+            return (_app_any(im[::-1]), _app_any(om[::-1]))
+        if not ix and ts and ts[0] == HASH:  # :176-177
+            return (im[::-1], _app_any(om[::-1]))
+        if not ix:  # :178-179
+            return (im[::-1], _concat(om[::-1], retainer_condition(ts)))
+        if not ts:  # :180-181
+            return (_app_any(im[::-1]), om[::-1])
+        t = ts[0]
+        if t == PLUS:
+            if ix[0] == n:  # :182-185
+                return go(ix[1:], ts[1:], n + 1, [ANY] + im, om)
+            return go(ix, ts[1:], n + 1, im, [ANY] + om)  # :186-187
+        if ix[0] == n:  # :188-191
+            return go(ix[1:], ts[1:], n + 1, [t] + im, om)
+        return go(ix, ts[1:], n + 1, im, [t] + om)  # :192-195
+    return (tuple(index), go(list(index), list(toks), 1, [], []))
+
+
+def retainer_to_index_key(index: Sequence[int], toks: Sequence[Word]):
+    """emqx_retainer_index.erl:66-68, 130-139 to_index_key/2 + split_index_tokens/5."""
+    ix, ts, n, it, ot = list(index), list(toks), 1, [], []
+    while True:
+        if not ix:
+            return (tuple(index), (tuple(it), tuple(ot + ts)))
+        if not ts:
+            return (tuple(index), (tuple(it), tuple(ot)))
+        if ix[0] == n:
+            it.append(ts[0])
+            ix = ix[1:]
+        else:
+            ot.append(ts[0])
+        ts = ts[1:]
+        n += 1
+
+
+def retainer_index_score(index: Sequence[int], toks: Sequence[Word]) -> int:
+    """emqx_retainer_index.erl:79-81, 141-152 index_score/2."""
+    ix, ts, n, score = list(index), list(toks), 1, 0
+    while ix and ts:
+        if ix[0] == n and ts[0] in (PLUS, HASH):
+            return score
+        if ix[0] == n:
+            ix, score = ix[1:], score + 1
+        ts, n = ts[1:], n + 1
+    return score
+
+
+def retainer_select_index(toks: Sequence[Word], indices: Sequence[Sequence[int]]):
+    """emqx_retainer_index.erl:83-91, 154-165 select_index/2 (None = undefined)."""
+    best, sel = 0, None
+    for ix in indices:
+        s = retainer_index_score(ix, toks)
+        if s > best:
+            best, sel = s, list(ix)
+    return sel
+
+
+def retainer_restore_topic(key) -> List[Word]:
+    """emqx_retainer_index.erl:118-121, 202-209 restore_topic/1."""
+    index, (it, ot) = key
+    ix, it, ot, n, out = list(index), list(it), list(ot), 1, []
+    while it:
+        if ix and ix[0] == n:
+            out.append(it[0])
+            ix, it = ix[1:], it[1:]
+        else:
+            out.append(ot[0])
+            ot = ot[1:]
+        n += 1
+    return out + ot
+
+
+def ets_match(pat, term) -> bool:
+    """ETS match-spec head matching of the patterns above against stored keys."""
+    if pat == ANY:
+        return True
+    if isinstance(pat, Improper):
+        term = list(term) if isinstance(term, (list, tuple)) else None
+        return (term is not None and len(term) >= len(pat.items)
+                and all(ets_match(p, t) for p, t in zip(pat.items, term)))
+    if isinstance(pat, list):
+        term = list(term) if isinstance(term, (list, tuple)) else None
+        return term is not None and len(term) == len(pat) and all(
+            ets_match(p, t) for p, t in zip(pat, term))
+    if isinstance(pat, tuple):
+        return isinstance(term, tuple) and len(term) == len(pat) and all(
+            ets_match(p, t) for p, t in zip(pat, term))
+    return pat == term
+
+
+class Retainer:
+    """emqx_retainer_mnesia (apps/emqx_retainer/src/emqx_retainer_mnesia.erl) over dicts:
+    ?TAB_MESSAGE (word tuple -> expiry) and ?TAB_INDEX (index key -> expiry) for the configured
+    index specs (config_indices/0, sorted).  Messages are represented by their topics."""
+
+    def __init__(self, index_specs: Sequence[Sequence[int]] = ()):
+        self.msgs: Dict[tuple, int] = {}
+        self.index: Dict[tuple, int] = {}
+        self.indices = sorted(list(ix) for ix in index_specs)
+
+    def store_retained(self, topic: bytes, expiry: int = 0) -> None:
+        """:138-152, 262-292 (the table-full check is the caller's)."""
+        toks = tuple(words(topic))
+        self.msgs[toks] = expiry
+        for ix in self.indices:
+            self.index[retainer_to_index_key(ix, toks)] = expiry
+
+    def _delete(self, toks: tuple) -> None:
+        """:351-362 delete_message_with_indices/2."""
+        self.msgs.pop(toks, None)
+        for ix in self.indices:
+            self.index.pop(retainer_to_index_key(ix, toks), None)
+
+    def delete_message(self, topic: bytes) -> None:
+        """:166-180: an exact topic, or every message a wildcard selects (Now = 0)."""
+        if not wildcard(topic):
+            self._delete(tuple(words(topic)))
+        else:
+            for t in self.search_table(words(topic), 0):
+                self._delete(tuple(words(t)))
+
+    def read_message(self, topic: bytes, now: int) -> List[bytes]:
+        """:182-183, 372-382 (note ``Et >= Now`` here, ``>`` in the match specs)."""
+        et = self.msgs.get(tuple(words(topic)))
+        return [] if et is None or not (et == 0 or et >= now) else [topic]
+
+    def search_table(self, toks: Sequence[Word], now: int) -> List[bytes]:
+        """:300-330 search_table/2,3: the index path when an index scores > 0, else a scan of
+        the message table with condition/1; both keep expiry 0 or > Now."""
+        ix = retainer_select_index(toks, self.indices)
+        if ix is None:
+            ms = retainer_condition(toks)
+            return [join(t) for t, et in self.msgs.items()
+                    if ets_match(ms, list(t)) and (et == 0 or et > now)]
+        ms = retainer_condition_index(ix, toks)
+        out = []
+        for key, et in self.index.items():
+            if ets_match(ms, key) and (et == 0 or et > now):
+                t = tuple(retainer_restore_topic(key))
+                met = self.msgs.get(t)
+                if met is not None and (met == 0 or met > now):
+                    out.append(join(t))
+        return out
+
+    def match_messages(self, topic: bytes, now: int) -> List[bytes]:
+        """:185-195 (all remaining answers at once)."""
+        return self.search_table(words(topic), now)
+
+    def size(self) -> int:
+        return len(self.msgs)
+
+    def clean(self) -> None:
+        self.msgs.clear()
+        self.index.clear()
+
+
+def retained_match(filt: bytes, topics: Iterable[bytes]) -> List[bytes]:
+    """The set match_messages selects, as a predicate: the topics whose word lists the
+    condition/1 pattern of ``filt`` matches (``+`` any one word, a last ``#`` any tail, the
+    '$' clauses of emqx_topic:match/2 NOT applied)."""
+    ms = retainer_condition(words(filt))
+    return [t for t in topics if ets_match(ms, words(t))]

@@ -201,6 +201,80 @@ BENCH_PATTERNS = {"sub_ptn": "device/{{id}}/+/{{num}}/#",
                   "expect_routes_per_lookup": 1}
 
 
+# apps/emqx_retainer/test/emqx_retainer_index_SUITE.erl:32-210 -- emqx_retainer_index.
+# Words: strings are binaries, {"atom": x} the atoms '' '+' '#' and the match-spec '_';
+# {"improper": [...]} is the improper list [... | '_'].
+_A = {"atom": "_"}
+RETAINER_INDEX = {
+    # t_foreach_index_key 32-43, t_to_index_key 45-61: (index, topic words, key)
+    "to_index_key": [
+        ([1, 3], ["a", "b", "c"], [[1, 3], [["a", "c"], ["b"]]]),
+        ([1, 4], ["a", "b", "c"], [[1, 4], [["a"], ["b", "c"]]]),
+    ],
+    # t_index_score 63-110: (index, filter words, score)
+    "index_score": [
+        ([1, 4], [{"atom": "+"}, "a", "b", {"atom": "+"}], 0),
+        ([1, 2], [{"atom": "+"}, "a", "b", {"atom": "+"}], 0),
+        ([1, 2], ["a", "b", {"atom": "+"}], 2),
+        ([1, 2], ["a"], 1),
+        ([2, 3, 4, 5], [{"atom": "+"}, "a", {"atom": "#"}], 1),
+        ([2, 3, 4, 5], [{"atom": "+"}, "a", "b", {"atom": "+"}], 2),
+    ],
+    # t_select_index 112-132: (filter words, indices, selected or None)
+    "select_index": [
+        ([{"atom": "+"}, "a", "b", {"atom": "+"}], [[1, 4], [2, 3, 4, 5], [1, 2]], [2, 3, 4, 5]),
+        ([{"atom": "+"}, "a", "b", {"atom": "+"}], [[1, 4]], None),
+    ],
+    # t_condition 134-147: (filter words, pattern)
+    "condition": [
+        ([{"atom": "+"}, "a", "b", {"atom": "+"}], [_A, "a", "b", _A]),
+        ([{"atom": "+"}, "a", {"atom": "#"}], {"improper": [_A, "a"]}),
+    ],
+    # t_condition_index 149-207: (index, filter words, pattern {Index, {IndexPart, OtherPart}})
+    "condition_index": [
+        ([2, 3], [{"atom": "+"}, "a", "b", {"atom": "+"}], [[2, 3], [["a", "b"], [_A, _A]]]),
+        ([3, 4], [{"atom": "+"}, "a", "b", {"atom": "+"}], [[3, 4], [["b", _A], [_A, "a"]]]),
+        ([3, 5], [{"atom": "+"}, "a", "b", {"atom": "+"}],
+         [[3, 5], [{"improper": ["b"]}, [_A, "a", _A]]]),
+        ([3, 5], [{"atom": "+"}, "a", "b", {"atom": "#"}],
+         [[3, 5], [{"improper": ["b"]}, {"improper": [_A, "a"]}]]),
+        ([3, 4], [{"atom": "+"}, "a", "b", {"atom": "#"}],
+         [[3, 4], [{"improper": ["b"]}, {"improper": [_A, "a"]}]]),
+        ([1], ["a", {"atom": "#"}], [[1], [["a"], _A]]),
+        ([1, 2, 3], [{"atom": ""}, "saya", {"atom": "+"}],
+         [[1, 2, 3], [[{"atom": ""}, "saya", _A], []]]),
+    ],
+    # t_restore_topic 209-228: (key, topic words)
+    "restore_topic": [
+        ([[2, 3], [["a", "b"], ["x", "y"]]], ["x", "a", "b", "y"]),
+        ([[3, 4], [["b", "y"], ["x", "a"]]], ["x", "a", "b", "y"]),
+        ([[3, 5], [["b"], ["x", "a", "y"]]], ["x", "a", "b", "y"]),
+    ],
+}
+
+# apps/emqx_retainer/test/emqx_retainer_SUITE.erl: retained stores and what a subscriber gets.
+# Each case: steps of ["store", topic, expiry_ms] / ["delete", topic] / ["clean"] /
+# ["match", [filters], now_ms, expected message count over all filters].
+RETAINER_CASES = {
+    # t_store_and_clean 124-153 (an empty retained payload deletes: emqx_retainer.erl)
+    "store_and_clean": [["store", "retained", 0], ["match", ["retained"], 1, 1],
+                        ["delete", "retained"], ["match", ["retained"], 1, 0],
+                        ["store", "retained", 0], ["clean"], ["match", ["retained"], 1, 0]],
+    # t_wildcard_subscription 203-240
+    "wildcard_subscription": [
+        ["store", "retained/0", 0], ["store", "retained/1", 0], ["store", "retained/a/b/c", 0],
+        ["store", "/x/y/z", 0],
+        ["match", ["retained/+", "retained/+/b/#", "/+/y/#"], 1, 4]],
+    # t_message_expiry 242-296: expiry = publish time (0) + Message-Expiry-Interval * 1000
+    # (emqx_retainer.erl:130-141; interval 0 or absent with the default config: never)
+    "message_expiry": [
+        ["store", "retained/0", 0], ["store", "retained/1", 2000], ["store", "retained/2", 5000],
+        ["store", "retained/3", 0], ["store", "$SYS/retained/4", 0],
+        ["match", ["retained/+", "$SYS/retained/+"], 1, 5],
+        ["match", ["retained/+", "$SYS/retained/+"], 3000, 4]],
+}
+
+
 def main():
     out = {
         "source": "transcribed from fengyangdi/emqx @ 5.0.14 test suites (see make_golden.py)",
@@ -210,7 +284,8 @@ def main():
         "make_prefixes": MAKE_PREFIXES, "do_compact": DO_COMPACT,
         "router_cases": ROUTER_CASES, "client_topics": CLIENT_TOPICS,
         "client_wild": CLIENT_WILD, "client_dollar": CLIENT_DOLLAR,
-        "bench_patterns": BENCH_PATTERNS,
+        "bench_patterns": BENCH_PATTERNS, "retainer_index": RETAINER_INDEX,
+        "retainer_cases": RETAINER_CASES,
     }
     with open(os.path.join(HERE, "reference_vectors.json"), "w") as f:
         json.dump(out, f, indent=1)

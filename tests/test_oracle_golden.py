@@ -239,3 +239,96 @@ def test_publish_oracle_fanout():
     entries, deliv = R.publish(r, b"a/+", "n1", subs)
     assert sorted(entries, key=repr) == sorted([(b"a/+", "n1"), (b"a/+", "n2")], key=repr)
     assert R.publish(r, b"zz", "n1", subs) == ([], [])
+
+
+# ---------------------------------------------------------------- retainer
+
+def _pat(x):
+    """Decode a golden pattern: lists, {"atom": a}, {"improper": [...]}, binaries."""
+    if isinstance(x, dict) and "improper" in x:
+        return R.Improper([_pat(y) for y in x["improper"]])
+    if isinstance(x, dict) and "atom" in x:
+        return x["atom"]
+    if isinstance(x, list):
+        return [_pat(y) for y in x]
+    return B(x)
+
+
+def _key(x):
+    """Golden index key / condition/2 pattern [[Index], [IndexPart, OtherPart]] -> tuples."""
+    ix, (a, b) = x
+    conv = (lambda p: tuple(p) if isinstance(p, list) else p)
+    return (tuple(ix), (conv(_pat(a)), conv(_pat(b))))
+
+
+def test_retainer_index_vectors(golden):
+    g = golden["retainer_index"]
+    for ix, ws, key in g["to_index_key"]:
+        assert R.retainer_to_index_key(ix, [W(w) for w in ws]) == _key(key)
+    for ix, ws, score in g["index_score"]:
+        assert R.retainer_index_score(ix, [W(w) for w in ws]) == score, (ix, ws)
+    for ws, indices, sel in g["select_index"]:
+        assert R.retainer_select_index([W(w) for w in ws], indices) == sel
+    for ws, pat in g["condition"]:
+        assert R.retainer_condition([W(w) for w in ws]) == _pat(pat), ws
+    for ix, ws, pat in g["condition_index"]:
+        got = R.retainer_condition_index(ix, [W(w) for w in ws])
+        exp_ix, (a, b) = pat
+        assert got == (tuple(exp_ix), (_pat(a), _pat(b))), (ix, ws, got)
+    for key, ws in g["restore_topic"]:
+        assert R.retainer_restore_topic(_key(key)) == [W(w) for w in ws]
+
+
+@pytest.mark.parametrize("indices", [[], [[1, 2], [2, 3]], [[1], [3, 4], [1, 2, 3]]])
+def test_retainer_suite_cases(golden, indices):
+    for case, steps in golden["retainer_cases"].items():
+        r = R.Retainer(indices)
+        for st in steps:
+            if st[0] == "store":
+                r.store_retained(B(st[1]), st[2])
+            elif st[0] == "delete":
+                r.delete_message(B(st[1]))
+            elif st[0] == "clean":
+                r.clean()
+            else:
+                _, filters, now, n = st
+                got = sum(len(r.match_messages(B(f), now)) for f in filters)
+                assert got == n, (case, st, indices)
+
+
+def test_retainer_index_path_quirk():
+    """With index specs configured, 5.0.14's index path over-selects when a filter ends before
+    the index's last position (condition/2's `[_|_], []` clause leaves the index part open,
+    emqx_retainer_index.erl:180-181): with the default specs (emqx_retainer_schema.erl:24-29)
+    'a/+' also selects 'a/x/y'.  The scan path (index_specs = []) selects exactly condition/1's
+    set; the engine implements that set."""
+    default = [[1, 2, 3], [1, 3], [2, 3], [3]]
+    q, plain = R.Retainer(default), R.Retainer()
+    for t in (b"a/x", b"a/x/y", b"b/x"):
+        q.store_retained(t)
+        plain.store_retained(t)
+    assert sorted(q.match_messages(b"a/+", 1)) == [b"a/x", b"a/x/y"]
+    assert plain.match_messages(b"a/+", 1) == [b"a/x"]
+
+
+def test_retainer_index_path_covers_scan():
+    """search_table's index path never misses what the scan selects (it may over-select, see
+    the quirk above), and the scan equals the predicate form."""
+    rng = random.Random(4)
+    vocab = [b"a", b"b", b"", b"$s", b"cc"]
+    topics = {b"/".join(rng.choice(vocab) for _ in range(rng.randint(1, 5))) for _ in range(400)}
+    plain, indexed = R.Retainer(), R.Retainer([[1, 2], [2, 3], [1, 3, 4]])
+    for t in topics:
+        e = rng.choice([0, 0, 50, 150])
+        plain.store_retained(t, e)
+        indexed.store_retained(t, e)
+    for _ in range(300):
+        d = rng.randint(1, 5)
+        ws = [rng.choice([b"+", b"a", b"b", b"", b"$s"]) for _ in range(d)]
+        if rng.random() < 0.3:
+            ws[-1] = b"#"
+        f = b"/".join(ws)
+        a = sorted(plain.match_messages(f, 100))
+        assert set(a) <= set(indexed.match_messages(f, 100)), f
+        live = [t for t in topics if plain.msgs[tuple(R.words(t))] in (0, 150)]
+        assert a == sorted(R.retained_match(f, live)), f
