@@ -21,9 +21,8 @@ ENGINE_SO = os.path.join(ROOT, "emqx_amd", "libemqx_gpumatch.so")
 ORACLE_SO = os.path.join(ROOT, "oracle", "build", "libemqx_ref.so")
 WORKLOAD_SO = os.path.join(ROOT, "workloads", "libemqx_workload.so")
 
-ENGINE_SRCS = ["gm_kernels.hip", "gm_engine.cpp"]
-ENGINE_DEPS = ENGINE_SRCS + ["gm_common.h", "gm_kernels.h", "gm_tok.inc", "gm_walk.inc",
-                              "gm_verify.inc"]
+ENGINE_SRCS = ["gm_kernels.hip", "gm_engine.cpp", "gm_retain.cpp"]
+ENGINE_DEPS = sorted(set(ENGINE_SRCS) | {f for f in os.listdir(CSRC) if f.endswith((".h", ".inc"))})
 
 
 def _hipcc() -> str:

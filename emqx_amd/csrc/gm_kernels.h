@@ -120,6 +120,27 @@ struct FanScratch {
 hipError_t launch_rules(const uint8_t* nb, const uint32_t* no, uint32_t n, const uint8_t* rb,
                         const uint32_t* ro, const uint32_t* rf, uint32_t nr, uint64_t rbytes,
                         uint32_t* out, hipStream_t s);
+// Committed retained-topic store (gm_retain.inc / gm_retain.cpp), device pointers.
+struct RetainDev {
+  const uint4* rn = nullptr;      // per node {tb | RTERM, te, c0, c1}
+  const uint4* redge = nullptr;   // edge slots {tok.lo, tok.hi, parent, child}
+  uint64_t rmask = 0;
+  const uint32_t* rch = nullptr;  // children lists
+  const uint2* rw = nullptr;      // per node {pool offset, length} of its word
+  const uint8_t* pool = nullptr;  // topic bytes
+  const uint32_t* sid = nullptr;  // topic id per sorted position
+  const uint64_t* sexp = nullptr; // expiry per sorted position (nullptr: none expires)
+};
+// count (fill = false) or fill the runs of each filter; rbase = scanned counts
+hipError_t launch_retain_walk(const RetainDev& st, const uint8_t* fb, const uint32_t* fo, uint32_t n,
+                              uint4* frames, uint32_t max_plus, uint32_t* cnt,
+                              const uint32_t* rbase, uint2* runs, bool fill, hipStream_t s);
+// count (adds to *total) or write the live topic ids of each run
+hipError_t launch_retain_runs(const RetainDev& st, const uint2* runs, uint32_t nr, uint64_t now,
+                              uint32_t* acnt, const uint32_t* abase, uint32_t* out,
+                              unsigned long long* total, bool fill, hipStream_t s);
+hipError_t launch_retain_ptr(const uint32_t* rbase, const uint32_t* abase, uint32_t n,
+                             uint32_t* ptr, hipStream_t s);
 // One patch of a delta commit: w (1..64) dwords from src[s..] to the device address dst.
 struct PatchEnt {
   uint64_t dst;

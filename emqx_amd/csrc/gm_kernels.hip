@@ -175,6 +175,7 @@ __global__ __launch_bounds__(WG) void k_scan_final(const uint32_t* __restrict__ 
 #include "gm_verify.inc"
 #include "gm_fanout.inc"
 #include "gm_rules.inc"
+#include "gm_retain.inc"
 
 uint32_t grid_for(uint64_t items, uint32_t cap_blocks) {
   uint64_t b = (items + WG - 1) / WG;
@@ -397,6 +398,39 @@ hipError_t launch_rules(const uint8_t* nb, const uint32_t* no, uint32_t n, const
     hipLaunchKernelGGL(k_rules<true>, grid, dim3(WG), 0, s, a);
   else
     hipLaunchKernelGGL(k_rules<false>, grid, dim3(WG), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_retain_walk(const RetainDev& st, const uint8_t* fb, const uint32_t* fo, uint32_t n,
+                              uint4* frames, uint32_t max_plus, uint32_t* cnt,
+                              const uint32_t* rbase, uint2* runs, bool fill, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  RetainArgs a{fb, fo, n, st.rn, st.redge, st.rmask, st.rch, st.rw, st.pool, frames, max_plus,
+               cnt, rbase, runs};
+  const dim3 grid((n + WG - 1) / WG);
+  if (fill)
+    hipLaunchKernelGGL(k_retain_walk<true>, grid, dim3(WG), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_retain_walk<false>, grid, dim3(WG), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_retain_runs(const RetainDev& st, const uint2* runs, uint32_t nr, uint64_t now,
+                              uint32_t* acnt, const uint32_t* abase, uint32_t* out,
+                              unsigned long long* total, bool fill, hipStream_t s) {
+  if (nr == 0) return hipSuccess;
+  RunArgs a{runs, nr, st.sexp, now, st.sid, acnt, abase, out, total};
+  const dim3 grid(grid_for((uint64_t)nr * 64, 8192));
+  if (fill)
+    hipLaunchKernelGGL(k_retain_runs<true>, grid, dim3(WG), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_retain_runs<false>, grid, dim3(WG), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_retain_ptr(const uint32_t* rbase, const uint32_t* abase, uint32_t n,
+                             uint32_t* ptr, hipStream_t s) {
+  hipLaunchKernelGGL(k_retain_ptr, dim3(n / WG + 1), dim3(WG), 0, s, rbase, abase, n, ptr);
   return hipGetLastError();
 }
 

@@ -49,6 +49,11 @@ class _PubOut(C.Structure):
                 ("deliver_sub", C.POINTER(C.c_uint32))]
 
 
+class _RetOut(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("n_ids", C.c_uint64), ("ptr", C.POINTER(C.c_uint64)),
+                ("id", C.POINTER(C.c_uint32))]
+
+
 class _Stats(C.Structure):
     _fields_ = [("epoch", C.c_uint64), ("n_filters", C.c_uint64), ("n_trie_filters", C.c_uint64),
                 ("n_route_keys", C.c_uint64), ("n_nodes", C.c_uint64), ("n_edges", C.c_uint64),
@@ -91,6 +96,16 @@ SYMBOLS = {
     "emqxgm_subscriber_delete": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint32]),
     "emqxgm_publish_batch": (C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(_PubOut)]),
     "emqxgm_match_rules": (C.c_int, [_P, _P, _P, C.c_uint32, _P, _P, _P, C.c_uint32, _P]),
+    "emqxgm_retain_create": (C.c_int, [C.c_int32, C.POINTER(_P)]),
+    "emqxgm_retain_destroy": (None, [_P]),
+    "emqxgm_retain_store": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint64, _U32P]),
+    "emqxgm_retain_delete": (C.c_int, [_P, C.c_char_p, C.c_uint32]),
+    "emqxgm_retain_clean": (C.c_int, [_P]),
+    "emqxgm_retain_commit": (C.c_int, [_P]),
+    "emqxgm_retain_size": (C.c_int, [_P, _U64P]),
+    "emqxgm_retain_read": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint64, _U32P]),
+    "emqxgm_retain_topic": (C.c_int, [_P, C.c_uint32, C.POINTER(_U8P), _U32P]),
+    "emqxgm_retain_match": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, C.POINTER(_RetOut)]),
     "emqxgm_set_profiling": (C.c_int, [_P, C.c_int]),
     "emqxgm_tune": (C.c_int, [_P, C.c_char_p, C.c_int64]),
     "emqxgm_get_stats": (C.c_int, [_P, C.POINTER(_Stats)]),

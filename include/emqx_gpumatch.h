@@ -193,6 +193,40 @@ int emqxgm_match_rules(emqxgm_t* h, const uint8_t* name_bytes, const uint32_t* n
                        uint32_t n, const uint8_t* rule_bytes, const uint32_t* rule_offsets,
                        const uint32_t* rule_flags, uint32_t n_rules, uint32_t* out);
 
+/* ---- retained-message store: reverse match (filter -> stored topics) ----
+ * The retainer's mnesia backend (apps/emqx_retainer/src/emqx_retainer_mnesia.erl) on the
+ * device: topics of retained messages (the messages stay with the caller) with their expiry
+ * times, and match_messages/3 (:185-195) for batches of subscription filters.  The selected set
+ * is search_table/3's full-scan set (:300-330, condition/1 of emqx_retainer_index.erl:97-112:
+ * '+' any word, a last '#' any tail, no '$' rule, expiry 0 or > now).  Mutations are visible
+ * after emqxgm_retain_commit. */
+typedef struct emqxgm_retain emqxgm_retain_t;
+int emqxgm_retain_create(int32_t device, emqxgm_retain_t** out);
+void emqxgm_retain_destroy(emqxgm_retain_t* r);
+/* store_retained/2 (:138-152): insert or overwrite; expiry_ms 0 = never; *id = stable id */
+int emqxgm_retain_store(emqxgm_retain_t* r, const uint8_t* topic, uint32_t len,
+                        uint64_t expiry_ms, uint32_t* id);
+/* delete_message/2 of one topic (:166-170, delete_message_by_topic/2 :345-349); absent: no-op */
+int emqxgm_retain_delete(emqxgm_retain_t* r, const uint8_t* topic, uint32_t len);
+int emqxgm_retain_clean(emqxgm_retain_t* r); /* clean/1 (:241-244) */
+int emqxgm_retain_commit(emqxgm_retain_t* r);
+/* size/1 (:246-247): committed topics */
+int emqxgm_retain_size(emqxgm_retain_t* r, uint64_t* n);
+/* read_message/2 (:182-183, read_messages/1 :372-382: expiry 0 or >= now), committed state:
+ * 1 and *id if the topic is stored and live, 0 if not */
+int emqxgm_retain_read(emqxgm_retain_t* r, const uint8_t* topic, uint32_t len, uint64_t now_ms,
+                       uint32_t* id);
+int emqxgm_retain_topic(emqxgm_retain_t* r, uint32_t id, const uint8_t** p, uint32_t* len);
+typedef struct emqxgm_retain_out { /* host-resident, valid until the next call on r */
+  uint32_t n;
+  uint64_t n_ids;
+  const uint64_t* ptr; /* [n+1]: filter i selects id[ptr[i] .. ptr[i+1]) */
+  const uint32_t* id;  /* topic ids, ascending in topic word order within a filter */
+} emqxgm_retain_out;
+/* match_messages/3 for a batch of filters (packed bytes + [n+1] offsets on the host) */
+int emqxgm_retain_match(emqxgm_retain_t* r, const uint8_t* bytes, const uint32_t* offsets,
+                        uint32_t n, uint64_t now_ms, emqxgm_retain_out* out);
+
 /* Diagnostic pass (instrumented walk kernel, not the production launch): runs the device
  * match and returns out[0] = trie states matched (SURVEY 8d S(t) summed over the batch),
  * out[1] = edge slots loaded, out[2] = pairs, out[3] = levels (words) in the batch,
