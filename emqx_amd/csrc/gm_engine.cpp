@@ -309,7 +309,6 @@ struct emqxgm {
   uint64_t h_stage_bytes = 0;
   hipEvent_t patch_ev = nullptr;    // the last patch upload + launch
   uint32_t delta_mode = 1;        // 0: always rebuild, 1: delta when small, 2: delta if possible
-  uint32_t tok_wg_per_cu = 4;     // persistent tokenizer workgroups per CU
 };
 
 namespace {
@@ -1144,7 +1143,7 @@ int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_
     if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[0], st));
     HIPCHK(h, hipMemsetAsync(s.ctl, 0, CTL_N * 4, st));
     if (census) HIPCHK(h, hipMemsetAsync(s.census, 0, CENSUS_N * sizeof(unsigned long long), st));
-    HIPCHK(h, launch_tok(d_bytes, d_off, n, h->ix, s, h->geom.cus * h->tok_wg_per_cu, st));
+    HIPCHK(h, launch_tok(d_bytes, d_off, n, h->ix, s, st));
     if (h->ix.trie_empty) {
       HIPCHK(h, hipMemsetAsync(s.row, 0, (size_t)(n + 1) * 4, st));
     } else {
@@ -1826,11 +1825,6 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
     h->cfg.walk_wg_per_cu = (uint32_t)value;
     h->geom = walk_geometry(h->cfg.device, h->cfg.walk_wg_per_cu);
     return 0;  // spill scratch is re-sized by the next match (ensure_scratch)
-  }
-  if (strcmp(key, "tok_wg_per_cu") == 0) {
-    if (value < 1 || value > 32) return -EINVAL;
-    h->tok_wg_per_cu = (uint32_t)value;
-    return 0;
   }
   if (strcmp(key, "delta_commit") == 0) {
     if (value < 0 || value > 2) return -EINVAL;

@@ -107,9 +107,8 @@ hipError_t launch_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* 
 uint32_t scan_tmp_words(uint32_t n);
 // tokenise: levels (nw), 64-B topic records (rec: first REC_TOKS tokens inline), tokens of
 // deeper levels (wh, at off[t] + t + level), exact route-key ids (exact_id, NONE if absent)
-// blocks: persistent tokenizer workgroups (tiles of 256 topics are strided over them)
 hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
-                      Scratch& sc, uint32_t blocks, hipStream_t s);
+                      Scratch& sc, hipStream_t s);
 
 // Per-batch scratch of the publish fan-out (gm_fanout.inc).
 struct FanScratch {

@@ -218,7 +218,7 @@ hipError_t launch_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* 
 }
 
 hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
-                      Scratch& sc, uint32_t blocks, hipStream_t s) {
+                      Scratch& sc, hipStream_t s) {
   if (n == 0) return hipSuccess;
   TokArgs a;
   a.bytes = bytes;
@@ -236,7 +236,7 @@ hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, con
   a.test_mask = ix.test_mask;
   a.full_mask = ix.full_mask;
   a.exact_empty = ix.exact_empty;
-  hipLaunchKernelGGL(k_tok, dim3(grid_for(n, blocks)), dim3(WG), 0, s, a);
+  hipLaunchKernelGGL(k_tok, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a);
   return hipGetLastError();
 }
 

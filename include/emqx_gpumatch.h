@@ -237,7 +237,6 @@ int emqxgm_walk_census(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_of
 
 int emqxgm_set_profiling(emqxgm_t* h, int on);
 /* Runtime tuning knobs: "walk_wg_per_cu" (persistent walk workgroups per CU);
- * "tok_wg_per_cu" (persistent tokenizer workgroups per CU, default 4);
  * "delta_commit": 0 = every commit rebuilds the index, 1 = small deltas are patched in place
  * (default), 2 = every delta that fits the tables' load bounds is patched in place. */
 int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value);
