@@ -261,6 +261,11 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   a.spill = sc.spill;
   a.spill_items = sc.spill_items;
   a.lanes = g.lanes;
+  // a batch too small to give every wave TBLK topics is spread over all of them instead
+  // (a 100k-topic batch would otherwise keep 3 in 4 waves idle)
+  const uint32_t waves = g.lanes / 64;
+  const uint32_t per_wave = waves ? (n + waves - 1) / waves : TBLK;
+  a.tblk = per_wave >= TBLK ? TBLK : ((per_wave + 7) & ~7u) < 8 ? 8 : ((per_wave + 7) & ~7u);
   a.census = census;
   if (census && spill)
     hipLaunchKernelGGL((k_walk<true, true>), dim3(g.blocks), dim3(WG), 0, s, a);
