@@ -129,16 +129,19 @@ struct RetainDev {
   const uint2* rw = nullptr;      // per node {pool offset, length} of its word
   const uint8_t* pool = nullptr;  // topic bytes
   const uint32_t* sid = nullptr;  // topic id per sorted position
-  const uint64_t* sexp = nullptr; // expiry per sorted position (nullptr: none expires)
+  const uint64_t* sexp = nullptr; // expiry per sorted position (~0: deleted)
 };
-// count (fill = false) or fill the runs of each filter; rbase = scanned counts
+// count (fill = false: cnt = runs + cnt_in) or fill (at rbase + rshift) the runs of each
+// filter in one store; delta tags its runs
 hipError_t launch_retain_walk(const RetainDev& st, const uint8_t* fb, const uint32_t* fo, uint32_t n,
                               uint4* frames, uint32_t max_plus, uint32_t* cnt,
-                              const uint32_t* rbase, uint2* runs, bool fill, hipStream_t s);
-// count (adds to *total) or write the live topic ids of each run
-hipError_t launch_retain_runs(const RetainDev& st, const uint2* runs, uint32_t nr, uint64_t now,
-                              uint32_t* acnt, const uint32_t* abase, uint32_t* out,
-                              unsigned long long* total, bool fill, hipStream_t s);
+                              const uint32_t* cnt_in, const uint32_t* rbase,
+                              const uint32_t* rshift, bool delta, uint2* runs, bool fill,
+                              hipStream_t s);
+// count (adds to *total) or write the live topic ids of each run (base or delta store)
+hipError_t launch_retain_runs(const RetainDev& base, const RetainDev& delta, const uint2* runs,
+                              uint32_t nr, uint64_t now, uint32_t* acnt, const uint32_t* abase,
+                              uint32_t* out, unsigned long long* total, bool fill, hipStream_t s);
 hipError_t launch_retain_ptr(const uint32_t* rbase, const uint32_t* abase, uint32_t n,
                              uint32_t* ptr, hipStream_t s);
 // One patch of a delta commit: w (1..64) dwords from src[s..] to the device address dst.

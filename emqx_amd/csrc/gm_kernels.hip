@@ -408,10 +408,12 @@ hipError_t launch_rules(const uint8_t* nb, const uint32_t* no, uint32_t n, const
 
 hipError_t launch_retain_walk(const RetainDev& st, const uint8_t* fb, const uint32_t* fo, uint32_t n,
                               uint4* frames, uint32_t max_plus, uint32_t* cnt,
-                              const uint32_t* rbase, uint2* runs, bool fill, hipStream_t s) {
+                              const uint32_t* cnt_in, const uint32_t* rbase,
+                              const uint32_t* rshift, bool delta, uint2* runs, bool fill,
+                              hipStream_t s) {
   if (n == 0) return hipSuccess;
   RetainArgs a{fb, fo, n, st.rn, st.redge, st.rmask, st.rch, st.rw, st.pool, frames, max_plus,
-               cnt, rbase, runs};
+               cnt, cnt_in, rbase, rshift, delta ? RUN_DELTA : 0u, runs};
   const dim3 grid((n + WG - 1) / WG);
   if (fill)
     hipLaunchKernelGGL(k_retain_walk<true>, grid, dim3(WG), 0, s, a);
@@ -420,11 +422,11 @@ hipError_t launch_retain_walk(const RetainDev& st, const uint8_t* fb, const uint
   return hipGetLastError();
 }
 
-hipError_t launch_retain_runs(const RetainDev& st, const uint2* runs, uint32_t nr, uint64_t now,
-                              uint32_t* acnt, const uint32_t* abase, uint32_t* out,
-                              unsigned long long* total, bool fill, hipStream_t s) {
+hipError_t launch_retain_runs(const RetainDev& base, const RetainDev& delta, const uint2* runs,
+                              uint32_t nr, uint64_t now, uint32_t* acnt, const uint32_t* abase,
+                              uint32_t* out, unsigned long long* total, bool fill, hipStream_t s) {
   if (nr == 0) return hipSuccess;
-  RunArgs a{runs, nr, st.sexp, now, st.sid, acnt, abase, out, total};
+  RunArgs a{runs, nr, base.sexp, base.sid, delta.sexp, delta.sid, now, acnt, abase, out, total};
   const dim3 grid(grid_for((uint64_t)nr * 64, 8192));
   if (fill)
     hipLaunchKernelGGL(k_retain_runs<true>, grid, dim3(WG), 0, s, a);

@@ -14,6 +14,7 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/emqx_gpumatch.h"
@@ -40,6 +41,13 @@ constexpr uint32_t RTERM_BIT = 0x80000000u;  // gm_retain.inc RTERM
 
 }  // namespace
 
+// One preorder topic store on the device (gm_retain.inc): the base or the delta.
+struct Store {
+  RetainDev d;
+  std::vector<Buf> bufs;
+  std::vector<uint32_t> order;  // topic id per sorted position
+};
+
 struct emqxgm_retain {
   std::mutex mu;
   int32_t device = 0;
@@ -49,13 +57,18 @@ struct emqxgm_retain {
   std::vector<uint8_t> pool;
   std::vector<Topic> topics;
   std::unordered_map<std::string, uint32_t> ids;
+  std::vector<uint32_t> changed;  // ids stored or deleted since the last commit
   bool dirty = false;
-  // committed store
-  RetainDev d;
-  std::vector<Buf> bufs;
+  // committed state: base store + delta store of the topics stored since the base was built
+  Store base, delta;
+  bool built = false;
+  std::vector<uint32_t> pos_of;         // per id: sorted position in the base, or NONE
+  std::unordered_set<uint32_t> delta_ids;  // live ids not in the base
   std::vector<uint8_t> alive_committed;  // per id
   std::vector<uint64_t> exp_committed;   // per id
   uint64_t n_committed = 0;
+  int64_t delta_max = -1;  // delta topics before a full rebuild (-1: max(4096, base / 16))
+  uint64_t full_builds = 0, delta_builds = 0;
   // batch scratch and host outputs
   std::vector<Buf> sc;
   std::vector<uint64_t> h_ptr;
@@ -63,6 +76,11 @@ struct emqxgm_retain {
 };
 
 namespace {
+
+enum { S_FB, S_FO, S_FRAMES, S_CNT, S_RBASE, S_RUNS, S_ACNT, S_ABASE, S_OUT, S_PTR, S_TMP, S_CTL,
+       S_CNT2, S_PATCH };
+
+int grow(emqxgm_retain* r, size_t slot, uint64_t bytes);
 
 int rfail(emqxgm_retain* r, hipError_t e, const char* what) {
   r->err = std::string(what) + ": " + hipGetErrorString(e);
@@ -134,21 +152,26 @@ uint64_t word_tok(const uint8_t* p, uint32_t len) {
   return word_token(packed, fnv, len, 0);
 }
 
-// Build the device store from the registry (full rebuild) and swap it in.
-int commit_store(emqxgm_retain* r) {
-  std::vector<uint32_t> order;
-  for (uint32_t id = 0; id < r->topics.size(); ++id)
-    if (r->topics[id].alive) order.push_back(id);
+// Build a store over the topics `order` (any order in, sorted out) and swap it into st.  The
+// store keeps its own packed copy of its topics' bytes.
+int build_store(emqxgm_retain* r, std::vector<uint32_t> order, Store& st) {
   const uint8_t* P = r->pool.data();
   std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
     const Topic &a = r->topics[x], &b = r->topics[y];
     return word_less(P + a.off, a.len, P + b.off, b.len);
   });
   const uint32_t N = (uint32_t)order.size();
-  if (r->pool.size() >= 0xFFFFFFFFull) {
-    r->err = "retained topic pool exceeds 4 GiB";
+  std::vector<uint8_t> spool;  // this store's topic bytes, in sorted order
+  std::vector<uint64_t> soff(N + 1, 0);
+  for (uint32_t i = 0; i < N; ++i) soff[i + 1] = soff[i] + r->topics[order[i]].len;
+  if (soff[N] >= 0xFFFFFFFFull) {
+    r->err = "retained topic bytes exceed 4 GiB";
     return -E2BIG;
   }
+  spool.resize(soff[N]);
+  for (uint32_t i = 0; i < N; ++i)
+    if (r->topics[order[i]].len)
+      memcpy(spool.data() + soff[i], P + r->topics[order[i]].off, r->topics[order[i]].len);
   // ---- topic trie in preorder ----
   std::vector<uint32_t> tb(1, 0), te(1, N), parent(1, NONE), woff(1, 0), wlen(1, 0);
   std::vector<uint8_t> term(1, 0);
@@ -180,7 +203,7 @@ int commit_store(emqxgm_retain* r) {
       tb.push_back(i);
       te.push_back(N);
       parent.push_back(path.back());
-      woff.push_back((uint32_t)(t.off + ws[k]));
+      woff.push_back((uint32_t)(soff[i] + ws[k]));
       wlen.push_back(wl);
       term.push_back(0);
       tok.push_back(word_tok(p + ws[k], wl));
@@ -218,11 +241,7 @@ int commit_store(emqxgm_retain* r) {
     edge[i] = make_uint4((uint32_t)tok[v], (uint32_t)(tok[v] >> 32), parent[v], v);
   }
   std::vector<uint64_t> sexp(N);
-  bool any_exp = false;
-  for (uint32_t i = 0; i < N; ++i) {
-    sexp[i] = r->topics[order[i]].expiry;
-    any_exp = any_exp || sexp[i] != 0;
-  }
+  for (uint32_t i = 0; i < N; ++i) sexp[i] = r->topics[order[i]].expiry;
   // ---- upload and swap ----
   if (hipSetDevice(r->device) != hipSuccess) return rfail(r, hipErrorInvalidDevice, "hipSetDevice");
   RCHK(r, hipStreamSynchronize(r->stream));
@@ -231,23 +250,107 @@ int commit_store(emqxgm_retain* r) {
   int rc = 0;
   if ((rc = upload(r, nb, rn, &d.rn)) || (rc = upload(r, nb, edge, &d.redge)) ||
       (rc = upload(r, nb, rch, &d.rch)) || (rc = upload(r, nb, rw, &d.rw)) ||
-      (rc = upload(r, nb, r->pool, &d.pool)) || (rc = upload(r, nb, order, &d.sid)) ||
-      (any_exp && (rc = upload(r, nb, sexp, &d.sexp)))) {
+      (rc = upload(r, nb, spool, &d.pool)) || (rc = upload(r, nb, order, &d.sid)) ||
+      (rc = upload(r, nb, sexp, &d.sexp))) {
     free_all(nb);
     return rc;
   }
   d.rmask = cap - 1;
-  free_all(r->bufs);
-  r->bufs.swap(nb);
-  r->d = d;
+  free_all(st.bufs);
+  st.bufs.swap(nb);
+  st.d = d;
+  st.order.swap(order);
+  return 0;
+}
+
+void mark_committed(emqxgm_retain* r, uint32_t id) {
+  if (r->alive_committed.size() < r->topics.size()) {
+    r->alive_committed.resize(r->topics.size(), 0);
+    r->exp_committed.resize(r->topics.size(), 0);
+  }
+  r->alive_committed[id] = r->topics[id].alive;
+  r->exp_committed[id] = r->topics[id].expiry;
+}
+
+// Full commit: every live topic into a new base, the delta store emptied.
+int commit_full(emqxgm_retain* r) {
+  std::vector<uint32_t> all;
+  for (uint32_t id = 0; id < r->topics.size(); ++id)
+    if (r->topics[id].alive) all.push_back(id);
+  int rc = build_store(r, std::move(all), r->base);
+  if (rc) return rc;
+  if ((rc = build_store(r, {}, r->delta))) return rc;
+  r->pos_of.assign(r->topics.size(), NONE);
+  for (uint32_t i = 0; i < r->base.order.size(); ++i) r->pos_of[r->base.order[i]] = i;
+  r->delta_ids.clear();
   r->alive_committed.assign(r->topics.size(), 0);
   r->exp_committed.assign(r->topics.size(), 0);
-  for (uint32_t id : order) {
-    r->alive_committed[id] = 1;
-    r->exp_committed[id] = r->topics[id].expiry;
+  for (uint32_t id = 0; id < r->topics.size(); ++id) mark_committed(r, id);
+  r->n_committed = r->base.order.size();
+  r->built = true;
+  r->full_builds += 1;
+  return 0;
+}
+
+// Delta commit: base topics stored again or deleted patch their expiry word (RDEAD: deleted);
+// topics new since the base go to the delta store, rebuilt here.  Too many of them: full.
+int commit_store(emqxgm_retain* r) {
+  auto& ch = r->changed;
+  std::sort(ch.begin(), ch.end());
+  ch.erase(std::unique(ch.begin(), ch.end()), ch.end());
+  if (!r->built || r->delta_max == 0) {
+    ch.clear();
+    return commit_full(r);
   }
-  r->n_committed = N;
-  r->dirty = false;
+  r->pos_of.resize(r->topics.size(), NONE);
+  std::vector<PatchEnt> ents;
+  std::vector<uint32_t> src;
+  bool delta_changed = false;
+  for (uint32_t id : ch) {
+    const Topic& t = r->topics[id];
+    const uint32_t p = r->pos_of[id];
+    if (p != NONE) {
+      const uint64_t e = t.alive ? t.expiry : ~0ull;  // gm_retain.inc RDEAD
+      ents.push_back(PatchEnt{(uint64_t)(uintptr_t)(r->base.d.sexp + p), (uint32_t)src.size(), 2u});
+      src.push_back((uint32_t)e);
+      src.push_back((uint32_t)(e >> 32));
+    } else if (t.alive) {
+      delta_changed = true;  // (an expiry change of a delta topic too)
+      r->delta_ids.insert(id);
+    } else if (r->delta_ids.erase(id)) {
+      delta_changed = true;
+    }
+  }
+  const uint64_t lim = r->delta_max > 0
+                           ? (uint64_t)r->delta_max
+                           : std::max<uint64_t>(4096, r->base.order.size() / 16);
+  if (r->delta_ids.size() > lim) {
+    ch.clear();
+    return commit_full(r);
+  }
+  if (hipSetDevice(r->device) != hipSuccess) return rfail(r, hipErrorInvalidDevice, "hipSetDevice");
+  int rc = 0;
+  if (!ents.empty()) {
+    const uint64_t eb = ents.size() * sizeof(PatchEnt), total = eb + src.size() * 4;
+    if ((rc = grow(r, S_PATCH, total))) return rc;
+    uint8_t* d = (uint8_t*)r->sc[S_PATCH].p;
+    RCHK(r, hipMemcpyAsync(d, ents.data(), eb, hipMemcpyHostToDevice, r->stream));
+    RCHK(r, hipMemcpyAsync(d + eb, src.data(), src.size() * 4, hipMemcpyHostToDevice, r->stream));
+    RCHK(r, launch_patch((const PatchEnt*)d, (uint32_t)ents.size(), (const uint32_t*)(d + eb),
+                         r->stream));
+    RCHK(r, hipStreamSynchronize(r->stream));
+  }
+  if (delta_changed &&
+      (rc = build_store(r, std::vector<uint32_t>(r->delta_ids.begin(), r->delta_ids.end()),
+                        r->delta)))
+    return rc;
+  for (uint32_t id : ch) {
+    const bool was = id < r->alive_committed.size() && r->alive_committed[id];
+    mark_committed(r, id);
+    r->n_committed += (uint64_t)r->topics[id].alive - (uint64_t)was;
+  }
+  ch.clear();
+  r->delta_builds += 1;
   return 0;
 }
 
@@ -264,7 +367,7 @@ int grow(emqxgm_retain* r, size_t slot, uint64_t bytes) {
   return 0;
 }
 
-enum { S_FB, S_FO, S_FRAMES, S_CNT, S_RBASE, S_RUNS, S_ACNT, S_ABASE, S_OUT, S_PTR, S_TMP, S_CTL };
+
 
 }  // namespace
 
@@ -296,7 +399,8 @@ void emqxgm_retain_destroy(emqxgm_retain_t* r) {
   if (!r) return;
   (void)hipSetDevice(r->device);
   if (r->stream) (void)hipStreamSynchronize(r->stream);
-  free_all(r->bufs);
+  free_all(r->base.bufs);
+  free_all(r->delta.bufs);
   free_all(r->sc);
   if (r->stream) (void)hipStreamDestroy(r->stream);
   delete r;
@@ -320,6 +424,7 @@ int emqxgm_retain_store(emqxgm_retain_t* r, const uint8_t* topic, uint32_t len,
     r->topics[i].alive = true;
     r->topics[i].expiry = expiry_ms;
   }
+  r->changed.push_back(i);
   r->dirty = true;
   if (id) *id = i;
   return 0;
@@ -331,6 +436,7 @@ int emqxgm_retain_delete(emqxgm_retain_t* r, const uint8_t* topic, uint32_t len)
   auto it = r->ids.find(std::string((const char*)topic, len));
   if (it != r->ids.end() && r->topics[it->second].alive) {
     r->topics[it->second].alive = false;
+    r->changed.push_back(it->second);
     r->dirty = true;
   }
   return 0;
@@ -340,6 +446,7 @@ int emqxgm_retain_clean(emqxgm_retain_t* r) {
   if (!r) return -EINVAL;
   std::lock_guard<std::mutex> g(r->mu);
   for (Topic& t : r->topics) t.alive = false;
+  r->built = false;  // the next commit rebuilds (an empty base)
   r->dirty = true;
   return 0;
 }
@@ -348,6 +455,26 @@ int emqxgm_retain_commit(emqxgm_retain_t* r) {
   if (!r) return -EINVAL;
   std::lock_guard<std::mutex> g(r->mu);
   return r->dirty ? commit_store(r) : 0;
+}
+
+int emqxgm_retain_tune(emqxgm_retain_t* r, const char* key, int64_t value) {
+  if (!r || !key) return -EINVAL;
+  std::lock_guard<std::mutex> g(r->mu);
+  if (strcmp(key, "delta_max") == 0) {
+    r->delta_max = value;
+    return 0;
+  }
+  return -EINVAL;
+}
+
+int emqxgm_retain_stats(emqxgm_retain_t* r, uint64_t out[4]) {
+  if (!r || !out) return -EINVAL;
+  std::lock_guard<std::mutex> g(r->mu);
+  out[0] = r->full_builds;
+  out[1] = r->delta_builds;
+  out[2] = r->base.order.size();
+  out[3] = r->delta.order.size();
+  return 0;
 }
 
 int emqxgm_retain_size(emqxgm_retain_t* r, uint64_t* n) {
@@ -422,10 +549,20 @@ int emqxgm_retain_match(emqxgm_retain_t* r, const uint8_t* bytes, const uint32_t
   uint32_t* ctl = (uint32_t*)B(S_CTL);
   uint32_t* cnt = (uint32_t*)B(S_CNT);
   uint32_t* rbase = (uint32_t*)B(S_RBASE);
-  // runs per filter -> scan -> runs
-  RCHK(r, launch_retain_walk(r->d, fb, fo, n, (uint4*)B(S_FRAMES), max_plus, cnt, nullptr, nullptr,
-                             false, s));
-  RCHK(r, launch_scan(cnt, rbase, n, (uint32_t*)B(S_TMP), ctl, s));
+  // runs per filter (base, then base + delta) -> scan -> runs (base, then delta after them)
+  const bool has_delta = !r->delta.order.empty();
+  uint32_t* cnt2 = nullptr;
+  if (has_delta) {
+    if ((rc = grow(r, S_CNT2, (uint64_t)n * 4))) return rc;
+    cnt2 = (uint32_t*)B(S_CNT2);
+  }
+  uint4* frames = (uint4*)B(S_FRAMES);
+  RCHK(r, launch_retain_walk(r->base.d, fb, fo, n, frames, max_plus, cnt, nullptr, nullptr, nullptr,
+                             false, nullptr, false, s));
+  if (has_delta)
+    RCHK(r, launch_retain_walk(r->delta.d, fb, fo, n, frames, max_plus, cnt2, cnt, nullptr, nullptr,
+                               true, nullptr, false, s));
+  RCHK(r, launch_scan(has_delta ? cnt2 : cnt, rbase, n, (uint32_t*)B(S_TMP), ctl, s));
   uint32_t nr = 0;
   RCHK(r, hipMemcpyAsync(&nr, ctl, 4, hipMemcpyDeviceToHost, s));
   RCHK(r, hipStreamSynchronize(s));
@@ -436,12 +573,16 @@ int emqxgm_retain_match(emqxgm_retain_t* r, const uint8_t* bytes, const uint32_t
   uint2* runs = (uint2*)B(S_RUNS);
   uint32_t* acnt = (uint32_t*)B(S_ACNT);
   uint32_t* abase = (uint32_t*)B(S_ABASE);
-  RCHK(r, launch_retain_walk(r->d, fb, fo, n, (uint4*)B(S_FRAMES), max_plus, cnt, rbase, runs, true,
-                             s));
+  RCHK(r, launch_retain_walk(r->base.d, fb, fo, n, frames, max_plus, nullptr, nullptr, rbase,
+                             nullptr, false, runs, true, s));
+  if (has_delta)
+    RCHK(r, launch_retain_walk(r->delta.d, fb, fo, n, frames, max_plus, nullptr, nullptr, rbase, cnt,
+                               true, runs, true, s));
   // live ids per run -> scan -> ids
   unsigned long long* total = (unsigned long long*)(ctl + 4);
   RCHK(r, hipMemsetAsync(total, 0, 8, s));
-  RCHK(r, launch_retain_runs(r->d, runs, nr, now_ms, acnt, nullptr, nullptr, total, false, s));
+  RCHK(r, launch_retain_runs(r->base.d, r->delta.d, runs, nr, now_ms, acnt, nullptr, nullptr, total,
+                             false, s));
   unsigned long long nid = 0;
   RCHK(r, hipMemcpyAsync(&nid, total, 8, hipMemcpyDeviceToHost, s));
   RCHK(r, hipStreamSynchronize(s));
@@ -452,7 +593,8 @@ int emqxgm_retain_match(emqxgm_retain_t* r, const uint8_t* bytes, const uint32_t
   RCHK(r, launch_scan(acnt, abase, nr, (uint32_t*)B(S_TMP), nullptr, s));
   if ((rc = grow(r, S_OUT, nid * 4 + 4))) return rc;
   uint32_t* ids = (uint32_t*)B(S_OUT);
-  RCHK(r, launch_retain_runs(r->d, runs, nr, now_ms, acnt, abase, ids, total, true, s));
+  RCHK(r, launch_retain_runs(r->base.d, r->delta.d, runs, nr, now_ms, acnt, abase, ids, total,
+                             true, s));
   uint32_t* ptr = (uint32_t*)B(S_PTR);
   RCHK(r, launch_retain_ptr(rbase, abase, n, ptr, s));
   r->h_ptr32.resize((size_t)n + 1);

@@ -103,6 +103,8 @@ SYMBOLS = {
     "emqxgm_retain_clean": (C.c_int, [_P]),
     "emqxgm_retain_commit": (C.c_int, [_P]),
     "emqxgm_retain_size": (C.c_int, [_P, _U64P]),
+    "emqxgm_retain_tune": (C.c_int, [_P, C.c_char_p, C.c_int64]),
+    "emqxgm_retain_stats": (C.c_int, [_P, _U64P]),
     "emqxgm_retain_read": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint64, _U32P]),
     "emqxgm_retain_topic": (C.c_int, [_P, C.c_uint32, C.POINTER(_U8P), _U32P]),
     "emqxgm_retain_match": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, C.POINTER(_RetOut)]),

@@ -79,6 +79,15 @@ class Retainer:
             self._check(self._lib.emqxgm_retain_commit(self._h), "retain_commit")
             self._dirty = False
 
+    def tune(self, key: str, value: int) -> None:
+        self._check(self._lib.emqxgm_retain_tune(self._h, key.encode(), int(value)), "retain_tune")
+
+    def stats(self) -> dict:
+        a = (C.c_uint64 * 4)()
+        self._check(self._lib.emqxgm_retain_stats(self._h, a), "retain_stats")
+        return {"full_builds": a[0], "delta_commits": a[1], "base_topics": a[2],
+                "delta_topics": a[3]}
+
     def size(self) -> int:
         self.commit()
         n = C.c_uint64()

@@ -210,6 +210,12 @@ int emqxgm_retain_store(emqxgm_retain_t* r, const uint8_t* topic, uint32_t len,
 int emqxgm_retain_delete(emqxgm_retain_t* r, const uint8_t* topic, uint32_t len);
 int emqxgm_retain_clean(emqxgm_retain_t* r); /* clean/1 (:241-244) */
 int emqxgm_retain_commit(emqxgm_retain_t* r);
+/* Committed state = a base store plus a small delta store of the topics stored since the base
+ * was built; re-storing or deleting a base topic patches it in place.  "delta_max": delta topics
+ * before a commit rebuilds the base (-1 = max(4096, base / 16), 0 = rebuild at every commit). */
+int emqxgm_retain_tune(emqxgm_retain_t* r, const char* key, int64_t value);
+/* out = {full rebuilds, delta commits, base topics (incl. deleted), delta topics} */
+int emqxgm_retain_stats(emqxgm_retain_t* r, uint64_t out[4]);
 /* size/1 (:246-247): committed topics */
 int emqxgm_retain_size(emqxgm_retain_t* r, uint64_t* n);
 /* read_message/2 (:182-183, read_messages/1 :372-382: expiry 0 or >= now), committed state:
@@ -221,7 +227,8 @@ typedef struct emqxgm_retain_out { /* host-resident, valid until the next call o
   uint32_t n;
   uint64_t n_ids;
   const uint64_t* ptr; /* [n+1]: filter i selects id[ptr[i] .. ptr[i+1]) */
-  const uint32_t* id;  /* topic ids, ascending in topic word order within a filter */
+  const uint32_t* id;  /* topic ids: a filter's base-store topics, then its delta-store topics,
+                          each ascending in topic word order */
 } emqxgm_retain_out;
 /* match_messages/3 for a batch of filters (packed bytes + [n+1] offsets on the host) */
 int emqxgm_retain_match(emqxgm_retain_t* r, const uint8_t* bytes, const uint32_t* offsets,

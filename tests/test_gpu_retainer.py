@@ -73,11 +73,15 @@ def test_retainer_edges(emqx):
     assert r.read_message(b"a/b", 1) == [b"a/b"] and r.read_message(b"a/x", 1) == []
 
 
-@pytest.mark.parametrize("seed", [1, 2])
-def test_retainer_random_vs_oracle(emqx, seed):
+@pytest.mark.parametrize("seed,dmax", [(1, -1), (2, -1), (3, 0), (4, 10**9)])
+def test_retainer_random_vs_oracle(emqx, seed, dmax):
+    """dmax: delta topics before a base rebuild (0: rebuild at every commit; 10**9: the base
+    is only ever patched -- deletions and re-stores -- and new topics live in the delta)."""
     rng = random.Random(seed)
     vocab = [b"a", b"b", b"", b"$s", b"cc", b"long-word-%d" % seed, b"long-word-x"]
     ref, dev = R.Retainer(), emqx.Retainer()
+    dev.tune("delta_max", dmax)
+    big = dmax == 10**9
     for step in range(6):
         for _ in range(rng.randint(50, 400)):
             t = b"/".join(rng.choice(vocab) for _ in range(rng.randint(1, 6)))
@@ -88,6 +92,10 @@ def test_retainer_random_vs_oracle(emqx, seed):
             else:
                 ref.delete_message(t)
                 dev.delete_message(t)
+        if big and step == 2:  # fill the base once; every later change patches or goes to delta
+            dev.tune("delta_max", 0)
+            dev.commit()
+            dev.tune("delta_max", dmax)
         if step == 3:  # a wildcard delete (Now = 0: every selected message)
             ref.delete_message(b"a/+/#")
             dev.delete_message(b"a/+/#")
@@ -101,8 +109,14 @@ def test_retainer_random_vs_oracle(emqx, seed):
         got = dev.match_messages_batch(filters, 100)
         for f, g in zip(filters, got):
             exp = ref.match_messages(f, 100)
-            assert g == sorted(exp, key=_wkey), (step, f)
+            # base topics first, then the delta's, each in topic word order
+            assert sorted(g, key=_wkey) == sorted(exp, key=_wkey) and len(set(g)) == len(g), (step, f)
         assert dev.size() == ref.size()
+    st = dev.stats()
+    if dmax == 0:
+        assert st["delta_commits"] == 0, st
+    elif big:
+        assert st["full_builds"] == 2 and st["delta_commits"] >= 3 and st["base_topics"] > 0, st
     dev.close()
 
 

@@ -39,6 +39,24 @@ def main():
         ptr, ids = r.match_ids(filters, 1)
         best = min(best, time.perf_counter() - t3)
         n_ids = len(ids)
+    # delta commits: 10k new retained topics, then 10k deletions of base topics
+    extra = [b"x/" + w.topic(i) for i in range(10_000)]
+    t4 = time.perf_counter()
+    for t in extra:
+        r.store_retained(t)
+    t5 = time.perf_counter()
+    r.commit()
+    t6 = time.perf_counter()
+    for i in range(10_000):
+        r.delete_message(w.topic(i))
+    r.commit()
+    t7 = time.perf_counter()
+    ptr2, ids2 = r.match_ids(filters, 1)
+    st = r.stats()
+    print(json.dumps({
+        "delta_store_10k_commit_s": round(t6 - t5, 4), "delta_store_10k_registry_s": round(t5 - t4, 4),
+        "delete_10k_base_topics_incl_registry_s": round(t7 - t6, 4), "stats": st,
+        "ids_after_churn": int(len(ids2))}), flush=True)
     print(json.dumps({
         "retained_topics": r.size(), "filters": len(filters), "ids_selected": n_ids,
         "store_registry_s": round(t1 - t0, 3), "commit_build_s": round(t2 - t1, 3),
