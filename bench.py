@@ -163,6 +163,7 @@ def main():
     walk_bytes = (64 + 4) * w.nt + 48 * census["states"] + 16 * census["pairs"]
     achieved = walk_bytes / (walk_ms * 1e-3) / 1e9 if walk_ms > 0 else 0.0
     topics_total = (w.nt * world) if args.shard == "topics" else w.nt
+    compulsory = int(w.toff[-1]) + 4 * w.nt + 8 * census["pairs"]
     value = topics_total / (elapsed / args.steps)
 
     traffic = _pmc_traffic(args.cfg, w.nt)
@@ -206,6 +207,7 @@ def main():
                 "walk_lane_iterations_per_batch": int(census["lane_iters"]),
                 "walk_wave_iterations_per_batch": int(census["wave_iters"]),
                 "pipeline_ms_per_batch": round(pipe_ms, 4),
+                "pairs_per_s": round(census["pairs"] * (topics_total / w.nt) / (elapsed / args.steps), 1),
             },
             "roofline": {
                 "kernel": "k_walk",
@@ -214,6 +216,10 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
+                # SURVEY 8d's compulsory-only bytes (topic bytes + offset + an 8-B pair per match)
+                # over the whole step, against the same peak
+                "compulsory_bytes_per_batch": int(compulsory),
+                "compulsory_frac": round(compulsory / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "walk_ms_per_launch": round(walk_ms, 4),
                 "algorithmic_bytes_per_launch": int(walk_bytes),
