@@ -189,10 +189,21 @@ struct TrieModel {
   bool needs_verify = false;
   uint32_t max_depth = 0;
   uint64_t n_trie = 0, n_route = 0;
-  // exact route keys: entry per committed key, bitmaps over entries
+  // exact route keys: entry per committed key, bitmaps over entries.  Two regions of one
+  // table: plain (non-wildcard) keys in buckets [0, xcap_p), wildcard keys in [xcap_p,
+  // xcap_p + xcap_w); a name can only equal a key of its own kind (same bytes, same words).
   std::vector<uint32_t> xpos;
   std::vector<uint64_t> xocc, xtomb;
-  uint64_t xcap = 0, x_occ = 0;
+  uint64_t xcap_p = 0, xcap_w = 0, x_occ_p = 0, x_occ_w = 0, n_route_p = 0, n_route_w = 0;
+  uint64_t xbase(bool w) const { return w ? xcap_p : 0; }
+  uint64_t xcapr(bool w) const { return w ? xcap_w : xcap_p; }
+  uint64_t& xoccr(bool w) { return w ? x_occ_w : x_occ_p; }
+  uint64_t& nroute(bool w) { return w ? n_route_w : n_route_p; }
+  // home bucket of a key hash in its region, and the next bucket of its probe sequence
+  uint64_t xhome(bool w, uint64_t fh) const { return xbase(w) + exact_slot(fh, xcapr(w) - 1); }
+  uint64_t xnext(bool w, uint64_t b) const {
+    return xbase(w) + ((b - xbase(w) + 1) & (xcapr(w) - 1));
+  }
   // device tables patched in place (owned by emqxgm::ix_bufs)
   uint32_t *d_edges = nullptr, *d_exact = nullptr, *d_tn = nullptr, *d_fv = nullptr;
 
@@ -639,9 +650,9 @@ void commit_stats(emqxgm* h, double ms, bool delta) {
   h->st.n_nodes = m.n_edges + 1;
   h->st.n_edges = m.n_edges;
   h->st.edge_slots = m.ecap;
-  h->st.exact_slots = m.xcap * XBUCKET;
+  h->st.exact_slots = (m.xcap_p + m.xcap_w) * XBUCKET;
   h->st.max_depth = m.max_depth;
-  h->st.device_bytes = m.ecap * SLOT_U4 * 16 + m.xcap * XBUCKET * 16 + m.tn_cap * 4 +
+  h->st.device_bytes = m.ecap * SLOT_U4 * 16 + (m.xcap_p + m.xcap_w) * XBUCKET * 16 + m.tn_cap * 4 +
                        m.fv_cap * 4 + h->pool.size() + (h->filters.size() + 1) * 8 +
                        h->filters.size() * VREC;
   h->st.last_commit_ms = ms;
@@ -751,18 +762,24 @@ int commit_full(emqxgm* h) {
   m.fv_cap = m.fvbits.size() + std::max<uint64_t>(1024, m.fvbits.size() / 4);
   m.fvbits.resize(m.fv_cap, 0u);
 
-  // ---- exact route keys: buckets of XBUCKET entries, load factor <= 1/2, filled in order ----
-  for (const Filter& f : h->filters) m.n_route += f.route_refs > 0;
-  m.xcap = pow2_at_least(std::max<uint64_t>(16, (m.n_route * 2 + XBUCKET - 1) / XBUCKET));
-  m.xocc.assign(m.xcap * XBUCKET / 64 + 1, 0ull);
-  m.xtomb.assign(m.xcap * XBUCKET / 64 + 1, 0ull);
+  // ---- exact route keys: buckets of XBUCKET entries, load factor <= 1/2 per region, filled
+  // in order; plain keys and wildcard keys in separate regions ----
+  for (const Filter& f : h->filters)
+    if (f.route_refs) m.nroute(f.wild) += 1;
+  m.n_route = m.n_route_p + m.n_route_w;
+  m.xcap_p = pow2_at_least(std::max<uint64_t>(16, (m.n_route_p * 2 + XBUCKET - 1) / XBUCKET));
+  m.xcap_w = pow2_at_least(std::max<uint64_t>(16, (m.n_route_w * 2 + XBUCKET - 1) / XBUCKET));
+  const uint64_t xcap = m.xcap_p + m.xcap_w;
+  m.xocc.assign(xcap * XBUCKET / 64 + 1, 0ull);
+  m.xtomb.assign(xcap * XBUCKET / 64 + 1, 0ull);
   m.xpos.assign(nf, NONE);
-  std::vector<uint4> xslots(m.xcap * XBUCKET, make_uint4(0u, 0u, NONE, 0u));
+  std::vector<uint4> xslots(xcap * XBUCKET, make_uint4(0u, 0u, NONE, 0u));
   for (uint32_t id = 0; id < h->filters.size(); ++id) {
     const Filter& f = h->filters[id];
     if (!f.route_refs) continue;
     const uint64_t fh = key_hash(h->pool.data() + f.off, f.len, fmask);
-    uint64_t b = exact_slot(fh, m.xcap - 1);
+    const bool w = f.wild;
+    uint64_t b = m.xhome(w, fh);
     for (;;) {
       uint32_t j = 0;
       while (j < XBUCKET && xslots[b * XBUCKET + j].z != NONE) ++j;
@@ -773,10 +790,11 @@ int commit_full(emqxgm* h) {
         m.xpos[id] = (uint32_t)e;
         break;
       }
-      b = (b + 1) & (m.xcap - 1);
+      b = m.xnext(w, b);
     }
   }
-  m.x_occ = m.n_route;
+  m.x_occ_p = m.n_route_p;
+  m.x_occ_w = m.n_route_w;
 
   // ---- upload and swap ----
   if (hipSetDevice(h->cfg.device) != hipSuccess) return fail(h, hipErrorInvalidDevice, "hipSetDevice");
@@ -797,7 +815,9 @@ int commit_full(emqxgm* h) {
   m.d_tn = (uint32_t*)nx.tn_of;
   m.d_fv = (uint32_t*)nx.fvbits;
   nx.emask = m.nbk - 1;
-  nx.xmask = m.xcap - 1;
+  nx.xmask = m.xcap_p - 1;
+  nx.xwbase = m.xcap_p;
+  nx.xwmask = m.xcap_w - 1;
   const uint32_t root_p = m.pchild[0];
   nx.root_cf = m.cf(0);
   nx.root_hf = m.hfd(0);
@@ -808,7 +828,8 @@ int commit_full(emqxgm* h) {
   nx.full_mask = fmask;
   nx.max_depth = m.max_depth;
   nx.trie_empty = (m.n_trie == 0);
-  nx.exact_empty = (m.n_route == 0);
+  nx.plain_empty = (m.n_route_p == 0);
+  nx.wild_empty = (m.n_route_w == 0);
   free_bufs(h->ix_bufs);
   h->ix_bufs.swap(nbufs);
   for (Filter& f : h->filters) {
@@ -965,29 +986,32 @@ int commit_delta(emqxgm* h) {
     xpatch[e] = make_uint4(0u, 0u, TOMB, 0xFFFFFFFFu);
     m.xpos[id] = NONE;
     m.n_route -= 1;
+    m.nroute(h->filters[id].wild) -= 1;
   }
   for (uint32_t id : radd) {
-    if ((m.x_occ + 1) * 4 > m.xcap * XBUCKET * 3) return 1;
     const Filter& f = h->filters[id];
+    const bool w = f.wild;
+    if ((m.xoccr(w) + 1) * 4 > m.xcapr(w) * XBUCKET * 3) return 1;
     const uint64_t fh = key_hash(h->pool.data() + f.off, f.len, fmask);
-    uint64_t b = exact_slot(fh, m.xcap - 1), e = DEAD;
+    uint64_t b = m.xhome(w, fh), e = DEAD;
     while (e == DEAD) {
       for (uint32_t j = 0; j < XBUCKET && e == DEAD; ++j) {
         const uint64_t q = b * XBUCKET + j;
         if (!bit(m.xocc, q)) {
           bset(m.xocc, q);
-          m.x_occ += 1;
+          m.xoccr(w) += 1;
           e = q;
         } else if (bit(m.xtomb, q)) {
           bclr(m.xtomb, q);
           e = q;
         }
       }
-      b = (b + 1) & (m.xcap - 1);
+      b = m.xnext(w, b);
     }
     xpatch[e] = make_uint4((uint32_t)fh, (uint32_t)(fh >> 32), id, f.len);
     m.xpos[id] = (uint32_t)e;
     m.n_route += 1;
+    m.nroute(w) += 1;
   }
 
   // ---- patch lists: a dirty node rewrites its own slot, and its parent's slot when it is the
@@ -1027,7 +1051,8 @@ int commit_delta(emqxgm* h) {
   ix.needs_verify = m.needs_verify;
   ix.max_depth = m.max_depth;
   ix.trie_empty = (m.n_trie == 0);
-  ix.exact_empty = (m.n_route == 0);
+  ix.plain_empty = (m.n_route_p == 0);
+  ix.wild_empty = (m.n_route_w == 0);
   for (uint32_t id : ch) {
     Filter& f = h->filters[id];
     f.trie_committed = f.in_trie;

@@ -18,8 +18,12 @@ struct DevIndex {
   const uint32_t* rt_dst = nullptr;  // aggre entries (dest handles)
   const uint32_t* dl_sub = nullptr;  // local deliveries (subscriber ids)
   uint32_t fan_nf = 0;
-  const uint4* exact = nullptr;   // exact buckets of XBUCKET {hash.lo, hash.hi, fid, len}
-  uint64_t xmask = 0;             // bucket count - 1
+  // exact route-key buckets of XBUCKET {hash.lo, hash.hi, fid, len}: plain (non-wildcard) keys
+  // in buckets [0, xmask], wildcard keys in [xwbase, xwbase + xwmask]
+  const uint4* exact = nullptr;
+  uint64_t xmask = 0;             // plain region bucket count - 1
+  uint64_t xwbase = 0;            // first bucket of the wildcard-key region
+  uint64_t xwmask = 0;            // wildcard region bucket count - 1
   const uint8_t* fbytes = nullptr;  // filter string pool
   const uint64_t* foff = nullptr;   // [n_filters+1]
   const uint4* fver = nullptr;      // 64-B verification record per filter id
@@ -28,7 +32,8 @@ struct DevIndex {
   uint64_t full_mask = ~0ull;
   uint32_t max_depth = 0;           // deepest trie filter in levels
   bool trie_empty = true;
-  bool exact_empty = true;
+  bool plain_empty = true;         // no committed non-wildcard route key
+  bool wild_empty = true;          // no committed wildcard route key
   bool needs_verify = false;        // some trie filter has a hashed (long or test) token
 };
 

@@ -235,7 +235,10 @@ hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, con
   a.fver = ix.fver;
   a.test_mask = ix.test_mask;
   a.full_mask = ix.full_mask;
-  a.exact_empty = ix.exact_empty;
+  a.xwbase = ix.xwbase;
+  a.xwmask = ix.xwmask;
+  a.plain_empty = ix.plain_empty;
+  a.wild_empty = ix.wild_empty;
   hipLaunchKernelGGL(k_tok, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a);
   return hipGetLastError();
 }

@@ -80,7 +80,9 @@ def test_delta_churn_vs_oracle_and_full_build(emqx, bits):
                 py.delete(f)
                 live.discard(f)
             elif r < 0.92:
-                k = rng.choice(_topics(rng, 1))
+                # route keys of both kinds: plain names and wildcard filter strings (the two
+                # regions of the exact table)
+                k = rng.choice(_topics(rng, 1)) if rng.random() < 0.5 else _filter(rng)
                 if k not in keys:
                     for e in (delta, full):
                         e.route_ref(k)
@@ -94,6 +96,7 @@ def test_delta_churn_vs_oracle_and_full_build(emqx, bits):
         full.commit()
         topics = _topics(rng, 400) + sorted(keys)[:50] + [f.replace(b"+", b"q").replace(b"#", b"z")
                                                           for f in sorted(live)[:50]]
+        topics += sorted(live)[:30]  # wildcard names: exact key lookup only (emqx_router.erl:143)
         a = _check(delta, py, keys, topics)
         b = full.match(topics)
         assert np.array_equal(a.row_ptr, b.row_ptr)

@@ -194,6 +194,50 @@ def test_wildcard_topic_routes_exact_only(emqx):
                                                (b"a/b", "node")]
 
 
+@pytest.mark.parametrize("full_bits", [64, 2])
+@pytest.mark.parametrize("kinds", ["wild", "plain", "both"])
+def test_route_key_regions(emqx, kinds, full_bits):
+    """Route keys live in two regions of the exact table (plain names, wildcard strings): a
+    publish name only probes the region of its own kind.  Only-wildcard keys (the IoT-tree
+    case: no probe for plain names at all), only-plain keys, both; 2-bit key hashes force every
+    key of a region onto one probe chain; a 40 kB wildcard name takes the global-memory path."""
+    rng = random.Random(17)
+    wild = [f"s/{i}/+/#".encode() for i in range(300)] + [b"+", b"#", b"a/+/b", b"+/+"]
+    plain = [f"s/{i}/x/y".encode() for i in range(300)] + [b"", b"a", b"a//b", b"$SYS/x"]
+    longw = b"/".join([b"w" * 50] * 800) + b"/+"
+    keys = (wild + [longw] if kinds != "plain" else []) + (plain if kinds != "wild" else [])
+    eng = emqx.Engine(full_hash_bits=full_bits)
+    for k in keys:
+        eng.route_ref(k)
+    eng.commit()
+    names = wild + plain + [longw, longw[:-1] + b"#", b"s/1/+", b"s/1/x", b"s/1/x/y/z"]
+    names += [f"s/{rng.randrange(400)}/x/y".encode() for _ in range(200)]
+    rng.shuffle(names)
+    res = eng.match(names)
+    ks = set(keys)
+    for i, t in enumerate(names):
+        ex = int(res.exact_id[i])
+        if t in ks:
+            assert ex != emqx.NONE and eng.filter_bytes(ex) == t, t[:40]
+        else:
+            assert ex == emqx.NONE, t[:40]
+    # delta commits move keys in and out of both regions
+    eng.tune("delta_commit", 2)
+    gone = set(rng.sample(sorted(ks), len(ks) // 3))
+    for k in gone:
+        eng.route_unref(k)
+    new = [f"n/{i}/+".encode() for i in range(50)] + [f"n/{i}".encode() for i in range(50)]
+    for k in new:
+        eng.route_ref(k)
+    eng.commit()
+    ks = (ks - gone) | set(new)
+    res = eng.match(names + new)
+    for i, t in enumerate(names + new):
+        ex = int(res.exact_id[i])
+        assert (ex != emqx.NONE and eng.filter_bytes(ex) == t) if t in ks else ex == emqx.NONE
+    eng.close()
+
+
 def test_empty_batch_and_empty_index(emqx):
     eng = emqx.Engine()
     res = eng.match([])
