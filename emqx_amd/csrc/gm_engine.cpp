@@ -10,6 +10,8 @@
 #include <errno.h>
 #include <hip/hip_runtime.h>
 #include <stddef.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -305,6 +307,23 @@ struct emqxgm {
   bool walk_spill = false;         // committed index needs the spilling walk variant
   uint32_t reject_cap = 1u << 20;  // cfg.reject_cap overrides (tests force the legacy path)
   uint64_t test_mask = 0;          // != 0: collision-test tokens (cfg.word_hash_bits)
+
+  // ---- pipelined device passes (emqxgm_match_device_submit / _wait): each pipe has its own
+  // scratch, stream and events, so a batch can be enqueued while the previous one still runs
+  // (its walk's tail then overlaps the next batch's tokenizer and walk) ----
+  struct Pipe {
+    Scratch sc;
+    std::vector<DevBuf> bufs;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint64_t ticket = 0;  // last ticket submitted here (0: never)
+    int state = 0;        // 0 idle / result taken, 1 in flight, 2 result ready
+    const uint8_t* d_bytes = nullptr;
+    const uint32_t* d_off = nullptr;
+    uint32_t n = 0, pairs = 0;
+    uint64_t bytes_len = 0;
+  } pipes[EMQXGM_PIPES];
+  uint64_t next_ticket = 1;
 
   // ---- delta commits ----
   TrieModel tm;
@@ -1064,7 +1083,11 @@ int commit_delta(emqxgm* h) {
 }
 
 // Make the pending registry the committed index: a delta commit when it fits, else a full build.
+int drain_pipes(emqxgm* h);
+
 int commit_locked(emqxgm* h) {
+  // passes in flight read the committed index: let them finish before it changes
+  if (int rc = drain_pipes(h)) return rc;
   const auto t0 = std::chrono::steady_clock::now();
   h->patches.clear();
   int rc = patch_wait(h);  // the previous commit's patches are applied before buffers change
@@ -1123,7 +1146,8 @@ int ensure_scratch(emqxgm* h, uint32_t n, uint64_t words, uint32_t pairs) {
       (rc = dev_alloc(h, (void**)&s.out2, (size_t)pcap * 4)) ||
       (rc = dev_alloc(h, (void**)&s.scan_tmp, (size_t)stw * 4)) ||
       (rc = dev_alloc(h, (void**)&s.ctl, CTL_N * 4)) ||
-      (rc = dev_alloc(h, (void**)&s.census, CENSUS_N * sizeof(unsigned long long))) ||
+      (rc = dev_alloc(h, (void**)&s.census,
+                      (CENSUS_N + 3 * (h->geom.lanes / 64)) * sizeof(unsigned long long))) ||
       (rc = dev_alloc(h, (void**)&s.spill, (size_t)scap * h->geom.lanes * sizeof(uint2))) ||
       (rc = dev_alloc(h, (void**)&s.rlist, (size_t)h->reject_cap * 8)))
     return rc;
@@ -1145,8 +1169,14 @@ int ensure_scratch(emqxgm* h, uint32_t n, uint64_t words, uint32_t pairs) {
 // Production order: tokenise -> walk -> verify (flags rejects, fixes counts) -> scan -> scatter.
 // If a batch rejected more pairs than k_scatter adjusts in-line (a weak-hash test config or an
 // adversarial index), the pass is redone on the legacy path: scan -> verify+scatter -> compaction.
-int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_t n,
-               uint64_t bytes_len, uint32_t* pairs, uint64_t* census = nullptr) {
+//
+// The pass is three steps so that a pipelined caller (emqxgm_match_device_submit/_wait) can
+// enqueue one batch while an earlier one still runs on another stream: pass_prepare (scratch),
+// pass_enqueue (every launch, then the control words to the host, no synchronisation),
+// pass_check (after the stream has drained: 0 done, 1 redo, < 0 error) and pass_finish.
+
+// Scratch for n topics; returns 0, or 2 when n == 0 (then the empty result is already set).
+int pass_prepare(emqxgm* h, uint32_t n, uint64_t bytes_len) {
   const uint64_t words = bytes_len + n + 1;  // token array: level k of topic t at off[t] + t + k
   if (words > 0xFFFFFFFFull) {
     h->err = "batch too large: topic bytes + topics must stay below 2^32";
@@ -1155,82 +1185,95 @@ int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_
   uint32_t want_pairs = std::max<uint32_t>(h->sc.p_cap, std::max<uint32_t>(1u << 20, n * 4u));
   int rc = ensure_scratch(h, std::max<uint32_t>(n, 1), words, want_pairs);
   if (rc) return rc;
+  if (n == 0) {
+    HIPCHK(h, hipMemsetAsync(h->sc.row, 0, 4, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 2;
+  }
+  return 0;
+}
+
+int pass_enqueue(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_t n,
+                 bool legacy, bool census) {
   Scratch& s = h->sc;
   hipStream_t st = h->stream;
-  if (n == 0) {
-    HIPCHK(h, hipMemsetAsync(s.row, 0, 4, st));
-    HIPCHK(h, hipStreamSynchronize(st));
-    *pairs = 0;
-    return 0;
-  }
-  bool legacy = false;
-  for (int attempt = 0;; ++attempt) {
-    if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[0], st));
-    HIPCHK(h, hipMemsetAsync(s.ctl, 0, CTL_N * 4, st));
-    if (census) HIPCHK(h, hipMemsetAsync(s.census, 0, CENSUS_N * sizeof(unsigned long long), st));
-    HIPCHK(h, launch_tok(d_bytes, d_off, n, h->ix, s, st));
-    if (h->ix.trie_empty) {
-      HIPCHK(h, hipMemsetAsync(s.row, 0, (size_t)(n + 1) * 4, st));
+  if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[0], st));
+  HIPCHK(h, hipMemsetAsync(s.ctl, 0, CTL_N * 4, st));
+  if (census)
+    HIPCHK(h, hipMemsetAsync(s.census, 0,
+                             (CENSUS_N + 3 * (h->geom.lanes / 64)) * sizeof(unsigned long long),
+                             st));
+  HIPCHK(h, launch_tok(d_bytes, d_off, n, h->ix, s, st));
+  if (h->ix.trie_empty) {
+    HIPCHK(h, hipMemsetAsync(s.row, 0, (size_t)(n + 1) * 4, st));
+  } else {
+    // per-topic reject counts: only the verification passes write (and then read) them
+    if (h->ix.needs_verify || legacy) HIPCHK(h, hipMemsetAsync(s.rej, 0, (size_t)n * 4, st));
+    if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[1], st));
+    HIPCHK(h, launch_walk(h->ix, s, n, h->geom, st, census ? s.census : nullptr, h->walk_spill));
+    if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[2], st));
+    if (!legacy) {
+      // pairs of filters made of short (exact) tokens need no byte check (gm_verify.inc)
+      if (h->ix.needs_verify) HIPCHK(h, launch_verify(d_bytes, d_off, h->ix, s, n, h->geom, st));
+      HIPCHK(h, launch_scan(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, st));
+      HIPCHK(h, launch_scatter(s, n, h->geom, st));
     } else {
-      // per-topic reject counts: only the verification passes write (and then read) them
-      if (h->ix.needs_verify || legacy) HIPCHK(h, hipMemsetAsync(s.rej, 0, (size_t)n * 4, st));
-      if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[1], st));
-      HIPCHK(h, launch_walk(h->ix, s, n, h->geom, st, census ? s.census : nullptr,
-                            h->walk_spill));
-      if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[2], st));
-      if (!legacy) {
-        // pairs of filters made of short (exact) tokens need no byte check (gm_verify.inc)
-        if (h->ix.needs_verify) HIPCHK(h, launch_verify(d_bytes, d_off, h->ix, s, n, h->geom, st));
-        HIPCHK(h, launch_scan(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, st));
-        HIPCHK(h, launch_scatter(s, n, h->geom, st));
-      } else {
-        HIPCHK(h, launch_scan(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, st));
-        HIPCHK(h, launch_verify_scatter(d_bytes, d_off, h->ix, s, n, st));
-      }
+      HIPCHK(h, launch_scan(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, st));
+      HIPCHK(h, launch_verify_scatter(d_bytes, d_off, h->ix, s, n, st));
     }
-    if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[3], st));
-    HIPCHK(h, hipMemcpyAsync(s.ctl_host, s.ctl, CTL_N * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(h, hipStreamSynchronize(st));
-    if (attempt > 6) {
-      h->err = "match pass did not converge";
-      return -ENOMEM;
-    }
-    const uint32_t top = s.ctl_host[CTL_PAIR_TOP];
-    if (top > s.p_cap) {
-      // staging overflow: nothing beyond the capacity was written; grow and redo the pass
-      h->st.reruns += 1;
-      const uint64_t np = std::min<uint64_t>(0xF0000000ull, (uint64_t)top * 2 + (1u << 20));
-      rc = ensure_scratch(h, n, words, (uint32_t)np);
-      if (rc) return rc;
-      continue;
-    }
-    if (s.ctl_host[CTL_ERR] && !h->walk_spill) {
-      // a walk lane's item stack outgrew LDS: redo with the spilling variant (kept for this
-      // committed index)
-      h->st.reruns += 1;
-      h->walk_spill = true;
-      continue;
-    }
-    if (s.ctl_host[CTL_ERR]) {
-      // a walk lane's item stack outgrew the spill: grow it to the proven bound and redo
-      const uint32_t bound = walk_spill_bound(h->ix.max_depth);
-      if (s.spill_items >= bound) {
-        h->err = "walk item stack exceeded its bound";
-        return -EIO;
-      }
-      h->st.reruns += 1;
-      h->spill_want = bound;
-      rc = ensure_scratch(h, n, words, s.p_cap);
-      if (rc) return rc;
-      continue;
-    }
-    if (!legacy && s.ctl_host[CTL_LEGACY]) {
-      h->st.reruns += 1;
-      legacy = true;
-      continue;
-    }
-    break;
   }
+  if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[3], st));
+  HIPCHK(h, hipMemcpyAsync(s.ctl_host, s.ctl, CTL_N * 4, hipMemcpyDeviceToHost, st));
+  return 0;
+}
+
+// After the pass's stream drained: 0 = done, 1 = redo (scratch grown / walk variant or path
+// switched), < 0 = error.
+int pass_check(emqxgm* h, uint32_t n, uint64_t bytes_len, int attempt, bool& legacy) {
+  Scratch& s = h->sc;
+  const uint64_t words = bytes_len + n + 1;
+  if (attempt > 6) {
+    h->err = "match pass did not converge";
+    return -ENOMEM;
+  }
+  const uint32_t top = s.ctl_host[CTL_PAIR_TOP];
+  if (top > s.p_cap) {
+    // staging overflow: nothing beyond the capacity was written; grow and redo the pass
+    h->st.reruns += 1;
+    const uint64_t np = std::min<uint64_t>(0xF0000000ull, (uint64_t)top * 2 + (1u << 20));
+    int rc = ensure_scratch(h, n, words, (uint32_t)np);
+    return rc ? rc : 1;
+  }
+  if (s.ctl_host[CTL_ERR] && !h->walk_spill) {
+    // a walk lane's item stack outgrew LDS: redo with the spilling variant (kept for this
+    // committed index)
+    h->st.reruns += 1;
+    h->walk_spill = true;
+    return 1;
+  }
+  if (s.ctl_host[CTL_ERR]) {
+    // a walk lane's item stack outgrew the spill: grow it to the proven bound and redo
+    const uint32_t bound = walk_spill_bound(h->ix.max_depth);
+    if (s.spill_items >= bound) {
+      h->err = "walk item stack exceeded its bound";
+      return -EIO;
+    }
+    h->st.reruns += 1;
+    h->spill_want = bound;
+    int rc = ensure_scratch(h, n, words, s.p_cap);
+    return rc ? rc : 1;
+  }
+  if (!legacy && s.ctl_host[CTL_LEGACY]) {
+    h->st.reruns += 1;
+    legacy = true;
+    return 1;
+  }
+  return 0;
+}
+
+int pass_finish(emqxgm* h, uint32_t n, bool legacy, uint32_t* pairs, uint64_t* census) {
+  Scratch& s = h->sc;
+  hipStream_t st = h->stream;
   if (h->profiling) {
     float a = 0, b = 0;
     if (!h->ix.trie_empty) {
@@ -1252,6 +1295,14 @@ int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_
   if (legacy) h->st.legacy_batches += 1;
   *pairs = s.ctl_host[CTL_TOTAL];
   if (census) {
+    if (const char* wf = getenv("EMQXGM_WAVE_TIMES")) {  // diagnostic: per-wave timeline
+      std::vector<unsigned long long> wt(3 * (h->geom.lanes / 64));
+      HIPCHK(h, hipMemcpy(wt.data(), s.census + CENSUS_N, wt.size() * 8, hipMemcpyDeviceToHost));
+      if (FILE* fp = fopen(wf, "wb")) {
+        fwrite(wt.data(), 8, wt.size(), fp);
+        fclose(fp);
+      }
+    }
     unsigned long long c[CENSUS_N] = {0, 0, 0, 0};
     HIPCHK(h, hipMemcpy(c, s.census, sizeof c, hipMemcpyDeviceToHost));
     census[0] = c[0];
@@ -1269,6 +1320,25 @@ int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_
   h->st.topics += n;
   h->st.pairs += *pairs;
   return 0;
+}
+
+int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_t n,
+               uint64_t bytes_len, uint32_t* pairs, uint64_t* census = nullptr) {
+  int rc = pass_prepare(h, n, bytes_len);
+  if (rc == 2) {
+    *pairs = 0;
+    return 0;
+  }
+  if (rc) return rc;
+  bool legacy = false;
+  for (int attempt = 0;; ++attempt) {
+    if ((rc = pass_enqueue(h, d_bytes, d_off, n, legacy, census != nullptr))) return rc;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    rc = pass_check(h, n, bytes_len, attempt, legacy);
+    if (rc < 0) return rc;
+    if (rc == 0) break;
+  }
+  return pass_finish(h, n, legacy, pairs, census);
 }
 
 int fan_alloc(emqxgm* h, std::vector<DevBuf>& keep, uint32_t** p, size_t words) {
@@ -1391,6 +1461,16 @@ void emqxgm_destroy(emqxgm_t* h) {
   if (!h) return;
   (void)hipSetDevice(h->cfg.device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (auto& p : h->pipes) {
+    if (p.stream) {
+      (void)hipStreamSynchronize(p.stream);
+      (void)hipStreamDestroy(p.stream);
+    }
+    for (auto& e : p.ev)
+      if (e) (void)hipEventDestroy(e);
+    free_bufs(p.bufs);
+    if (p.sc.ctl_host) (void)hipHostFree(p.sc.ctl_host);
+  }
   free_bufs(h->ix_bufs);
   free_bufs(h->sc_bufs);
   free_bufs(h->fan_bufs);
@@ -1656,6 +1736,105 @@ int emqxgm_match_device(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_o
   return 0;
 }
 
+// ---- pipelined passes ----
+namespace {
+// Runs the single-pass code on a pipe: swaps the pipe's scratch, stream and events with the
+// handle's own for the lifetime of the object.
+struct OnPipe {
+  emqxgm* h;
+  emqxgm::Pipe& p;
+  OnPipe(emqxgm* h_, emqxgm::Pipe& p_) : h(h_), p(p_) { swap(); }
+  ~OnPipe() { swap(); }
+  void swap() {
+    std::swap(h->sc, p.sc);
+    std::swap(h->sc_bufs, p.bufs);
+    std::swap(h->stream, p.stream);
+    for (int i = 0; i < 4; ++i) std::swap(h->ev[i], p.ev[i]);
+  }
+};
+
+// Completes an in-flight pass (stream drained, checked, redone synchronously if it has to be).
+int pipe_complete(emqxgm* h, emqxgm::Pipe& p) {
+  if (p.state != 1) return 0;
+  OnPipe on(h, p);
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  bool legacy = false;
+  int rc = pass_check(h, p.n, p.bytes_len, 0, legacy);
+  if (rc < 0) {
+    p.state = 0;
+    return rc;
+  }
+  rc = rc == 0 ? pass_finish(h, p.n, false, &p.pairs, nullptr)
+               : run_device(h, p.d_bytes, p.d_off, p.n, p.bytes_len, &p.pairs);
+  p.state = rc ? 0 : 2;
+  return rc;
+}
+
+int drain_pipes(emqxgm* h) {
+  for (auto& p : h->pipes)
+    if (int rc = pipe_complete(h, p)) return rc;
+  return 0;
+}
+}  // namespace
+
+int emqxgm_match_device_submit(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_offsets,
+                               uint32_t n, uint64_t bytes_len, uint64_t* ticket) {
+  if (!h || !ticket || (!d_offsets && n)) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
+  const uint64_t tk = h->next_ticket;
+  emqxgm::Pipe& p = h->pipes[tk % EMQXGM_PIPES];
+  if (p.state == 1) {
+    h->err = "pipe busy: wait for the ticket submitted EMQXGM_PIPES submissions ago";
+    return -EBUSY;
+  }
+  if (!p.stream) {
+    HIPCHK(h, hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking));
+    for (auto& e : p.ev) HIPCHK(h, hipEventCreate(&e));
+  }
+  {
+    OnPipe on(h, p);
+    int rc = pass_prepare(h, n, bytes_len);
+    if (rc < 0) return rc;
+    p.d_bytes = d_bytes;
+    p.d_off = d_offsets;
+    p.n = n;
+    p.bytes_len = bytes_len;
+    p.pairs = 0;
+    if (rc == 2) {
+      p.state = 2;  // empty batch: already complete
+    } else {
+      if ((rc = pass_enqueue(h, d_bytes, d_offsets, n, false, false))) return rc;
+      p.state = 1;
+    }
+  }
+  p.ticket = tk;
+  h->next_ticket += 1;
+  *ticket = tk;
+  return 0;
+}
+
+int emqxgm_match_device_wait(emqxgm_t* h, uint64_t ticket, emqxgm_dev_out* out) {
+  if (!h || !out) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
+  emqxgm::Pipe& p = h->pipes[ticket % EMQXGM_PIPES];
+  if (ticket == 0 || p.ticket != ticket || p.state == 0) {
+    h->err = "unknown ticket, or its result was already taken / overwritten";
+    return -ENOENT;
+  }
+  int rc = pipe_complete(h, p);
+  if (rc) return rc;
+  p.state = 0;
+  out->n = p.n;
+  out->n_pairs = p.pairs;
+  out->row_ptr = p.sc.row;
+  out->filter_id = p.sc.out;
+  out->exact_id = p.sc.exact_id;
+  out->n_words = p.sc.nw;
+  return 0;
+}
+
 int emqxgm_match_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets, uint32_t n,
                        emqxgm_out* out) {
   if (!h || !out || (!offsets && n)) return -EINVAL;
@@ -1847,6 +2026,7 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
   std::lock_guard<std::mutex> g(h->mu);
   if (strcmp(key, "walk_wg_per_cu") == 0) {
     if (value < 1 || value > 16) return -EINVAL;
+    if (int rc = drain_pipes(h)) return rc;  // in-flight passes use the old geometry
     h->cfg.walk_wg_per_cu = (uint32_t)value;
     h->geom = walk_geometry(h->cfg.device, h->cfg.walk_wg_per_cu);
     return 0;  // spill scratch is re-sized by the next match (ensure_scratch)

@@ -88,6 +88,8 @@ SYMBOLS = {
     "emqxgm_filter_bytes": (C.c_int, [_P, C.c_uint32, C.POINTER(_U8P), _U32P]),
     "emqxgm_match_batch": (C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(_Out)]),
     "emqxgm_match_device": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, C.POINTER(_DevOut)]),
+    "emqxgm_match_device_submit": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, _U64P]),
+    "emqxgm_match_device_wait": (C.c_int, [_P, C.c_uint64, C.POINTER(_DevOut)]),
     "emqxgm_walk_census": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, _U64P]),
     "emqxgm_route_add": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32]),
     "emqxgm_route_delete": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32]),
@@ -346,6 +348,25 @@ class Engine:
         o = _DevOut()
         self._check(self._lib.emqxgm_match_device(self._h, C.c_void_p(d_bytes), C.c_void_p(d_off),
                                                   n, bytes_len, C.byref(o)), "match_device")
+        return DeviceResult(o.n, o.n_pairs, o.row_ptr or 0, o.filter_id or 0, o.exact_id or 0,
+                            o.n_words or 0)
+
+    PIPES = 2  # EMQXGM_PIPES
+
+    def match_device_submit(self, d_bytes: int, d_off: int, n: int, bytes_len: int) -> int:
+        """emqxgm_match_device_submit: enqueue a device pass, return its ticket (pipelined: up
+        to PIPES passes in flight; ticket k's result stays valid until ticket k + PIPES)."""
+        t = C.c_uint64(0)
+        self._check(self._lib.emqxgm_match_device_submit(
+            self._h, C.c_void_p(d_bytes), C.c_void_p(d_off), n, bytes_len, C.byref(t)),
+            "match_device_submit")
+        return int(t.value)
+
+    def match_device_wait(self, ticket: int) -> DeviceResult:
+        """emqxgm_match_device_wait: complete a submitted pass; its device-resident result."""
+        o = _DevOut()
+        self._check(self._lib.emqxgm_match_device_wait(self._h, ticket, C.byref(o)),
+                    "match_device_wait")
         return DeviceResult(o.n, o.n_pairs, o.row_ptr or 0, o.filter_id or 0, o.exact_id or 0,
                             o.n_words or 0)
 

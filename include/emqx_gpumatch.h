@@ -146,6 +146,22 @@ int emqxgm_match_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offset
 int emqxgm_match_device(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_offsets,
                         uint32_t n, uint64_t bytes_len, emqxgm_dev_out* out);
 
+/* Pipelined form of emqxgm_match_device for a stream of batches (the reference's publishers
+ * call match_routes concurrently, emqx_broker.erl:231; a batcher in front of the NIF hands the
+ * engine one batch after another).  _submit enqueues the whole pass for one batch and returns
+ * at once with a ticket; _wait(ticket) completes it (redoing it synchronously in the rare case
+ * of a staging overflow or deep walk) and returns the device-resident result.  Up to
+ * EMQXGM_PIPES passes are in flight per handle, each on its own HIP stream and scratch, so one
+ * batch's walk tail overlaps the next batch's tokenizer and walk.  Ticket k's result lives in
+ * pipe k % EMQXGM_PIPES and stays valid until ticket k + EMQXGM_PIPES is submitted; submitting
+ * it before ticket k was waited for returns -EBUSY.  The caller keeps d_bytes/d_offsets alive
+ * until the wait.  A commit first completes every pass in flight (results stay retrievable).
+ * Results are identical to emqxgm_match_device's. */
+#define EMQXGM_PIPES 2
+int emqxgm_match_device_submit(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_offsets,
+                               uint32_t n, uint64_t bytes_len, uint64_t* ticket);
+int emqxgm_match_device_wait(emqxgm_t* h, uint64_t ticket, emqxgm_dev_out* out);
+
 /* ---- publish fan-out (emqx_broker.erl:218-355) -------------------------------------------
  * Routes with dest identity: a plain route {Filter, Node} passes group = EMQXGM_NONE; a shared-
  * subscription route {Filter, {Group, Node}} passes both (handles < 2^31, chosen by the caller).

@@ -496,3 +496,76 @@ def test_device_api_matches_host_api(emqx):
     assert hip.hipMemcpy(fid.ctypes.data, d.filter_id, fid.nbytes, 2) == 0
     assert np.array_equal(row.astype(np.uint64), host.row_ptr)
     assert np.array_equal(fid, host.filter_id)
+
+
+def _dev_to_host(d, n):
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    row = np.empty(n + 1, np.uint32)
+    fid = np.empty(d.n_pairs, np.uint32)
+    ex = np.empty(n, np.uint32)
+    for a, p in ((row, d.row_ptr), (fid, d.filter_id), (ex, d.exact_id)):
+        if a.nbytes:
+            assert hip.hipMemcpy(a.ctypes.data, p, a.nbytes, 2) == 0
+    return row, fid, ex
+
+
+def test_pipelined_passes(emqx):
+    """emqxgm_match_device_submit/_wait: several batches in flight on two pipes give exactly the
+    synchronous results; a staging overflow inside a pipe is redone; empty batches; -EBUSY for a
+    third submission before the first wait; a commit completes the passes in flight against the
+    index they were submitted on."""
+    import torch
+    import workloads
+    w = workloads.generate(1, 5000, 30000)
+    eng, _ = _load_both(emqx, w)
+    # batches: three slices of the workload, an empty one, and one with > 1M pairs (overflows
+    # the default staging capacity of max(1M, 4n) pairs inside its pipe)
+    import itertools
+    words = "abcdefghij"
+    many = set()
+    for k in range(11):  # every filter matching a/b/.../j: literal or '+' per level, '#' tails
+        for pat in itertools.product((0, 1), repeat=k):
+            lv = ["+" if x else words[i] for i, x in enumerate(pat)]
+            many.add("/".join(lv + ["#"]) if k < 10 else "/".join(lv))
+    for f in sorted(many):
+        eng.trie_insert(f.encode())
+    eng.commit()
+    heavy = ["/".join(words).encode()] * 1000  # ~2M pairs: overflows a fresh pipe's staging
+    hb, ho = emqx.engine.pack(heavy)
+    batches = [(w.tbytes[:int(w.toff[k])], w.toff[:k + 1]) for k in (10000, 20000, 30000)]
+    batches = [(b[int(o[0]):], o - o[0]) for b, o in batches]
+    batches += [(np.zeros(1, np.uint8), np.zeros(1, np.uint32)), (hb, ho)] + batches
+    dev = [(torch.from_numpy(b).cuda(), torch.from_numpy(o.astype(np.uint32).view(np.int32)).cuda())
+           for b, o in batches]
+    torch.cuda.synchronize()
+    want = []
+    for (b, o), (db, do) in zip(batches, dev):
+        n = len(o) - 1
+        want.append(_dev_to_host(eng.match_device(db.data_ptr(), do.data_ptr(), n, int(o[-1])), n))
+    tickets = []
+    got = []
+    for i, ((b, o), (db, do)) in enumerate(zip(batches, dev)):
+        tickets.append(eng.match_device_submit(db.data_ptr(), do.data_ptr(), len(o) - 1, int(o[-1])))
+        if i >= 1:
+            j = i - 1
+            got.append(_dev_to_host(eng.match_device_wait(tickets[j]), len(batches[j][1]) - 1))
+    with pytest.raises(emqx.EngineError):
+        eng.match_device_wait(tickets[0])  # result already taken
+    db, do = dev[0]
+    n0 = len(batches[0][1]) - 1
+    t_a = eng.match_device_submit(db.data_ptr(), do.data_ptr(), n0, int(batches[0][1][-1]))
+    with pytest.raises(emqx.EngineError):  # pipe of the last ticket still holds its pass
+        eng.match_device_submit(db.data_ptr(), do.data_ptr(), n0, int(batches[0][1][-1]))
+    got.append(_dev_to_host(eng.match_device_wait(tickets[-1]), len(batches[-1][1]) - 1))
+    for i, (a, b) in enumerate(zip(want, got)):
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y), i
+    # a commit completes the pass in flight; its result reflects the index it was submitted on
+    eng.trie_insert(b"#")
+    eng.commit()
+    row, fid, ex = _dev_to_host(eng.match_device_wait(t_a), n0)
+    assert all(np.array_equal(x, y) for x, y in zip((row, fid, ex), want[0]))
+    assert eng.stats()["reruns"] >= 1
+    eng.close()
