@@ -116,7 +116,15 @@ def main():
     torch.cuda.synchronize()
 
     # ---- one diagnostic census pass (outside the timed region): S(t), slot loads, pairs ----
+    # S(t) as SURVEY 8d defines it (every matched prefix state) comes from a census of the
+    # unpruned walk; the production walk skips leaf-only children a deeper topic cannot match
+    # (CF_LEAFP), so its own loads and iterations come from a second census
+    eng.tune("leaf_prune", 0)
+    census_full = eng.walk_census(tb.data_ptr(), to.data_ptr(), w.nt, nbytes)
+    eng.tune("leaf_prune", 1)
     census = eng.walk_census(tb.data_ptr(), to.data_ptr(), w.nt, nbytes)
+    census["states_visited"] = census["states"]
+    census["states"] = census_full["states"]
 
     # pipelined steps (default): each step submits its batch and completes the previous one, so
     # two passes are in flight on the engine's two pipes (emqxgm_match_device_submit/_wait) and
@@ -236,6 +244,8 @@ def main():
                     (f"topic-replica x{world}" if args.shard == "topics" else f"filter-shard x{world}"),
                 "pairs_per_batch": int(census["pairs"]),
                 "trie_states_per_batch": int(census["states"]),
+                "walk_states_visited_per_batch": int(census["states_visited"]),
+                "edge_slot_loads_unpruned_per_batch": int(census_full["slot_loads"]),
                 "edge_slot_loads_per_batch": int(census["slot_loads"]),
                 "walk_lane_iterations_per_batch": int(census["lane_iters"]),
                 "walk_wave_iterations_per_batch": int(census["wave_iters"]),

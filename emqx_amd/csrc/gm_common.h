@@ -79,7 +79,7 @@ GM_HD uint64_t key_hash(const uint8_t* p, uint32_t len, uint64_t mask) {
 // 32 B per slot, 2 x uint4, one slot per trie edge (parent --level token--> child C):
 //   s0 = {tok.lo, tok.hi, parent, cf}       key = (parent node id, level token), exact
 //   s1 = {hf, tw, p.cf, p.hf}
-//   cf  = C's node id (27 bits) | C's flags (5 bits)
+//   cf  = C's node id (26 bits) | C's flags (6 bits)
 //   hf  = filter id of "C_path/#", NONE, or (CF_HFM) index into the multi[] list pool
 //   tw  = wildcard filter(s) ending exactly at C (fid, or LIST_MULTI|multi index)
 //   p   = C's '+' child {cf, hf} (cf = 0 if there is none; node 0 is the root, never a child),
@@ -95,9 +95,13 @@ GM_HD uint64_t key_hash(const uint8_t* p, uint32_t len, uint64_t mask) {
 constexpr uint32_t SLOT_U4 = 2;
 constexpr uint32_t EBUCKET = 2;
 constexpr uint32_t EDGE_SLACK = 4;  // slots >= 4 x edges (load <= 1/4): fewer bucket overflows
-constexpr uint32_t CF_ID_BITS = 27;
+constexpr uint32_t CF_ID_BITS = 26;
 constexpr uint32_t CF_ID_MASK = (1u << CF_ID_BITS) - 1;
 constexpr uint32_t MAX_NODES = CF_ID_MASK;
+// child's children (literal and '+') are all leaves: no children and no '#' filter of their own,
+// so they matter only to a topic whose last word they consume -- a deeper topic skips them
+// (never set wrongly: a delta commit only ever clears it)
+constexpr uint32_t CF_LEAFP = 1u << 26;
 constexpr uint32_t CF_LIT = 1u << 27;   // child has literal (non-'+') children
 constexpr uint32_t CF_PLUS = 1u << 28;  // child has a '+' child
 constexpr uint32_t CF_HFM = 1u << 29;   // hf is a multi[] index

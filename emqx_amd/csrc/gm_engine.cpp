@@ -183,6 +183,7 @@ struct TrieModel {
   EdgeMap emap;
   // per node (root = 0): hf/tw/tn are NONE, a filter id, or LIST_MULTI | multi[] position
   std::vector<uint32_t> parent, ref, nlit, pchild, hf, tw, tn;
+  std::vector<uint8_t> leafp;  // CF_LEAFP: exact at a full build, only cleared by deltas
   std::vector<uint64_t> tok;
   std::vector<uint64_t> slot;       // edge slot of the node's incoming edge (DEAD: root/removed)
   std::vector<uint64_t> occ, tomb;  // bitmaps over edge slots: used (live or TOMB), TOMB
@@ -216,6 +217,7 @@ struct TrieModel {
     if (hf[i] != NONE && (hf[i] & LIST_MULTI)) f |= CF_HFM;
     if (tw[i] != NONE) f |= CF_TW;
     if (tn[i] != NONE) f |= CF_TN;
+    if (leafp[i]) f |= CF_LEAFP;
     return f;
   }
   uint32_t hfd(uint32_t i) const { return hf[i] == NONE ? NONE : (hf[i] & ~LIST_MULTI); }
@@ -234,8 +236,18 @@ struct TrieModel {
     hf.push_back(NONE);
     tw.push_back(NONE);
     tn.push_back(NONE);
+    leafp.push_back(0);
     slot.push_back(DEAD);
     return c;
+  }
+  // node y gained a child or a '#' filter: its parent's children are no longer all leaves
+  void unleaf(uint32_t y, std::vector<uint32_t>& dirty) {
+    if (y == 0) return;
+    const uint32_t p = parent[y];
+    if (leafp[p]) {
+      leafp[p] = 0;
+      dirty.push_back(p);
+    }
   }
 };
 
@@ -715,7 +727,7 @@ int commit_full(emqxgm* h) {
       uint32_t* v = m.emap.get_or_insert(cur, tok, ins);
       if (ins) {
         if (m.parent.size() >= MAX_NODES) {
-          h->err = "trie exceeds 2^27-1 nodes";
+          h->err = "trie exceeds 2^26-1 nodes";
           return -E2BIG;
         }
         const uint32_t child = m.new_node(cur, tok);
@@ -730,6 +742,15 @@ int commit_full(emqxgm* h) {
     }
     m.max_depth = std::max<uint32_t>(m.max_depth, (uint32_t)path_len);
     lb.add(hash_last ? m.hf[cur] : f.wild ? m.tw[cur] : m.tn[cur], id);
+  }
+  // CF_LEAFP: a node whose children are all leaves (no children, no '#' filter)
+  {
+    const size_t nn = m.parent.size();
+    m.leafp.assign(nn, 1);
+    for (size_t y = 1; y < nn; ++y)
+      if (m.nlit[y] || m.pchild[y] || m.hf[y] != NONE) m.leafp[m.parent[y]] = 0;
+    for (size_t x = 0; x < nn; ++x)
+      if (!m.nlit[x] && !m.pchild[x]) m.leafp[x] = 0;
   }
   // flatten multi lists
   std::vector<uint32_t> multi(1, 0);
@@ -982,6 +1003,7 @@ int commit_delta(emqxgm* h) {
           m.pchild[cur] = c;
         else
           m.nlit[cur] += 1;
+        m.unleaf(cur, dirty);
         dirty.push_back(cur);
         dirty.push_back(c);
       }
@@ -992,6 +1014,7 @@ int commit_delta(emqxgm* h) {
     uint32_t& fld = hash_last ? m.hf[cur] : f.wild ? m.tw[cur] : m.tn[cur];
     if (fld != NONE) return 1;  // a second key at one node needs a multi[] list
     fld = id;
+    if (hash_last) m.unleaf(cur, dirty);
     dirty.push_back(cur);
     m.n_trie += 1;
   }
@@ -2030,6 +2053,12 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
     h->cfg.walk_wg_per_cu = (uint32_t)value;
     h->geom = walk_geometry(h->cfg.device, h->cfg.walk_wg_per_cu);
     return 0;  // spill scratch is re-sized by the next match (ensure_scratch)
+  }
+  if (strcmp(key, "leaf_prune") == 0) {  // 1 (default): the walk skips leaf-only children
+    if (value < 0 || value > 1) return -EINVAL;
+    if (int rc = drain_pipes(h)) return rc;
+    h->ix.leafp_mask = value ? CF_LEAFP : 0u;
+    return 0;
   }
   if (strcmp(key, "delta_commit") == 0) {
     if (value < 0 || value > 2) return -EINVAL;

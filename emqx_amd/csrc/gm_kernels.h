@@ -35,6 +35,7 @@ struct DevIndex {
   bool plain_empty = true;         // no committed non-wildcard route key
   bool wild_empty = true;          // no committed wildcard route key
   bool needs_verify = false;        // some trie filter has a hashed (long or test) token
+  uint32_t leafp_mask = 1u << 26;   // CF_LEAFP: walk skips leaf-only children (0: off, tests)
 };
 
 // Per-batch scratch (device memory, owned by the engine, grown on demand).

@@ -270,6 +270,7 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   const uint32_t per_wave = waves ? (n + waves - 1) / waves : TBLK;
   a.tblk = per_wave >= TBLK ? TBLK : ((per_wave + 7) & ~7u) < 8 ? 8 : ((per_wave + 7) & ~7u);
   a.census = census;
+  a.leafp_mask = ix.leafp_mask;
   if (census && spill)
     hipLaunchKernelGGL((k_walk<true, true>), dim3(g.blocks), dim3(WG), 0, s, a);
   else if (census)

@@ -408,9 +408,12 @@ def test_cfg3_full_size(emqx):
     import torch
     tb = torch.from_numpy(sb).cuda()
     to = torch.from_numpy(so.view(np.int32)).cuda()
+    pruned = eng.walk_census(tb.data_ptr(), to.data_ptr(), len(idx), int(so[-1]))
+    eng.tune("leaf_prune", 0)  # S(t) counts every matched prefix state
     census = eng.walk_census(tb.data_ptr(), to.data_ptr(), len(idx), int(so[-1]))
-    assert census["pairs"] == int(row[-1])
+    assert census["pairs"] == pruned["pairs"] == int(row[-1])
     assert census["states"] == int(ref.states(sb, so, threads=16).sum())
+    assert pruned["states"] < census["states"]
 
 
 def test_cfg4_exact_heavy_10m(emqx):
@@ -568,4 +571,32 @@ def test_pipelined_passes(emqx):
     row, fid, ex = _dev_to_host(eng.match_device_wait(t_a), n0)
     assert all(np.array_equal(x, y) for x, y in zip((row, fid, ex), want[0]))
     assert eng.stats()["reruns"] >= 1
+    eng.close()
+
+
+@pytest.mark.parametrize("cfg", [2, 3])
+def test_leaf_prune_is_exact(emqx, cfg):
+    """CF_LEAFP pruning (skip children that are all leaves when the topic goes deeper) returns
+    exactly the unpruned walk's rows and the oracle's, and makes fewer edge loads."""
+    import workloads
+    nf, nt = (30_000, 30_000) if cfg == 2 else (200_000, 50_000)
+    w = workloads.generate(cfg, nf, nt)
+    eng, ref = _load_both(emqx, w)
+    res = _assert_engine_equals_ref(eng, ref, None, w.tbytes, w.toff)
+    import torch
+    db = torch.from_numpy(w.tbytes).cuda()
+    do = torch.from_numpy(w.toff.view(np.int32)).cuda()
+    torch.cuda.synchronize()
+    pruned = eng.walk_census(db.data_ptr(), do.data_ptr(), w.nt, int(w.toff[-1]))
+    eng.tune("leaf_prune", 0)
+    full = eng.walk_census(db.data_ptr(), do.data_ptr(), w.nt, int(w.toff[-1]))
+    res0 = eng.match_packed(w.tbytes, w.toff)
+    assert np.array_equal(res0.row_ptr, res.row_ptr)
+    rid = np.repeat(np.arange(w.nt), np.diff(res.row_ptr.astype(np.int64)))
+    srt = lambda f: f[np.lexsort((f, rid))]  # noqa: E731  rows as sorted sets
+    assert np.array_equal(srt(res0.filter_id), srt(res.filter_id))
+    assert pruned["pairs"] == full["pairs"]
+    assert pruned["slot_loads"] <= full["slot_loads"]
+    if cfg == 3:
+        assert pruned["slot_loads"] < 0.9 * full["slot_loads"], (pruned, full)
     eng.close()
