@@ -79,8 +79,8 @@ GM_HD uint64_t key_hash(const uint8_t* p, uint32_t len, uint64_t mask) {
 // 32 B per slot, 2 x uint4, one slot per trie edge (parent --level token--> child C):
 //   s0 = {tok.lo, tok.hi, parent, cf}       key = (parent node id, level token), exact
 //   s1 = {hf, tw, p.cf, p.hf}
-//   cf  = C's node id (26 bits) | C's flags (6 bits)
-//   hf  = filter id of "C_path/#", NONE, or (CF_HFM) index into the multi[] list pool
+//   cf  = C's node id (26 bits) | C's flags (4 bits) | C's depth code (2 bits)
+//   hf  = filter id of "C_path/#", NONE, or LIST_MULTI | index into the multi[] list pool
 //   tw  = wildcard filter(s) ending exactly at C (fid, or LIST_MULTI|multi index)
 //   p   = C's '+' child {cf, hf} (cf = 0 if there is none; node 0 is the root, never a child),
 //         carried so that the walk expands it without a probe.  The rest of p (its terminal
@@ -98,13 +98,20 @@ constexpr uint32_t EDGE_SLACK = 4;  // slots >= 4 x edges (load <= 1/4): fewer b
 constexpr uint32_t CF_ID_BITS = 26;
 constexpr uint32_t CF_ID_MASK = (1u << CF_ID_BITS) - 1;
 constexpr uint32_t MAX_NODES = CF_ID_MASK;
-// child's children (literal and '+') are all leaves: no children and no '#' filter of their own,
-// so they matter only to a topic whose last word they consume -- a deeper topic skips them
-// (never set wrongly: a delta commit only ever clears it)
-constexpr uint32_t CF_LEAFP = 1u << 26;
+// Depth code h of the child C (bits CF_H0 | CF_H1 = h & 1, h & 2): every filter strictly below
+// C ends within h levels of C and none of them is a '#' filter, so a topic with more than h
+// words left after C cannot match anything below it and the walk does not expand C's children.
+// h = 0: unbounded (a '#' below, deeper filters, or unknown).  Exact at a full build; a delta
+// commit only ever resets codes to 0.
+constexpr uint32_t CF_H0 = 1u << 26;
 constexpr uint32_t CF_LIT = 1u << 27;   // child has literal (non-'+') children
 constexpr uint32_t CF_PLUS = 1u << 28;  // child has a '+' child
-constexpr uint32_t CF_HFM = 1u << 29;   // hf is a multi[] index
+constexpr uint32_t CF_H1 = 1u << 29;
+constexpr uint32_t CF_HMASK = CF_H0 | CF_H1;
+GM_HD uint32_t cf_depth_code(uint32_t cf) { return ((cf >> 26) & 1u) | ((cf >> 28) & 2u); }
+GM_HD uint32_t cf_with_depth_code(uint32_t cf, uint32_t h) {
+  return (cf & ~CF_HMASK) | ((h & 1u) << 26) | ((h & 2u) << 28);
+}
 constexpr uint32_t CF_TW = 1u << 30;    // child terminates >=1 wildcard filter
 constexpr uint32_t CF_TN = 1u << 31;    // child terminates >=1 non-wildcard trie key
 constexpr uint32_t LIST_MULTI = 0x80000000u;  // tw/tn value is a multi[] index

@@ -183,7 +183,8 @@ struct TrieModel {
   EdgeMap emap;
   // per node (root = 0): hf/tw/tn are NONE, a filter id, or LIST_MULTI | multi[] position
   std::vector<uint32_t> parent, ref, nlit, pchild, hf, tw, tn;
-  std::vector<uint8_t> leafp;  // CF_LEAFP: exact at a full build, only cleared by deltas
+  std::vector<uint8_t> hcode;  // depth code (gm_common.h CF_H0/CF_H1): exact at a full build,
+                               // only reset to 0 (unbounded) by delta commits
   std::vector<uint64_t> tok;
   std::vector<uint64_t> slot;       // edge slot of the node's incoming edge (DEAD: root/removed)
   std::vector<uint64_t> occ, tomb;  // bitmaps over edge slots: used (live or TOMB), TOMB
@@ -214,13 +215,11 @@ struct TrieModel {
     uint32_t f = i;
     if (nlit[i]) f |= CF_LIT;
     if (pchild[i]) f |= CF_PLUS;
-    if (hf[i] != NONE && (hf[i] & LIST_MULTI)) f |= CF_HFM;
     if (tw[i] != NONE) f |= CF_TW;
     if (tn[i] != NONE) f |= CF_TN;
-    if (leafp[i]) f |= CF_LEAFP;
-    return f;
+    return cf_with_depth_code(f, hcode[i]);
   }
-  uint32_t hfd(uint32_t i) const { return hf[i] == NONE ? NONE : (hf[i] & ~LIST_MULTI); }
+  uint32_t hfd(uint32_t i) const { return hf[i]; }  // id, LIST_MULTI | multi index, or NONE
   void node_slot(uint32_t c, uint4* sl) const {  // the 2 x uint4 of c's incoming edge
     const uint32_t p = pchild[c];
     sl[0] = make_uint4((uint32_t)tok[c], (uint32_t)(tok[c] >> 32), parent[c], cf(c));
@@ -236,17 +235,21 @@ struct TrieModel {
     hf.push_back(NONE);
     tw.push_back(NONE);
     tn.push_back(NONE);
-    leafp.push_back(0);
+    hcode.push_back(0);
     slot.push_back(DEAD);
     return c;
   }
-  // node y gained a child or a '#' filter: its parent's children are no longer all leaves
-  void unleaf(uint32_t y, std::vector<uint32_t>& dirty) {
-    if (y == 0) return;
-    const uint32_t p = parent[y];
-    if (leafp[p]) {
-      leafp[p] = 0;
-      dirty.push_back(p);
+  // a filter was added along path[0] = root .. path[m] (its end node; hash_last: a '#' filter
+  // hanging off path[m]): a code its ancestors can no longer guarantee is reset to unbounded
+  void widen_codes(const std::vector<uint32_t>& path, bool hash_last,
+                   std::vector<uint32_t>& dirty) {
+    const size_t m = path.size() - 1;
+    for (size_t i = 0; i < m; ++i) {
+      const uint32_t x = path[i];
+      if (hcode[x] && (hash_last || m - i > hcode[x])) {
+        hcode[x] = 0;
+        dirty.push_back(x);
+      }
     }
   }
 };
@@ -743,14 +746,19 @@ int commit_full(emqxgm* h) {
     m.max_depth = std::max<uint32_t>(m.max_depth, (uint32_t)path_len);
     lb.add(hash_last ? m.hf[cur] : f.wild ? m.tw[cur] : m.tn[cur], id);
   }
-  // CF_LEAFP: a node whose children are all leaves (no children, no '#' filter)
+  // depth codes: H(x) = how many levels below x the filters under x reach (a '#' filter below
+  // x: unbounded), bottom-up over node ids (a parent's id is smaller than its children's)
   {
     const size_t nn = m.parent.size();
-    m.leafp.assign(nn, 1);
-    for (size_t y = 1; y < nn; ++y)
-      if (m.nlit[y] || m.pchild[y] || m.hf[y] != NONE) m.leafp[m.parent[y]] = 0;
-    for (size_t x = 0; x < nn; ++x)
-      if (!m.nlit[x] && !m.pchild[x]) m.leafp[x] = 0;
+    constexpr uint32_t INF = 0xFFu;
+    std::vector<uint8_t> H(nn, 0);
+    for (size_t y = nn; y-- > 1;) {
+      const uint32_t up = (m.hf[y] != NONE || H[y] == INF) ? INF : std::min<uint32_t>(H[y] + 1u, INF - 1);
+      uint8_t& hp = H[m.parent[y]];
+      hp = (uint8_t)std::max<uint32_t>(hp, up);
+    }
+    m.hcode.assign(nn, 0);
+    for (size_t x = 0; x < nn; ++x) m.hcode[x] = (H[x] >= 1 && H[x] <= 3) ? H[x] : 0;
   }
   // flatten multi lists
   std::vector<uint32_t> multi(1, 0);
@@ -972,6 +980,7 @@ int commit_delta(emqxgm* h) {
     const bool hash_last = is_hash[nw - 1];
     const size_t path_len = hash_last ? nw - 1 : nw;
     uint32_t cur = 0;
+    path.assign(1, 0u);  // root .. end node
     for (size_t w = 0; w < path_len; ++w) {
       const uint64_t tok = is_plus[w] ? PLUS_TOK : toks[w];
       bool ins;
@@ -1003,18 +1012,18 @@ int commit_delta(emqxgm* h) {
           m.pchild[cur] = c;
         else
           m.nlit[cur] += 1;
-        m.unleaf(cur, dirty);
         dirty.push_back(cur);
         dirty.push_back(c);
       }
       cur = *v;
       m.ref[cur] += 1;
+      path.push_back(cur);
     }
     m.max_depth = std::max<uint32_t>(m.max_depth, (uint32_t)path_len);
     uint32_t& fld = hash_last ? m.hf[cur] : f.wild ? m.tw[cur] : m.tn[cur];
     if (fld != NONE) return 1;  // a second key at one node needs a multi[] list
     fld = id;
-    if (hash_last) m.unleaf(cur, dirty);
+    m.widen_codes(path, hash_last, dirty);
     dirty.push_back(cur);
     m.n_trie += 1;
   }
@@ -2057,7 +2066,7 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
   if (strcmp(key, "leaf_prune") == 0) {  // 1 (default): the walk skips leaf-only children
     if (value < 0 || value > 1) return -EINVAL;
     if (int rc = drain_pipes(h)) return rc;
-    h->ix.leafp_mask = value ? CF_LEAFP : 0u;
+    h->ix.leafp_mask = value ? CF_HMASK : 0u;
     return 0;
   }
   if (strcmp(key, "delta_commit") == 0) {

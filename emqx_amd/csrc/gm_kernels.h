@@ -35,7 +35,7 @@ struct DevIndex {
   bool plain_empty = true;         // no committed non-wildcard route key
   bool wild_empty = true;          // no committed wildcard route key
   bool needs_verify = false;        // some trie filter has a hashed (long or test) token
-  uint32_t leafp_mask = 1u << 26;   // CF_LEAFP: walk skips leaf-only children (0: off, tests)
+  uint32_t leafp_mask = (1u << 26) | (1u << 29);  // CF_HMASK: depth-code pruning (0: off)
 };
 
 // Per-batch scratch (device memory, owned by the engine, grown on demand).

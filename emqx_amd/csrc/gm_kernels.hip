@@ -239,7 +239,10 @@ hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, con
   a.xwmask = ix.xwmask;
   a.plain_empty = ix.plain_empty;
   a.wild_empty = ix.wild_empty;
-  hipLaunchKernelGGL(k_tok, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a);
+  if (ix.plain_empty)
+    hipLaunchKernelGGL(k_tok<false>, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_tok<true>, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a);
   return hipGetLastError();
 }
 
