@@ -211,15 +211,22 @@ def main():
     cpu = _cpu_baseline(w, args, cpu_job) if cpu_job is not None else None
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e:
-        # host-resident batch in, host CSR out (PCIe both ways): reported beside `value`
-        eng.match_packed(w.tbytes, w.toff)
+        # host-resident batch in, host CSR out (PCIe both ways): reported beside `value`.  The
+        # topics sit in pinned host memory, as a NIF batcher packs its window
+        # (emqxgm_host_alloc); results are read in the handle's pinned buffers (no copy).
+        hb = eng.pinned(len(w.tbytes))
+        hb[:] = w.tbytes
+        ho = eng.pinned(w.nt + 1, np.uint32)
+        ho[:] = w.toff
+        eng.match_packed(hb, ho, copy=False)
         best = 1e9
-        for _ in range(3):
+        for _ in range(5):
             t1 = time.perf_counter()
-            eng.match_packed(w.tbytes, w.toff)
+            eng.match_packed(hb, ho, copy=False)
             best = min(best, time.perf_counter() - t1)
         e2e = {"value": round(w.nt / best, 1), "unit": "topics/s", "ms_per_batch": round(best * 1e3, 3),
-               "includes": "H2D topic bytes + offsets, the device pass, D2H CSR rows + exact ids"}
+               "includes": "H2D topic bytes + offsets from pinned host memory, the device pass, "
+                           "D2H CSR rows (u64) + filter ids + exact ids into pinned host memory"}
 
     if rank == 0:
         line = {

@@ -303,9 +303,14 @@ struct emqxgm {
   uint32_t* d_in_off = nullptr;
   uint64_t in_bytes_cap = 0, in_off_cap = 0;
 
-  // ---- host outputs ----
-  std::vector<uint64_t> h_row;
-  std::vector<uint32_t> h_fid, h_exact, h_row32, h_fid_tmp;
+  // ---- host outputs (match_batch: pinned, filled by D2H copies straight from the device) ----
+  struct Pinned {
+    void* p = nullptr;
+    size_t cap = 0;
+  };
+  Pinned hp_row, hp_fid, hp_exact;
+  uint64_t* d_row64 = nullptr;  // device u64 row pointers of one chunk
+  uint64_t row64_cap = 0;
 
   // ---- publish fan-out state (host registry; device tables built at commit) ----
   std::unordered_map<uint32_t, std::vector<std::pair<uint32_t, uint32_t>>> rdest;  // (node, group)
@@ -1426,6 +1431,19 @@ int run_fanout(emqxgm* h, uint32_t n, uint32_t* n_routes, uint32_t* n_deliv) {
   return 0;
 }
 
+// Grows a pinned host buffer to `bytes` (keep: preserve the old contents).
+int pinned_reserve(emqxgm* h, emqxgm::Pinned& b, size_t bytes, bool keep) {
+  if (bytes <= b.cap) return 0;
+  const size_t cap = std::max<size_t>(bytes + bytes / 4, 1 << 16);
+  void* p = nullptr;
+  HIPCHK(h, hipHostMalloc(&p, cap, hipHostMallocDefault));
+  if (keep && b.p && b.cap) memcpy(p, b.p, b.cap);
+  if (b.p) (void)hipHostFree(b.p);
+  b.p = p;
+  b.cap = cap;
+  return 0;
+}
+
 int ensure_input(emqxgm* h, uint64_t bytes, uint64_t offs) {
   if (bytes > h->in_bytes_cap) {
     if (h->d_in_bytes) (void)hipFree(h->d_in_bytes);
@@ -1503,6 +1521,9 @@ void emqxgm_destroy(emqxgm_t* h) {
     free_bufs(p.bufs);
     if (p.sc.ctl_host) (void)hipHostFree(p.sc.ctl_host);
   }
+  for (auto* b : {&h->hp_row, &h->hp_fid, &h->hp_exact})
+    if (b->p) (void)hipHostFree(b->p);
+  if (h->d_row64) (void)hipFree(h->d_row64);
   free_bufs(h->ix_bufs);
   free_bufs(h->sc_bufs);
   free_bufs(h->fan_bufs);
@@ -1872,52 +1893,73 @@ int emqxgm_match_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offset
   if (!h || !out || (!offsets && n)) return -EINVAL;
   std::lock_guard<std::mutex> g(h->mu);
   if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
-  h->h_row.assign((size_t)n + 1, 0);
-  h->h_exact.assign(n, NONE);
-  h->h_fid.clear();
+  // results land in pinned host buffers of the handle by D2H copies (u64 row pointers are built
+  // on the device): no host-side conversion or initialisation per topic
+  int rc = 0;
+  if ((rc = pinned_reserve(h, h->hp_row, ((size_t)n + 1) * 8, false)) ||
+      (rc = pinned_reserve(h, h->hp_exact, std::max<size_t>((size_t)n * 4, 4), false)) ||
+      (rc = pinned_reserve(h, h->hp_fid, 4, false)))
+    return rc;
+  uint64_t* row = (uint64_t*)h->hp_row.p;
+  row[0] = 0;
+  uint64_t total = 0;
   std::vector<uint32_t> loff;
-  for (uint32_t i0 = 0; i0 < n || (n == 0 && i0 == 0); i0 += h->cfg.batch_max) {
+  for (uint32_t i0 = 0; i0 < n; i0 += h->cfg.batch_max) {
     const uint32_t i1 = std::min<uint64_t>((uint64_t)i0 + h->cfg.batch_max, n);
     const uint32_t m = i1 - i0;
-    const uint64_t b0 = n ? offsets[i0] : 0, b1 = n ? offsets[i1] : 0;
+    const uint64_t b0 = offsets[i0], b1 = offsets[i1];
     if (b1 < b0) return -EINVAL;
     loff.resize((size_t)m + 1);
     for (uint32_t i = 0; i <= m; ++i) {
       if (offsets[i0 + i] < b0 || (i && offsets[i0 + i] < offsets[i0 + i - 1])) return -EINVAL;
       loff[i] = (uint32_t)(offsets[i0 + i] - b0);
     }
-    int rc = ensure_input(h, std::max<uint64_t>(b1 - b0, 1), (uint64_t)m + 1);
-    if (rc) return rc;
+    if ((rc = ensure_input(h, std::max<uint64_t>(b1 - b0, 1), (uint64_t)m + 1))) return rc;
     if (b1 > b0)
       HIPCHK(h, hipMemcpyAsync(h->d_in_bytes, bytes + b0, b1 - b0, hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, hipMemcpyAsync(h->d_in_off, loff.data(), ((size_t)m + 1) * 4, hipMemcpyHostToDevice,
                              h->stream));
     uint32_t pairs = 0;
-    rc = run_device(h, h->d_in_bytes, h->d_in_off, m, b1 - b0, &pairs);
-    if (rc) return rc;
-    h->h_row32.resize((size_t)m + 1);
-    h->h_fid_tmp.resize(pairs);
-    if (m) {
-      HIPCHK(h, hipMemcpyAsync(h->h_row32.data(), h->sc.row, ((size_t)m + 1) * 4,
-                               hipMemcpyDeviceToHost, h->stream));
-      HIPCHK(h, hipMemcpyAsync(h->h_exact.data() + i0, h->sc.exact_id, (size_t)m * 4,
-                               hipMemcpyDeviceToHost, h->stream));
+    if ((rc = run_device(h, h->d_in_bytes, h->d_in_off, m, b1 - b0, &pairs))) return rc;
+    if ((uint64_t)m + 1 > h->row64_cap) {
+      if (h->d_row64) (void)hipFree(h->d_row64);
+      h->d_row64 = nullptr;
+      h->row64_cap = 0;
+      HIPCHK(h, hipMalloc((void**)&h->d_row64, ((size_t)m + 1) * 8));
+      h->row64_cap = (uint64_t)m + 1;
     }
+    if ((rc = pinned_reserve(h, h->hp_fid, std::max<size_t>((total + pairs) * 4, 4), true)))
+      return rc;
+    HIPCHK(h, launch_row64(h->sc.row, total, h->d_row64, m + 1, h->stream));
+    HIPCHK(h, hipMemcpyAsync(row + i0, h->d_row64, ((size_t)m + 1) * 8, hipMemcpyDeviceToHost,
+                             h->stream));
+    HIPCHK(h, hipMemcpyAsync((uint32_t*)h->hp_exact.p + i0, h->sc.exact_id, (size_t)m * 4,
+                             hipMemcpyDeviceToHost, h->stream));
     if (pairs)
-      HIPCHK(h, hipMemcpyAsync(h->h_fid_tmp.data(), h->sc.out, (size_t)pairs * 4,
+      HIPCHK(h, hipMemcpyAsync((uint32_t*)h->hp_fid.p + total, h->sc.out, (size_t)pairs * 4,
                                hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    const uint64_t base = h->h_fid.size();
-    for (uint32_t i = 0; i <= m; ++i) h->h_row[i0 + i] = base + h->h_row32[i];
-    h->h_fid.insert(h->h_fid.end(), h->h_fid_tmp.begin(), h->h_fid_tmp.end());
-    if (n == 0) break;
+    total += pairs;
   }
   out->n = n;
-  out->n_pairs = h->h_fid.size();
-  out->row_ptr = h->h_row.data();
-  out->filter_id = h->h_fid.data();
-  out->exact_id = h->h_exact.data();
+  out->n_pairs = total;
+  out->row_ptr = row;
+  out->filter_id = (const uint32_t*)h->hp_fid.p;
+  out->exact_id = (const uint32_t*)h->hp_exact.p;
   return 0;
+}
+
+void* emqxgm_host_alloc(emqxgm_t* h, uint64_t bytes) {
+  if (!h) return nullptr;
+  void* p = nullptr;
+  if (hipSetDevice(h->cfg.device) != hipSuccess ||
+      hipHostMalloc(&p, std::max<uint64_t>(bytes, 1), hipHostMallocDefault) != hipSuccess)
+    return nullptr;
+  return p;
+}
+
+void emqxgm_host_free(emqxgm_t* h, void* p) {
+  if (h && p) (void)hipHostFree(p);
 }
 
 int emqxgm_publish_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets, uint32_t n,

@@ -172,5 +172,8 @@ hipError_t launch_scatter(Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_
 hipError_t launch_verify_scatter(const uint8_t* bytes, const uint32_t* off, const DevIndex& ix,
                                  Scratch& sc, uint32_t n, hipStream_t s);
 hipError_t launch_fixup(Scratch& sc, uint32_t n, hipStream_t s);
+// out[i] = base + row[i], i < m (u64 CSR row pointers of the host API, built on the device)
+hipError_t launch_row64(const uint32_t* row, uint64_t base, uint64_t* out, uint32_t m,
+                        hipStream_t s);
 
 }  // namespace gm

@@ -177,6 +177,11 @@ __global__ __launch_bounds__(WG) void k_scan_final(const uint32_t* __restrict__ 
 #include "gm_rules.inc"
 #include "gm_retain.inc"
 
+__global__ __launch_bounds__(WG) void k_row64(const uint32_t* row, uint64_t base, uint64_t* out,
+                                              uint32_t m) {
+  for (uint32_t i = blockIdx.x * WG + threadIdx.x; i < m; i += gridDim.x * WG) out[i] = base + row[i];
+}
+
 uint32_t grid_for(uint64_t items, uint32_t cap_blocks) {
   uint64_t b = (items + WG - 1) / WG;
   if (b == 0) b = 1;
@@ -348,6 +353,13 @@ hipError_t launch_fixup(Scratch& sc, uint32_t n, hipStream_t s) {
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_compact_rows, dim3(grid_for(n, 4096)), dim3(WG), 0, s, sc.row, sc.out,
                      sc.row2, sc.out2, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_row64(const uint32_t* row, uint64_t base, uint64_t* out, uint32_t m,
+                        hipStream_t s) {
+  if (m == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_row64, dim3(grid_for(m, 4096)), dim3(WG), 0, s, row, base, out, m);
   return hipGetLastError();
 }
 

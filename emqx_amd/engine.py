@@ -89,6 +89,8 @@ SYMBOLS = {
     "emqxgm_match_batch": (C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(_Out)]),
     "emqxgm_match_device": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, C.POINTER(_DevOut)]),
     "emqxgm_match_device_submit": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, _U64P]),
+    "emqxgm_host_alloc": (C.c_void_p, [_P, C.c_uint64]),
+    "emqxgm_host_free": (None, [_P, C.c_void_p]),
     "emqxgm_match_device_wait": (C.c_int, [_P, C.c_uint64, C.POINTER(_DevOut)]),
     "emqxgm_walk_census": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, _U64P]),
     "emqxgm_route_add": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32]),
@@ -215,9 +217,13 @@ class Engine:
         if rc != 0:
             raise EngineError(f"emqxgm_create failed ({rc}): no usable HIP device {device}")
         self._h = h
+        self._pinned = []
 
     def close(self):
         if getattr(self, "_h", None):
+            for p in getattr(self, "_pinned", []):
+                self._lib.emqxgm_host_free(self._h, p)
+            self._pinned = []
             self._lib.emqxgm_destroy(self._h)
             self._h = None
 
@@ -324,19 +330,32 @@ class Engine:
         return C.string_at(p, n.value)
 
     # ---- match ----
-    def match_packed(self, buf: np.ndarray, off: np.ndarray) -> MatchResult:
+    def match_packed(self, buf: np.ndarray, off: np.ndarray, copy: bool = True) -> MatchResult:
+        """emqxgm_match_batch over packed topics.  copy=False returns views of the handle's
+        pinned result buffers (valid until the next call on this handle)."""
         off32 = np.ascontiguousarray(off, dtype=np.uint32)
         buf = np.ascontiguousarray(buf, dtype=np.uint8)
         n = len(off32) - 1
         out = _Out()
         self._check(self._lib.emqxgm_match_batch(self._h, _ptr(buf), _ptr(off32), n,
                                                  C.byref(out)), "match_batch")
-        row = np.ctypeslib.as_array(out.row_ptr, shape=(n + 1,)).copy()
-        fid = (np.ctypeslib.as_array(out.filter_id, shape=(out.n_pairs,)).copy()
+        cp = (lambda a: a.copy()) if copy else (lambda a: a)  # noqa: E731
+        row = cp(np.ctypeslib.as_array(out.row_ptr, shape=(n + 1,)))
+        fid = (cp(np.ctypeslib.as_array(out.filter_id, shape=(out.n_pairs,)))
                if out.n_pairs else np.zeros(0, np.uint32))
-        ex = (np.ctypeslib.as_array(out.exact_id, shape=(n,)).copy() if n
+        ex = (cp(np.ctypeslib.as_array(out.exact_id, shape=(n,))) if n
               else np.zeros(0, np.uint32))
         return MatchResult(row, fid, ex)
+
+    def pinned(self, n: int, dtype=np.uint8) -> np.ndarray:
+        """A numpy array in pinned host memory (emqxgm_host_alloc), freed with the engine."""
+        nbytes = max(1, int(n) * np.dtype(dtype).itemsize)
+        p = self._lib.emqxgm_host_alloc(self._h, nbytes)
+        if not p:
+            raise EngineError("emqxgm_host_alloc failed")
+        self._pinned.append(p)
+        arr = np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(p))
+        return arr.view(dtype)[:int(n)]
 
     def match(self, topics: Sequence[bytes]) -> MatchResult:
         buf, off = pack(list(topics), np.uint64)

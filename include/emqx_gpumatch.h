@@ -158,6 +158,12 @@ int emqxgm_match_device(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_o
  * until the wait.  A commit first completes every pass in flight (results stay retrievable).
  * Results are identical to emqxgm_match_device's. */
 #define EMQXGM_PIPES 2
+
+/* Pinned (page-locked) host memory on the handle's device, for the caller's topic staging: a
+ * batcher that packs its window into it gets full-speed H2D copies from emqxgm_match_batch.
+ * NULL on failure.  emqxgm_host_free releases it. */
+void* emqxgm_host_alloc(emqxgm_t* h, uint64_t bytes);
+void emqxgm_host_free(emqxgm_t* h, void* p);
 int emqxgm_match_device_submit(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_offsets,
                                uint32_t n, uint64_t bytes_len, uint64_t* ticket);
 int emqxgm_match_device_wait(emqxgm_t* h, uint64_t ticket, emqxgm_dev_out* out);

@@ -600,3 +600,29 @@ def test_leaf_prune_is_exact(emqx, cfg):
     if cfg == 3:
         assert pruned["slot_loads"] < 0.9 * full["slot_loads"], (pruned, full)
     eng.close()
+
+
+def test_host_batch_chunks_and_pinned_io(emqx):
+    """emqxgm_match_batch splits a batch larger than batch_max into device passes; row pointers
+    (u64, built on the device) continue across chunks and the pinned result buffers grow; topic
+    bytes staged in emqxgm_host_alloc memory give the same answer."""
+    import workloads
+    w = workloads.generate(1, 5000, 20000)
+    ref_eng, _ = _load_both(emqx, w)
+    want = ref_eng.match_packed(w.tbytes, w.toff)
+    eng, _ = _load_both(emqx, w, batch_max=3000)  # 7 chunks
+    got = eng.match_packed(w.tbytes, w.toff)
+    assert np.array_equal(got.row_ptr, want.row_ptr)
+    assert np.array_equal(got.filter_id, want.filter_id)
+    assert np.array_equal(got.exact_id, want.exact_id)
+    hb = eng.pinned(len(w.tbytes))
+    hb[:] = w.tbytes
+    ho = eng.pinned(w.nt + 1, np.uint32)
+    ho[:] = w.toff
+    view = eng.match_packed(hb, ho, copy=False)
+    assert np.array_equal(view.row_ptr, want.row_ptr)
+    assert np.array_equal(view.filter_id, want.filter_id)
+    empty = eng.match([])
+    assert list(empty.row_ptr) == [0] and empty.filter_id.size == 0
+    eng.close()
+    ref_eng.close()
