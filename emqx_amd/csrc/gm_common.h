@@ -97,7 +97,15 @@ constexpr uint32_t EBUCKET = 2;
 constexpr uint32_t EDGE_SLACK = 4;  // slots >= 4 x edges (load <= 1/4): fewer bucket overflows
 constexpr uint32_t CF_ID_BITS = 26;
 constexpr uint32_t CF_ID_MASK = (1u << CF_ID_BITS) - 1;
-constexpr uint32_t MAX_NODES = CF_ID_MASK;
+constexpr uint32_t MAX_NODES = CF_ID_MASK - 1;  // ids stay below TOMB's and NONE's low 26 bits
+// Child signature: the top 6 bits of a slot's parent word (parent ids use 26) hold a 1-bit-per-
+// class summary of the child's literal children's level tokens (class = sig_bit(token)); the
+// walk does not probe a literal child whose token's class bit is clear.  Bits are only ever
+// added (a delta commit ORs a new child in, deletions leave them), so a clear bit is exact.
+constexpr uint32_t SIG_SHIFT = CF_ID_BITS;
+GM_HD uint32_t sig_bit(uint64_t tok) {
+  return 1u << (uint32_t)(((((tok * 0x9E3779B97F4A7C15ull) >> 32) & 0xFFFFFFFFull) * 6ull) >> 32);
+}
 // Depth code h of the child C (bits CF_H0 | CF_H1 = h & 1, h & 2): every filter strictly below
 // C ends within h levels of C and none of them is a '#' filter, so a topic with more than h
 // words left after C cannot match anything below it and the walk does not expand C's children.

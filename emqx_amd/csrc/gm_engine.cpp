@@ -183,6 +183,7 @@ struct TrieModel {
   EdgeMap emap;
   // per node (root = 0): hf/tw/tn are NONE, a filter id, or LIST_MULTI | multi[] position
   std::vector<uint32_t> parent, ref, nlit, pchild, hf, tw, tn;
+  std::vector<uint8_t> sig;    // gm_common.h sig_bit classes of the node's literal children
   std::vector<uint8_t> hcode;  // depth code (gm_common.h CF_H0/CF_H1): exact at a full build,
                                // only reset to 0 (unbounded) by delta commits
   std::vector<uint64_t> tok;
@@ -222,7 +223,8 @@ struct TrieModel {
   uint32_t hfd(uint32_t i) const { return hf[i]; }  // id, LIST_MULTI | multi index, or NONE
   void node_slot(uint32_t c, uint4* sl) const {  // the 2 x uint4 of c's incoming edge
     const uint32_t p = pchild[c];
-    sl[0] = make_uint4((uint32_t)tok[c], (uint32_t)(tok[c] >> 32), parent[c], cf(c));
+    sl[0] = make_uint4((uint32_t)tok[c], (uint32_t)(tok[c] >> 32),
+                       parent[c] | ((uint32_t)sig[c] << SIG_SHIFT), cf(c));
     sl[1] = make_uint4(hfd(c), tw[c], p ? cf(p) : 0u, p ? hfd(p) : NONE);
   }
   uint32_t new_node(uint32_t par, uint64_t t) {
@@ -236,6 +238,7 @@ struct TrieModel {
     tw.push_back(NONE);
     tn.push_back(NONE);
     hcode.push_back(0);
+    sig.push_back(0);
     slot.push_back(DEAD);
     return c;
   }
@@ -751,6 +754,9 @@ int commit_full(emqxgm* h) {
     m.max_depth = std::max<uint32_t>(m.max_depth, (uint32_t)path_len);
     lb.add(hash_last ? m.hf[cur] : f.wild ? m.tw[cur] : m.tn[cur], id);
   }
+  // child signatures
+  for (size_t y = 1; y < m.parent.size(); ++y)
+    if (m.tok[y] != PLUS_TOK) m.sig[m.parent[y]] |= (uint8_t)sig_bit(m.tok[y]);
   // depth codes: H(x) = how many levels below x the filters under x reach (a '#' filter below
   // x: unbounded), bottom-up over node ids (a parent's id is smaller than its children's)
   {
@@ -873,6 +879,7 @@ int commit_full(emqxgm* h) {
   nx.xwmask = m.xcap_w - 1;
   const uint32_t root_p = m.pchild[0];
   nx.root_cf = m.cf(0);
+  nx.root_sig = m.sig[0];
   nx.root_hf = m.hfd(0);
   nx.root_pcf = root_p ? m.cf(root_p) : 0u;
   nx.root_phf = root_p ? m.hfd(root_p) : NONE;
@@ -1013,10 +1020,12 @@ int commit_delta(emqxgm* h) {
         m.slot[c] = i;
         epatch[i] = c;
         m.n_edges += 1;
-        if (is_plus[w])
+        if (is_plus[w]) {
           m.pchild[cur] = c;
-        else
+        } else {
           m.nlit[cur] += 1;
+          m.sig[cur] |= (uint8_t)sig_bit(tok);
+        }
         dirty.push_back(cur);
         dirty.push_back(c);
       }
@@ -1101,6 +1110,7 @@ int commit_delta(emqxgm* h) {
   DevIndex& ix = h->ix;
   const uint32_t root_p = m.pchild[0];
   ix.root_cf = m.cf(0);
+  ix.root_sig = m.sig[0];
   ix.root_hf = m.hfd(0);
   ix.root_pcf = root_p ? m.cf(root_p) : 0u;
   ix.root_phf = root_p ? m.hfd(root_p) : NONE;

@@ -12,6 +12,7 @@ struct DevIndex {
   const uint32_t* multi = nullptr;  // [count, fid...] lists
   uint32_t root_cf = 0, root_hf = 0xFFFFFFFFu;
   uint32_t root_pcf = 0, root_phf = 0xFFFFFFFFu;  // root's '+' child (cf 0: none)
+  uint32_t root_sig = 0x3Fu;                       // root's child signature (gm_common.h)
   const uint32_t* tn_of = nullptr;  // per node: non-wildcard trie keys ending there
   // publish fan-out tables (gm_fanout.inc), per filter id < fan_nf
   const uint4* fan = nullptr;        // [fan_nf] {rt off, rt count, dl off, dl count}

@@ -279,6 +279,7 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   a.tblk = per_wave >= TBLK ? TBLK : ((per_wave + 7) & ~7u) < 8 ? 8 : ((per_wave + 7) & ~7u);
   a.census = census;
   a.leafp_mask = ix.leafp_mask;
+  a.root_sig = ix.root_sig;
   if (census && spill)
     hipLaunchKernelGGL((k_walk<true, true>), dim3(g.blocks), dim3(WG), 0, s, a);
   else if (census)
