@@ -65,8 +65,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # EMQXGM_DIST_BACKEND=gloo rehearses the N>1 control flow with several ranks sharing the
+    # GPUs of a smaller box (RCCL refuses two ranks on one device); production is RCCL ("nccl")
     if world > 1:
-        dist.init_process_group("nccl")
+        dist.init_process_group(os.environ.get("EMQXGM_DIST_BACKEND", "nccl"))
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
