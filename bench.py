@@ -227,9 +227,32 @@ def main():
             t1 = time.perf_counter()
             eng.match_packed(hb, ho, copy=False)
             best = min(best, time.perf_counter() - t1)
-        e2e = {"value": round(w.nt / best, 1), "unit": "topics/s", "ms_per_batch": round(best * 1e3, 3),
+        # the NIF batcher's call: emqxgm_match_batch_submit/_wait with HOST_PIPES batches in
+        # flight (one batch's upload, another's pass and a third's download overlap)
+        k = max(10, args.steps)
+        pend = []
+        for _ in range(eng.HOST_PIPES):
+            pend.append(eng.match_batch_submit(hb, ho))
+            if len(pend) == eng.HOST_PIPES:
+                eng.match_batch_wait(pend.pop(0), copy=False)
+        while pend:
+            eng.match_batch_wait(pend.pop(0), copy=False)
+        t1 = time.perf_counter()
+        for _ in range(k):
+            pend.append(eng.match_batch_submit(hb, ho))
+            if len(pend) == eng.HOST_PIPES:
+                eng.match_batch_wait(pend.pop(0), copy=False)
+        while pend:
+            eng.match_batch_wait(pend.pop(0), copy=False)
+        pipe_s = (time.perf_counter() - t1) / k
+        e2e = {"value": round(w.nt / pipe_s, 1), "unit": "topics/s",
+               "ms_per_batch": round(pipe_s * 1e3, 3), "batches_in_flight": eng.HOST_PIPES,
                "includes": "H2D topic bytes + offsets from pinned host memory, the device pass, "
-                           "D2H CSR rows (u64) + filter ids + exact ids into pinned host memory"}
+                           "row pointers (u32) + filter ids + exact ids written into pinned host "
+                           "memory (emqxgm_match_batch_submit/_wait)",
+               "one_call_at_a_time": {"value": round(w.nt / best, 1),
+                                      "ms_per_batch": round(best * 1e3, 3),
+                                      "api": "emqxgm_match_batch (u64 row pointers)"}}
 
     if rank == 0:
         line = {

@@ -15,9 +15,12 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <memory>
 #include <mutex>
 #include <new>
+#include <shared_mutex>
 #include <string>
 #include <unordered_map>
 #include <utility>
@@ -150,6 +153,52 @@ struct DevBuf {
   size_t bytes = 0;
 };
 
+// Device buffers freed together.  Epochs share them: consecutive delta commits patch one table
+// set in place, and an append-only mirror that outgrows its buffer moves to a new one while the
+// epochs still reading the old buffer keep it alive.
+struct DevOwner {
+  std::vector<DevBuf> bufs;
+  DevOwner() = default;
+  explicit DevOwner(std::vector<DevBuf>&& b) : bufs(std::move(b)) {}
+  DevOwner(const DevOwner&) = delete;
+  DevOwner& operator=(const DevOwner&) = delete;
+  ~DevOwner() {
+    for (auto& b : bufs)
+      if (b.p) (void)hipFree(b.p);
+  }
+};
+using OwnerP = std::shared_ptr<DevOwner>;
+
+// One committed index as match passes read it (the reference's committed mria state: readers
+// never see a transaction half applied, emqx_router_utils.erl:74-135).  A pass takes the current
+// epoch under emqxgm::emu and enqueues every launch that reads the tables before letting go, so a
+// later delta commit -- which patches the shared tables in place -- is ordered behind it on the
+// GPU (hipStreamWaitEvent on the pass's `done` event); a full build writes new tables and never
+// waits for readers at all.
+struct Epoch {
+  uint64_t id = 0;
+  DevIndex ix;
+  std::vector<OwnerP> owners;   // tables, fan-out tables, pool mirrors
+  hipEvent_t ready = nullptr;   // this epoch's uploads / patches are complete (writer stream)
+  std::atomic<bool> walk_spill{false};  // its walks need the spilling variant (learnt by a pass)
+  ~Epoch() {
+    if (ready) (void)hipEventDestroy(ready);
+  }
+};
+using EpochP = std::shared_ptr<Epoch>;
+
+// A reader's pass resources: scratch, stream, timing events.  One for synchronous calls, one per
+// pipelined pass slot (device-resident and host-in/host-out pipes).
+struct PassCtx {
+  Scratch sc;
+  std::vector<DevBuf> bufs;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t done = nullptr;  // recorded after each pass enqueued here (guarded by emqxgm::emu)
+  bool done_rec = false;
+  EpochP epoch;               // epoch of the pass last enqueued here (kept until it completes)
+};
+
 constexpr uint64_t DEAD = ~0ull;  // TrieModel::slot of the root and of removed nodes
 
 // Device writes staged by one commit (k_patch): dword runs to device addresses, uploaded in
@@ -209,7 +258,7 @@ struct TrieModel {
   uint64_t xnext(bool w, uint64_t b) const {
     return xbase(w) + ((b - xbase(w) + 1) & (xcapr(w) - 1));
   }
-  // device tables patched in place (owned by emqxgm::ix_bufs)
+  // device tables patched in place (owned by emqxgm::o_tab)
   uint32_t *d_edges = nullptr, *d_exact = nullptr, *d_tn = nullptr, *d_fv = nullptr;
 
   uint32_t cf(uint32_t i) const {  // gm_common.h cf: id | flags
@@ -264,7 +313,7 @@ struct FanModel {
   uint64_t cap = 0;  // filter ids with an entry (0: no tables)
   uint64_t rt_used = 0, rt_cap = 0, dl_used = 0, dl_cap = 0, garbage = 0;
   std::vector<uint4> ent;
-  uint32_t *d_ent = nullptr, *d_rt = nullptr, *d_dl = nullptr;  // owned by emqxgm::fan_tab_bufs
+  uint32_t *d_ent = nullptr, *d_rt = nullptr, *d_dl = nullptr;  // owned by emqxgm::o_fan
 };
 
 inline bool bit(const std::vector<uint64_t>& b, uint64_t i) { return (b[i >> 6] >> (i & 63)) & 1; }
@@ -273,10 +322,27 @@ inline void bclr(std::vector<uint64_t>& b, uint64_t i) { b[i >> 6] &= ~(1ull << 
 
 }  // namespace
 
+// Device mirror of an append-only host array (filter pool, offsets, verification records).
+struct Mirror {
+  DevBuf b;
+  OwnerP o;              // owns b; epochs that read b hold it too
+  uint64_t uploaded = 0; // bytes already on the device
+};
+
+// Locking (include/emqx_gpumatch.h "Threading"):
+//   wmu  writers: registry mutations and commit (a full build runs under it for seconds);
+//   pmu  the registry's storage (pool, filters, slots): writers hold it exclusively only while
+//        they grow it, filter_bytes / lookup_id / trie_member read under it shared;
+//   emu  the current epoch and the reader streams' done events: a reader holds it while it
+//        enqueues a pass, a writer while it orders its patches behind those passes and swaps;
+//   mmu  the readers' pass resources (sync context, pipes, geometry): match calls serialise
+//        on it among themselves, never against a writer;
+//   stmu / errmu  statistics and the last-error string.
 struct emqxgm {
-  std::mutex mu;
+  std::mutex wmu, emu, mmu, stmu, errmu;
+  std::shared_mutex pmu;
   emqxgm_cfg cfg{};
-  hipStream_t stream = nullptr;
+  hipStream_t wstream = nullptr;  // writer stream: patch uploads and k_patch
   std::string err;
 
   // ---- registry (pending state) ----
@@ -287,21 +353,23 @@ struct emqxgm {
   uint64_t n_trie_pending = 0, n_route_pending = 0;
   bool dirty = false;
 
-  // ---- committed device index ----
+  // ---- the writer's working copy of the committed index (published as epochs) ----
   uint64_t epoch = 0;
   DevIndex ix;
-  std::vector<DevBuf> ix_bufs;
-  uint64_t pool_uploaded = 0;  // bytes of pool already on device
-  DevBuf d_pool, d_foff, d_fver;
-  uint64_t foff_uploaded = 0, fver_uploaded = 0;  // bytes
+  OwnerP o_tab;  // edge slots, multi lists, tn side array, verify bits, exact table
+  Mirror m_pool, m_foff, m_fver;
   std::vector<uint64_t> foff_host;  // [n_filters+1]
   std::vector<uint8_t> fver_host;   // 64 B per filter
   emqxgm_stats st{};
 
-  // ---- batch scratch ----
-  Scratch sc;
-  std::vector<DevBuf> sc_bufs;
+  // ---- what readers see ----
+  EpochP cur;                      // current epoch (emu)
+  std::vector<EpochP> graveyard;   // retired epochs a reader may still hold (swept by writers)
+
+  // ---- reader side (mmu) ----
+  PassCtx sync;                    // synchronous calls
   WalkGeom geom;
+  uint32_t leafp_mask = CF_HMASK;  // depth-code pruning (tune "leaf_prune")
   uint8_t* d_in_bytes = nullptr;
   uint32_t* d_in_off = nullptr;
   uint64_t in_bytes_cap = 0, in_off_cap = 0;
@@ -325,9 +393,7 @@ struct emqxgm {
   std::vector<uint32_t> h_rf, h_rd, h_df, h_ds, h_tmp32;
 
   bool profiling = false;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   uint32_t spill_want = 0;         // walk spill items per lane (grown on overflow)
-  bool walk_spill = false;         // committed index needs the spilling walk variant
   uint32_t reject_cap = 1u << 20;  // cfg.reject_cap overrides (tests force the legacy path)
   uint64_t test_mask = 0;          // != 0: collision-test tokens (cfg.word_hash_bits)
 
@@ -335,10 +401,7 @@ struct emqxgm {
   // scratch, stream and events, so a batch can be enqueued while the previous one still runs
   // (its walk's tail then overlaps the next batch's tokenizer and walk) ----
   struct Pipe {
-    Scratch sc;
-    std::vector<DevBuf> bufs;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    PassCtx c;
     uint64_t ticket = 0;  // last ticket submitted here (0: never)
     int state = 0;        // 0 idle / result taken, 1 in flight, 2 result ready
     const uint8_t* d_bytes = nullptr;
@@ -348,13 +411,33 @@ struct emqxgm {
   } pipes[EMQXGM_PIPES];
   uint64_t next_ticket = 1;
 
-  // ---- delta commits ----
+  // ---- pipelined host passes (emqxgm_match_batch_submit / _wait): the pipe's stream carries the
+  // H2D copy of its batch, the pass and the copy of its result into pinned host memory, so one
+  // batch's upload, another's pass and a third's download overlap ----
+  struct HostPipe {
+    PassCtx c;
+    uint64_t ticket = 0;
+    int state = 0;  // as Pipe
+    uint8_t* d_bytes = nullptr;
+    uint32_t* d_off = nullptr;
+    uint64_t bytes_cap = 0, off_cap = 0;
+    uint32_t* h_row = nullptr;  // pinned results: row pointers [n+1], exact ids [n], filter ids
+    uint32_t* h_exact = nullptr;
+    uint32_t* h_fid = nullptr;
+    uint64_t row_cap = 0, fid_cap = 0;  // entries
+    uint32_t n = 0, pairs = 0;
+    uint64_t bytes_len = 0;
+  } hpipes[EMQXGM_HOST_PIPES];
+  uint64_t next_hticket = 1;
+  uint32_t host_out_mode = 1;  // results to the host: 1 = copy kernel, 0 = hipMemcpyAsync
+
+  // ---- delta commits (writer side) ----
   TrieModel tm;
   std::vector<uint32_t> changed;  // filter ids whose trie / route-key membership may differ
   FanModel fm;
   std::vector<uint32_t> fan_changed;  // filter ids whose fan-out lists may differ
   bool fan_rebuild = false;           // every filter's lists may differ (local node changed)
-  std::vector<DevBuf> fan_tab_bufs;
+  OwnerP o_fan;                       // the fan-out tables
   PatchList patches;
   DevBuf d_patch;                   // device copy of the staged patch list
   DevBuf d_rules;                   // emqxgm_match_rules inputs and output
@@ -366,8 +449,13 @@ struct emqxgm {
 
 namespace {
 
+void set_err(emqxgm* h, std::string msg) {
+  std::lock_guard<std::mutex> g(h->errmu);
+  h->err = std::move(msg);
+}
+
 int fail(emqxgm* h, hipError_t e, const char* what) {
-  h->err = std::string(what) + ": " + hipGetErrorString(e);
+  set_err(h, std::string(what) + ": " + hipGetErrorString(e));
   return -EIO;
 }
 
@@ -470,19 +558,26 @@ struct ListBuild {
   }
 };
 
+int patch_wait(emqxgm* h);
+
 // Grow-and-append a device mirror of an append-only host array (bytes [uploaded, total)).
-// Without growth and with a patch list, the new tail (whole dwords) goes into the list.
-int append_upload(emqxgm* h, DevBuf& buf, uint64_t& uploaded, const void* src, uint64_t total,
-                  PatchList* pl) {
+// Without growth and with a patch list, the new tail (whole dwords) goes into the list.  Readers
+// of committed epochs only read the prefix those epochs knew, so the tail is written while they
+// run; a grown mirror moves to a new buffer and the epochs holding the old one keep it.
+int append_upload(emqxgm* h, Mirror& m, const void* src, uint64_t total, PatchList* pl) {
+  DevBuf& buf = m.b;
+  uint64_t& uploaded = m.uploaded;
   const uint64_t need = std::max<uint64_t>(16, (total + 3) & ~3ull);
   if (need > buf.bytes) {
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (int rc = patch_wait(h)) return rc;  // earlier patches into the old buffer have landed
     DevBuf nb;
     nb.bytes = std::max<uint64_t>(need, buf.bytes * 2);
     HIPCHK(h, hipMalloc(&nb.p, nb.bytes));
+    auto o = std::make_shared<DevOwner>();
+    o->bufs.push_back(nb);
     if (uploaded) HIPCHK(h, hipMemcpy(nb.p, buf.p, uploaded, hipMemcpyDeviceToDevice));
-    if (buf.p) (void)hipFree(buf.p);
     buf = nb;
+    m.o = std::move(o);  // the old buffer lives on with the epochs that read it
     pl = nullptr;
   }
   if (total > uploaded) {
@@ -501,8 +596,8 @@ int append_upload(emqxgm* h, DevBuf& buf, uint64_t& uploaded, const void* src, u
 }
 
 // Upload the staged patch list: one copy through pinned memory and one k_patch launch on the
-// engine stream (matches are ordered behind it).  patch_wait() before the staging is reused
-// or a patched buffer is freed.
+// writer stream (publish_epoch orders it behind the passes already enqueued and every later pass
+// behind it).  patch_wait() before the staging is reused or a patched buffer is freed.
 int patch_wait(emqxgm* h) {
   if (h->patch_ev) HIPCHK(h, hipEventSynchronize(h->patch_ev));
   return 0;
@@ -531,11 +626,11 @@ int patch_flush(emqxgm* h) {
   }
   memcpy(h->h_stage, pl.ents.data(), eb);
   memcpy(h->h_stage + eb, pl.src.data(), pl.src.size() * 4);
-  HIPCHK(h, hipMemcpyAsync(h->d_patch.p, h->h_stage, total, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(h->d_patch.p, h->h_stage, total, hipMemcpyHostToDevice, h->wstream));
   HIPCHK(h, launch_patch((const PatchEnt*)h->d_patch.p, (uint32_t)pl.ents.size(),
-                         (const uint32_t*)((uint8_t*)h->d_patch.p + eb), h->stream));
+                         (const uint32_t*)((uint8_t*)h->d_patch.p + eb), h->wstream));
   if (!h->patch_ev) HIPCHK(h, hipEventCreateWithFlags(&h->patch_ev, hipEventDisableTiming));
-  HIPCHK(h, hipEventRecord(h->patch_ev, h->stream));
+  HIPCHK(h, hipEventRecord(h->patch_ev, h->wstream));
   pl.clear();
   return 0;
 }
@@ -555,15 +650,14 @@ int upload_pool(emqxgm* h, PatchList* pl) {
     h->fver_host.insert(h->fver_host.end(), r, r + VREC);
   }
   int rc = 0;
-  if ((rc = append_upload(h, h->d_pool, h->pool_uploaded, h->pool.data(), h->pool.size(), pl)) ||
-      (rc = append_upload(h, h->d_foff, h->foff_uploaded, h->foff_host.data(),
+  if ((rc = append_upload(h, h->m_pool, h->pool.data(), h->pool.size(), pl)) ||
+      (rc = append_upload(h, h->m_foff, h->foff_host.data(),
                           h->foff_host.size() * sizeof(uint64_t), pl)) ||
-      (rc = append_upload(h, h->d_fver, h->fver_uploaded, h->fver_host.data(),
-                          h->fver_host.size(), pl)))
+      (rc = append_upload(h, h->m_fver, h->fver_host.data(), h->fver_host.size(), pl)))
     return rc;
-  h->ix.fbytes = (const uint8_t*)h->d_pool.p;
-  h->ix.foff = (const uint64_t*)h->d_foff.p;
-  h->ix.fver = (const uint4*)h->d_fver.p;
+  h->ix.fbytes = (const uint8_t*)h->m_pool.b.p;
+  h->ix.foff = (const uint64_t*)h->m_foff.b.p;
+  h->ix.fver = (const uint4*)h->m_fver.b.p;
   return 0;
 }
 
@@ -615,7 +709,7 @@ int fan_full(emqxgm* h) {
     m.rt_cap = m.rt_used + std::max<uint64_t>(16384, m.rt_used / 4);
     m.dl_cap = m.dl_used + std::max<uint64_t>(16384, m.dl_used / 4);
     if (m.rt_cap >= 0xFFFFFFFFull || m.dl_cap >= 0xFFFFFFFFull) {
-      h->err = "fan-out pools exceed 2^32 entries";
+      set_err(h, "fan-out pools exceed 2^32 entries");
       return -E2BIG;
     }
     rt.resize(m.rt_cap, 0u);
@@ -638,8 +732,7 @@ int fan_full(emqxgm* h) {
     ix.rt_dst = ix.dl_sub = nullptr;
   }
   ix.fan_nf = (uint32_t)m.cap;
-  free_bufs(h->fan_tab_bufs);
-  h->fan_tab_bufs.swap(nb);
+  h->o_fan = std::make_shared<DevOwner>(std::move(nb));  // the old tables live on with their epochs
   h->fan_changed.clear();
   h->fan_rebuild = false;
   m.valid = true;
@@ -685,6 +778,7 @@ int fan_commit(emqxgm* h) {
 
 void commit_stats(emqxgm* h, double ms, bool delta) {
   const TrieModel& m = h->tm;
+  std::lock_guard<std::mutex> g(h->stmu);
   h->st.epoch = h->epoch;
   h->st.n_filters = h->filters.size();
   h->st.n_trie_filters = m.n_trie;
@@ -738,7 +832,7 @@ int commit_full(emqxgm* h) {
       uint32_t* v = m.emap.get_or_insert(cur, tok, ins);
       if (ins) {
         if (m.parent.size() >= MAX_NODES) {
-          h->err = "trie exceeds 2^26-1 nodes";
+          set_err(h, "trie exceeds 2^26-1 nodes");
           return -E2BIG;
         }
         const uint32_t child = m.new_node(cur, tok);
@@ -890,26 +984,20 @@ int commit_full(emqxgm* h) {
   nx.trie_empty = (m.n_trie == 0);
   nx.plain_empty = (m.n_route_p == 0);
   nx.wild_empty = (m.n_route_w == 0);
-  free_bufs(h->ix_bufs);
-  h->ix_bufs.swap(nbufs);
-  for (Filter& f : h->filters) {
-    f.trie_committed = f.in_trie;
-    f.route_committed = f.route_refs > 0;
-  }
+  h->o_tab = std::make_shared<DevOwner>(std::move(nbufs));  // old tables live on with their epochs
   h->ix = nx;
   m.valid = true;
   h->tm = std::move(m);
-  h->changed.clear();
-  h->walk_spill = false;
+  h->changed.clear();  // every filter's committed flags follow at publish (commit_locked)
   return 0;
 }
 
 // Delta commit: apply the membership changes since the last commit to the host model and patch
 // the device tables in place (k_patch).  Returns 0 when applied, 1 when the delta does not fit
 // (too large, a table would pass its load bound, a node list would need a multi[] list, ...):
-// the caller then runs the full build, which also rebuilds the model.  Readers are stream-
-// ordered behind the patches, and a commit holds the handle lock, so no match sees a half-
-// applied delta.
+// the caller then runs the full build, which also rebuilds the model.  The patches are only
+// staged here; publish_epoch applies them on the GPU after every pass already enqueued and before
+// every later one, so no match sees a half-applied delta.
 int commit_delta(emqxgm* h) {
   TrieModel& m = h->tm;
   if (!m.valid || h->delta_mode == 0) return 1;
@@ -1105,7 +1193,7 @@ int commit_delta(emqxgm* h) {
   fv_words.erase(std::unique(fv_words.begin(), fv_words.end()), fv_words.end());
   for (uint32_t w : fv_words) pl.add(m.d_fv + w, &m.fvbits[w], 1);
   int rc = 0;
-  if ((rc = upload_pool(h, &pl)) || (rc = fan_commit(h)) || (rc = patch_flush(h))) return rc;
+  if ((rc = upload_pool(h, &pl)) || (rc = fan_commit(h))) return rc;
 
   DevIndex& ix = h->ix;
   const uint32_t root_p = m.pchild[0];
@@ -1119,60 +1207,144 @@ int commit_delta(emqxgm* h) {
   ix.trie_empty = (m.n_trie == 0);
   ix.plain_empty = (m.n_route_p == 0);
   ix.wild_empty = (m.n_route_w == 0);
-  for (uint32_t id : ch) {
-    Filter& f = h->filters[id];
-    f.trie_committed = f.in_trie;
-    f.route_committed = f.route_refs > 0;
-  }
-  ch.clear();
-  m.valid = true;
+  m.valid = true;  // h->changed: their committed flags follow at publish (commit_locked)
   return 0;
 }
 
-// Make the pending registry the committed index: a delta commit when it fits, else a full build.
-int drain_pipes(emqxgm* h);
+// The reader contexts whose passes a writer orders its patches behind.
+template <class F>
+void for_each_reader(emqxgm* h, F f) {
+  f(h->sync);
+  for (auto& p : h->pipes) f(p.c);
+  for (auto& p : h->hpipes) f(p.c);
+}
 
+// Publishes the writer's working index as the next epoch (under emu).  A delta commit's patches
+// rewrite tables that passes enqueued on the current epoch may still read: the writer stream
+// first waits for each reader stream's last pass (GPU-side, the host does not block), then runs
+// the patch upload and k_patch, and the new epoch's `ready` event follows them -- every later
+// pass waits on it.  A full build's tables are new, so it waits for nobody.
+int publish_epoch(emqxgm* h, bool delta) {
+  auto E = std::make_shared<Epoch>();
+  E->id = h->epoch + 1;
+  E->ix = h->ix;
+  E->owners = {h->o_tab, h->o_fan, h->m_pool.o, h->m_foff.o, h->m_fver.o};
+  HIPCHK(h, hipEventCreateWithFlags(&E->ready, hipEventDisableTiming));
+  std::lock_guard<std::mutex> g(h->emu);
+  if (delta && h->cur) E->walk_spill.store(h->cur->walk_spill.load());
+  if (!h->patches.ents.empty()) {
+    int rc = 0;
+    for_each_reader(h, [&](PassCtx& c) {
+      if (!rc && c.done_rec && hipStreamWaitEvent(h->wstream, c.done, 0) != hipSuccess)
+        rc = fail(h, hipErrorUnknown, "hipStreamWaitEvent(writer, reader pass)");
+    });
+    if (rc || (rc = patch_flush(h))) return rc;
+  }
+  HIPCHK(h, hipEventRecord(E->ready, h->wstream));
+  if (h->cur) h->graveyard.push_back(std::move(h->cur));
+  h->cur = std::move(E);
+  h->epoch += 1;
+  return 0;
+}
+
+// Frees retired epochs no reader holds any more (writers only: readers never free).
+void sweep_graveyard(emqxgm* h) {
+  std::vector<EpochP> dead;
+  {
+    std::lock_guard<std::mutex> g(h->emu);
+    auto& gy = h->graveyard;
+    for (size_t i = 0; i < gy.size();) {
+      if (gy[i].use_count() == 1) {
+        dead.push_back(std::move(gy[i]));
+        gy[i] = std::move(gy.back());
+        gy.pop_back();
+      } else {
+        ++i;
+      }
+    }
+  }
+  // dead epochs (and the device buffers only they owned) are freed here, outside emu
+}
+
+// Make the pending registry the committed index: a delta commit when it fits, else a full build.
+// Runs under wmu only: readers keep matching against the current epoch while a full build runs.
 int commit_locked(emqxgm* h) {
-  // passes in flight read the committed index: let them finish before it changes
-  if (int rc = drain_pipes(h)) return rc;
   const auto t0 = std::chrono::steady_clock::now();
+  sweep_graveyard(h);
   h->patches.clear();
   int rc = patch_wait(h);  // the previous commit's patches are applied before buffers change
   if (rc) return rc;
   rc = commit_delta(h);
   const bool delta = rc == 0;
-  if (rc > 0) rc = commit_full(h);
-  if (rc) return rc;
-  h->epoch += 1;
+  if (rc > 0) {
+    h->patches.clear();  // a declined delta stages nothing
+    rc = commit_full(h);
+  }
+  if (rc || (rc = publish_epoch(h, delta))) return rc;
+  {
+    // the registry's committed flags (trie_member, the next delta) follow the published epoch
+    std::unique_lock<std::shared_mutex> g(h->pmu);
+    auto flip = [](Filter& f) {
+      f.trie_committed = f.in_trie;
+      f.route_committed = f.route_refs > 0;
+    };
+    if (delta) {
+      for (uint32_t id : h->changed) flip(h->filters[id]);
+    } else {
+      for (Filter& f : h->filters) flip(f);
+    }
+  }
+  h->changed.clear();
   h->dirty = false;
   commit_stats(h, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
                delta);
   return 0;
 }
 
-int dev_alloc(emqxgm* h, void** p, size_t bytes) {
+int dev_alloc(emqxgm* h, PassCtx& c, void** p, size_t bytes) {
   HIPCHK(h, hipMalloc(p, std::max<size_t>(bytes, 16)));
   DevBuf b;
   b.p = *p;
   b.bytes = bytes;
-  h->sc_bufs.push_back(b);
+  c.bufs.push_back(b);
   return 0;
 }
 
-// (Re)allocate batch scratch for n topics, `words` words and `pairs` staged pairs.
-int ensure_scratch(emqxgm* h, uint32_t n, uint64_t words, uint32_t pairs) {
-  Scratch& s = h->sc;
+// A reader context's stream and events (created on first use).
+int ctx_init(emqxgm* h, PassCtx& c) {
+  if (c.stream) return 0;
+  HIPCHK(h, hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+  for (auto& e : c.ev) HIPCHK(h, hipEventCreate(&e));
+  HIPCHK(h, hipEventCreateWithFlags(&c.done, hipEventDisableTiming));
+  return 0;
+}
+
+void ctx_free(PassCtx& c) {
+  if (c.stream) {
+    (void)hipStreamSynchronize(c.stream);
+    (void)hipStreamDestroy(c.stream);
+  }
+  for (auto& e : c.ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c.done) (void)hipEventDestroy(c.done);
+  free_bufs(c.bufs);
+  if (c.sc.ctl_host) (void)hipHostFree(c.sc.ctl_host);
+  c = PassCtx();
+}
+
+// (Re)allocate a context's batch scratch for n topics, `words` words and `pairs` staged pairs.
+int ensure_scratch(emqxgm* h, PassCtx& c, uint32_t n, uint64_t words, uint32_t pairs) {
+  Scratch& s = c.sc;
   const uint32_t spill_need = std::max<uint32_t>(h->spill_want, WALK_SPILL_MIN);
   if (n <= s.n_cap && words <= s.w_cap && pairs <= s.p_cap && spill_need <= s.spill_items &&
-      s.spill_lanes == h->geom.lanes &&
-      s.ctl)
+      s.spill_lanes == h->geom.lanes && s.ctl)
     return 0;
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipStreamSynchronize(c.stream));
   const uint32_t ncap = std::max(n, s.n_cap);
   const uint64_t wcap = std::max(words, s.w_cap);
   const uint32_t pcap = std::max(pairs, s.p_cap);
   const uint32_t scap = std::max(spill_need, s.spill_items);
-  free_bufs(h->sc_bufs);
+  free_bufs(c.bufs);
   if (s.ctl_host) {
     (void)hipHostFree(s.ctl_host);
     s.ctl_host = nullptr;
@@ -1180,23 +1352,23 @@ int ensure_scratch(emqxgm* h, uint32_t n, uint64_t words, uint32_t pairs) {
   s = Scratch();
   int rc = 0;
   const uint32_t stw = scan_tmp_words(ncap);
-  if ((rc = dev_alloc(h, (void**)&s.nw, (size_t)ncap * 4)) ||
-      (rc = dev_alloc(h, (void**)&s.wh, (size_t)wcap * 8)) ||
-      (rc = dev_alloc(h, (void**)&s.rec, (size_t)ncap * 16 * REC_U4)) ||
-      (rc = dev_alloc(h, (void**)&s.cnt, (size_t)ncap * 4)) ||
-      (rc = dev_alloc(h, (void**)&s.row, (size_t)(ncap + 1) * 4)) ||
-      (rc = dev_alloc(h, (void**)&s.row2, (size_t)(ncap + 1) * 4)) ||
-      (rc = dev_alloc(h, (void**)&s.rej, (size_t)ncap * 4)) ||
-      (rc = dev_alloc(h, (void**)&s.exact_id, (size_t)ncap * 4)) ||
-      (rc = dev_alloc(h, (void**)&s.stg, (size_t)pcap * 16)) ||
-      (rc = dev_alloc(h, (void**)&s.out, (size_t)pcap * 4)) ||
-      (rc = dev_alloc(h, (void**)&s.out2, (size_t)pcap * 4)) ||
-      (rc = dev_alloc(h, (void**)&s.scan_tmp, (size_t)stw * 4)) ||
-      (rc = dev_alloc(h, (void**)&s.ctl, CTL_N * 4)) ||
-      (rc = dev_alloc(h, (void**)&s.census,
+  if ((rc = dev_alloc(h, c, (void**)&s.nw, (size_t)ncap * 4)) ||
+      (rc = dev_alloc(h, c, (void**)&s.wh, (size_t)wcap * 8)) ||
+      (rc = dev_alloc(h, c, (void**)&s.rec, (size_t)ncap * 16 * REC_U4)) ||
+      (rc = dev_alloc(h, c, (void**)&s.cnt, (size_t)ncap * 4)) ||
+      (rc = dev_alloc(h, c, (void**)&s.row, (size_t)(ncap + 1) * 4)) ||
+      (rc = dev_alloc(h, c, (void**)&s.row2, (size_t)(ncap + 1) * 4)) ||
+      (rc = dev_alloc(h, c, (void**)&s.rej, (size_t)ncap * 4)) ||
+      (rc = dev_alloc(h, c, (void**)&s.exact_id, (size_t)ncap * 4)) ||
+      (rc = dev_alloc(h, c, (void**)&s.stg, (size_t)pcap * 16)) ||
+      (rc = dev_alloc(h, c, (void**)&s.out, (size_t)pcap * 4)) ||
+      (rc = dev_alloc(h, c, (void**)&s.out2, (size_t)pcap * 4)) ||
+      (rc = dev_alloc(h, c, (void**)&s.scan_tmp, (size_t)stw * 4)) ||
+      (rc = dev_alloc(h, c, (void**)&s.ctl, CTL_N * 4)) ||
+      (rc = dev_alloc(h, c, (void**)&s.census,
                       (CENSUS_N + 3 * (h->geom.lanes / 64)) * sizeof(unsigned long long))) ||
-      (rc = dev_alloc(h, (void**)&s.spill, (size_t)scap * h->geom.lanes * sizeof(uint2))) ||
-      (rc = dev_alloc(h, (void**)&s.rlist, (size_t)h->reject_cap * 8)))
+      (rc = dev_alloc(h, c, (void**)&s.spill, (size_t)scap * h->geom.lanes * sizeof(uint2))) ||
+      (rc = dev_alloc(h, c, (void**)&s.rlist, (size_t)h->reject_cap * 8)))
     return rc;
   s.r_cap = h->reject_cap;
   HIPCHK(h, hipHostMalloc((void**)&s.ctl_host, CTL_N * 4, hipHostMallocDefault));
@@ -1210,126 +1382,153 @@ int ensure_scratch(emqxgm* h, uint32_t n, uint64_t words, uint32_t pairs) {
   return 0;
 }
 
-// One device pass over n topics already in HBM.  Leaves results in h->sc (row, out, exact_id)
-// and the total pair count in *pairs.
+// One device pass over n topics already in HBM.  Leaves results in the context's scratch (row,
+// out, exact_id) and the total pair count in *pairs.
 //
 // Production order: tokenise -> walk -> verify (flags rejects, fixes counts) -> scan -> scatter.
 // If a batch rejected more pairs than k_scatter adjusts in-line (a weak-hash test config or an
 // adversarial index), the pass is redone on the legacy path: scan -> verify+scatter -> compaction.
 //
-// The pass is three steps so that a pipelined caller (emqxgm_match_device_submit/_wait) can
-// enqueue one batch while an earlier one still runs on another stream: pass_prepare (scratch),
-// pass_enqueue (every launch, then the control words to the host, no synchronisation),
-// pass_check (after the stream has drained: 0 done, 1 redo, < 0 error) and pass_finish.
+// The pass is split so that a pipelined caller (emqxgm_match_device_submit/_wait,
+// emqxgm_match_batch_submit/_wait) can enqueue one batch while an earlier one still runs on
+// another stream: pass_prepare (scratch), pass_submit (takes the current epoch and enqueues every
+// launch, then the control words to the host, no synchronisation), pass_check (after the stream
+// has drained: 0 done, 1 redo, < 0 error) and pass_finish.
 
 // Scratch for n topics; returns 0, or 2 when n == 0 (then the empty result is already set).
-int pass_prepare(emqxgm* h, uint32_t n, uint64_t bytes_len) {
+int pass_prepare(emqxgm* h, PassCtx& c, uint32_t n, uint64_t bytes_len) {
   const uint64_t words = bytes_len + n + 1;  // token array: level k of topic t at off[t] + t + k
   if (words > 0xFFFFFFFFull) {
-    h->err = "batch too large: topic bytes + topics must stay below 2^32";
+    set_err(h, "batch too large: topic bytes + topics must stay below 2^32");
     return -E2BIG;
   }
-  uint32_t want_pairs = std::max<uint32_t>(h->sc.p_cap, std::max<uint32_t>(1u << 20, n * 4u));
-  int rc = ensure_scratch(h, std::max<uint32_t>(n, 1), words, want_pairs);
+  uint32_t want_pairs = std::max<uint32_t>(c.sc.p_cap, std::max<uint32_t>(1u << 20, n * 4u));
+  int rc = ensure_scratch(h, c, std::max<uint32_t>(n, 1), words, want_pairs);
   if (rc) return rc;
   if (n == 0) {
-    HIPCHK(h, hipMemsetAsync(h->sc.row, 0, 4, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemsetAsync(c.sc.row, 0, 4, c.stream));
+    HIPCHK(h, hipStreamSynchronize(c.stream));
     return 2;
   }
   return 0;
 }
 
-int pass_enqueue(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_t n,
-                 bool legacy, bool census) {
-  Scratch& s = h->sc;
-  hipStream_t st = h->stream;
-  if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[0], st));
+// Every launch of one pass against epoch E on the context's stream (caller holds emu).
+int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
+                 const uint32_t* d_off, uint32_t n, bool legacy, bool census) {
+  Scratch& s = c.sc;
+  hipStream_t st = c.stream;
+  DevIndex ix = E.ix;
+  ix.leafp_mask = h->leafp_mask;
+  HIPCHK(h, hipStreamWaitEvent(st, E.ready, 0));  // the epoch's uploads / patches have landed
+  if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[0], st));
   HIPCHK(h, hipMemsetAsync(s.ctl, 0, CTL_N * 4, st));
   if (census)
     HIPCHK(h, hipMemsetAsync(s.census, 0,
                              (CENSUS_N + 3 * (h->geom.lanes / 64)) * sizeof(unsigned long long),
                              st));
-  HIPCHK(h, launch_tok(d_bytes, d_off, n, h->ix, s, st));
-  if (h->ix.trie_empty) {
+  HIPCHK(h, launch_tok(d_bytes, d_off, n, ix, s, st));
+  if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[1], st));
+  if (ix.trie_empty) {
     HIPCHK(h, hipMemsetAsync(s.row, 0, (size_t)(n + 1) * 4, st));
   } else {
     // per-topic reject counts: only the verification passes write (and then read) them
-    if (h->ix.needs_verify || legacy) HIPCHK(h, hipMemsetAsync(s.rej, 0, (size_t)n * 4, st));
-    if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[1], st));
-    HIPCHK(h, launch_walk(h->ix, s, n, h->geom, st, census ? s.census : nullptr, h->walk_spill));
-    if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[2], st));
+    if (ix.needs_verify || legacy) HIPCHK(h, hipMemsetAsync(s.rej, 0, (size_t)n * 4, st));
+    HIPCHK(h, launch_walk(ix, s, n, h->geom, st, census ? s.census : nullptr,
+                          E.walk_spill.load(std::memory_order_relaxed)));
+    if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[2], st));
     if (!legacy) {
       // pairs of filters made of short (exact) tokens need no byte check (gm_verify.inc)
-      if (h->ix.needs_verify) HIPCHK(h, launch_verify(d_bytes, d_off, h->ix, s, n, h->geom, st));
+      if (ix.needs_verify) HIPCHK(h, launch_verify(d_bytes, d_off, ix, s, n, h->geom, st));
       HIPCHK(h, launch_scan(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, st));
       HIPCHK(h, launch_scatter(s, n, h->geom, st));
     } else {
       HIPCHK(h, launch_scan(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, st));
-      HIPCHK(h, launch_verify_scatter(d_bytes, d_off, h->ix, s, n, st));
+      HIPCHK(h, launch_verify_scatter(d_bytes, d_off, ix, s, n, st));
     }
   }
-  if (h->profiling) HIPCHK(h, hipEventRecord(h->ev[3], st));
+  if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[3], st));
   HIPCHK(h, hipMemcpyAsync(s.ctl_host, s.ctl, CTL_N * 4, hipMemcpyDeviceToHost, st));
   return 0;
 }
 
+// Marks the end of the table reads a context enqueued (caller holds emu): a later delta commit
+// orders its patches behind this point.
+int mark_done(emqxgm* h, PassCtx& c) {
+  HIPCHK(h, hipEventRecord(c.done, c.stream));
+  c.done_rec = true;
+  return 0;
+}
+
+// Takes the current epoch and enqueues one pass on it.  emu is held for the enqueue only (a few
+// asynchronous launches); the pass then runs while writers build, patch and swap.
+int pass_submit(emqxgm* h, PassCtx& c, const uint8_t* d_bytes, const uint32_t* d_off,
+                uint32_t n, bool legacy, bool census) {
+  std::lock_guard<std::mutex> g(h->emu);
+  c.epoch = h->cur;
+  int rc = pass_enqueue(h, c, *c.epoch, d_bytes, d_off, n, legacy, census);
+  return rc ? rc : mark_done(h, c);
+}
+
 // After the pass's stream drained: 0 = done, 1 = redo (scratch grown / walk variant or path
 // switched), < 0 = error.
-int pass_check(emqxgm* h, uint32_t n, uint64_t bytes_len, int attempt, bool& legacy) {
-  Scratch& s = h->sc;
+int pass_check(emqxgm* h, PassCtx& c, uint32_t n, uint64_t bytes_len, int attempt, bool& legacy) {
+  Scratch& s = c.sc;
+  Epoch& E = *c.epoch;
   const uint64_t words = bytes_len + n + 1;
   if (attempt > 6) {
-    h->err = "match pass did not converge";
+    set_err(h, "match pass did not converge");
     return -ENOMEM;
   }
   const uint32_t top = s.ctl_host[CTL_PAIR_TOP];
+  auto rerun = [&]() {
+    std::lock_guard<std::mutex> g(h->stmu);
+    h->st.reruns += 1;
+  };
   if (top > s.p_cap) {
     // staging overflow: nothing beyond the capacity was written; grow and redo the pass
-    h->st.reruns += 1;
+    rerun();
     const uint64_t np = std::min<uint64_t>(0xF0000000ull, (uint64_t)top * 2 + (1u << 20));
-    int rc = ensure_scratch(h, n, words, (uint32_t)np);
+    int rc = ensure_scratch(h, c, n, words, (uint32_t)np);
     return rc ? rc : 1;
   }
-  if (s.ctl_host[CTL_ERR] && !h->walk_spill) {
+  if (s.ctl_host[CTL_ERR] && !E.walk_spill.load()) {
     // a walk lane's item stack outgrew LDS: redo with the spilling variant (kept for this
     // committed index)
-    h->st.reruns += 1;
-    h->walk_spill = true;
+    rerun();
+    E.walk_spill.store(true);
     return 1;
   }
   if (s.ctl_host[CTL_ERR]) {
     // a walk lane's item stack outgrew the spill: grow it to the proven bound and redo
-    const uint32_t bound = walk_spill_bound(h->ix.max_depth);
+    const uint32_t bound = walk_spill_bound(E.ix.max_depth);
     if (s.spill_items >= bound) {
-      h->err = "walk item stack exceeded its bound";
+      set_err(h, "walk item stack exceeded its bound");
       return -EIO;
     }
-    h->st.reruns += 1;
+    rerun();
     h->spill_want = bound;
-    int rc = ensure_scratch(h, n, words, s.p_cap);
+    int rc = ensure_scratch(h, c, n, words, s.p_cap);
     return rc ? rc : 1;
   }
   if (!legacy && s.ctl_host[CTL_LEGACY]) {
-    h->st.reruns += 1;
+    rerun();
     legacy = true;
     return 1;
   }
   return 0;
 }
 
-int pass_finish(emqxgm* h, uint32_t n, bool legacy, uint32_t* pairs, uint64_t* census) {
-  Scratch& s = h->sc;
-  hipStream_t st = h->stream;
-  if (h->profiling) {
-    float a = 0, b = 0;
-    if (!h->ix.trie_empty) {
-      HIPCHK(h, hipEventElapsedTime(&a, h->ev[1], h->ev[2]));
-      h->st.walk_ms += a;
-      h->st.walk_launches += 1;
-    }
-    HIPCHK(h, hipEventElapsedTime(&b, h->ev[0], h->ev[3]));
-    h->st.total_ms += b;
+int pass_finish(emqxgm* h, PassCtx& c, uint32_t n, bool legacy, uint32_t* pairs, uint64_t* census) {
+  Scratch& s = c.sc;
+  hipStream_t st = c.stream;
+  float tok = 0, walk = 0, all = 0;
+  const bool timed = h->profiling;
+  const bool walked = !c.epoch->ix.trie_empty;
+  if (timed) {
+    HIPCHK(h, hipEventElapsedTime(&tok, c.ev[0], c.ev[1]));
+    if (walked) HIPCHK(h, hipEventElapsedTime(&walk, c.ev[1], c.ev[2]));
+    HIPCHK(h, hipEventElapsedTime(&all, c.ev[0], c.ev[3]));
   }
   if (legacy && s.ctl_host[CTL_ANY_REJ]) {
     HIPCHK(h, launch_fixup(s, n, st));
@@ -1338,9 +1537,24 @@ int pass_finish(emqxgm* h, uint32_t n, bool legacy, uint32_t* pairs, uint64_t* c
     std::swap(s.row, s.row2);
     std::swap(s.out, s.out2);
   }
-  if (s.ctl_host[CTL_ANY_REJ]) h->st.rejected_pairs += legacy ? 0 : s.ctl_host[CTL_NREJ];
-  if (legacy) h->st.legacy_batches += 1;
   *pairs = s.ctl_host[CTL_TOTAL];
+  {
+    std::lock_guard<std::mutex> g(h->stmu);
+    if (timed) {
+      h->st.tok_ms += tok;
+      h->st.tok_launches += 1;
+      if (walked) {
+        h->st.walk_ms += walk;
+        h->st.walk_launches += 1;
+      }
+      h->st.total_ms += all;
+    }
+    if (s.ctl_host[CTL_ANY_REJ]) h->st.rejected_pairs += legacy ? 0 : s.ctl_host[CTL_NREJ];
+    if (legacy) h->st.legacy_batches += 1;
+    h->st.batches += 1;
+    h->st.topics += n;
+    h->st.pairs += *pairs;
+  }
   if (census) {
     if (const char* wf = getenv("EMQXGM_WAVE_TIMES")) {  // diagnostic: per-wave timeline
       std::vector<unsigned long long> wt(3 * (h->geom.lanes / 64));
@@ -1350,28 +1564,27 @@ int pass_finish(emqxgm* h, uint32_t n, bool legacy, uint32_t* pairs, uint64_t* c
         fclose(fp);
       }
     }
-    unsigned long long c[CENSUS_N] = {0, 0, 0, 0};
-    HIPCHK(h, hipMemcpy(c, s.census, sizeof c, hipMemcpyDeviceToHost));
-    census[0] = c[0];
-    census[1] = c[1];
+    unsigned long long cv[CENSUS_N] = {0, 0, 0, 0};
+    HIPCHK(h, hipMemcpy(cv, s.census, sizeof cv, hipMemcpyDeviceToHost));
+    census[0] = cv[0];
+    census[1] = cv[1];
     census[2] = *pairs;
     std::vector<uint32_t> nw(n);
     HIPCHK(h, hipMemcpy(nw.data(), s.nw, (size_t)n * 4, hipMemcpyDeviceToHost));
     uint64_t nwords = 0;
     for (uint32_t v : nw) nwords += v;
     census[3] = nwords;
-    census[4] = c[2];
-    census[5] = c[3];
+    census[4] = cv[2];
+    census[5] = cv[3];
   }
-  h->st.batches += 1;
-  h->st.topics += n;
-  h->st.pairs += *pairs;
   return 0;
 }
 
-int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_t n,
+// A whole synchronous pass on context c (redone until it converges).  c.epoch is the epoch the
+// result belongs to; the caller drops it when done with the result.
+int run_device(emqxgm* h, PassCtx& c, const uint8_t* d_bytes, const uint32_t* d_off, uint32_t n,
                uint64_t bytes_len, uint32_t* pairs, uint64_t* census = nullptr) {
-  int rc = pass_prepare(h, n, bytes_len);
+  int rc = pass_prepare(h, c, n, bytes_len);
   if (rc == 2) {
     *pairs = 0;
     return 0;
@@ -1379,13 +1592,13 @@ int run_device(emqxgm* h, const uint8_t* d_bytes, const uint32_t* d_off, uint32_
   if (rc) return rc;
   bool legacy = false;
   for (int attempt = 0;; ++attempt) {
-    if ((rc = pass_enqueue(h, d_bytes, d_off, n, legacy, census != nullptr))) return rc;
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    rc = pass_check(h, n, bytes_len, attempt, legacy);
+    if ((rc = pass_submit(h, c, d_bytes, d_off, n, legacy, census != nullptr))) return rc;
+    HIPCHK(h, hipStreamSynchronize(c.stream));
+    rc = pass_check(h, c, n, bytes_len, attempt, legacy);
     if (rc < 0) return rc;
     if (rc == 0) break;
   }
-  return pass_finish(h, n, legacy, pairs, census);
+  return pass_finish(h, c, n, legacy, pairs, census);
 }
 
 int fan_alloc(emqxgm* h, std::vector<DevBuf>& keep, uint32_t** p, size_t words) {
@@ -1397,12 +1610,16 @@ int fan_alloc(emqxgm* h, std::vector<DevBuf>& keep, uint32_t** p, size_t words) 
   return 0;
 }
 
-// Publish fan-out over the match result of the last run_device pass (n topics): counts, two
-// scans, then (outputs grown to the totals) the fill.  Leaves the results in h->fs.
+// Publish fan-out over the match result of the last run_device pass on the sync context (n
+// topics): counts, two scans, then (outputs grown to the totals) the fill.  Leaves the results in
+// h->fs.  The fan-out tables must be those of the epoch the match ran against: emu is held from
+// the count pass to the fill pass (one short host wait in between), and 1 is returned when a
+// commit published another epoch since the match (the caller redoes both).
 int run_fanout(emqxgm* h, uint32_t n, uint32_t* n_routes, uint32_t* n_deliv) {
+  PassCtx& c = h->sync;
   FanScratch& f = h->fs;
-  Scratch& s = h->sc;
-  hipStream_t st = h->stream;
+  Scratch& s = c.sc;
+  hipStream_t st = c.stream;
   int rc = 0;
   if (n > f.n_cap || !f.cr) {
     HIPCHK(h, hipStreamSynchronize(st));
@@ -1418,7 +1635,10 @@ int run_fanout(emqxgm* h, uint32_t n, uint32_t* n_routes, uint32_t* n_deliv) {
     *n_routes = *n_deliv = 0;
     return 0;
   }
-  HIPCHK(h, launch_fanout(h->ix, s, f, n, false, st));
+  std::lock_guard<std::mutex> g(h->emu);
+  if (h->cur != c.epoch) return 1;
+  const DevIndex& ix = c.epoch->ix;
+  HIPCHK(h, launch_fanout(ix, s, f, n, false, st));
   HIPCHK(h, launch_scan(f.cr, f.rp, n, s.scan_tmp, s.ctl + CTL_FAN_R, st));
   HIPCHK(h, launch_scan(f.cd, f.dp, n, s.scan_tmp, s.ctl + CTL_FAN_D, st));
   HIPCHK(h, hipMemcpyAsync(s.ctl_host + CTL_FAN_R, s.ctl + CTL_FAN_R, 8, hipMemcpyDeviceToHost, st));
@@ -1435,7 +1655,8 @@ int run_fanout(emqxgm* h, uint32_t n, uint32_t* n_routes, uint32_t* n_deliv) {
     f.r_cap = rc_;
     f.d_cap = dc;
   }
-  HIPCHK(h, launch_fanout(h->ix, s, f, n, true, st));
+  HIPCHK(h, launch_fanout(ix, s, f, n, true, st));
+  if ((rc = mark_done(h, c))) return rc;
   *n_routes = nr;
   *n_deliv = nd;
   return 0;
@@ -1472,6 +1693,152 @@ int ensure_input(emqxgm* h, uint64_t bytes, uint64_t offs) {
   return 0;
 }
 
+// Completes an in-flight device pipe (stream drained, checked, redone synchronously if it has
+// to be).
+int pipe_complete(emqxgm* h, emqxgm::Pipe& p) {
+  if (p.state != 1) return 0;
+  HIPCHK(h, hipStreamSynchronize(p.c.stream));
+  bool legacy = false;
+  int rc = pass_check(h, p.c, p.n, p.bytes_len, 0, legacy);
+  if (rc < 0) {
+    p.state = 0;
+    p.c.epoch.reset();
+    return rc;
+  }
+  rc = rc == 0 ? pass_finish(h, p.c, p.n, false, &p.pairs, nullptr)
+               : run_device(h, p.c, p.d_bytes, p.d_off, p.n, p.bytes_len, &p.pairs);
+  p.state = rc ? 0 : 2;
+  p.c.epoch.reset();
+  return rc;
+}
+
+int drain_pipes(emqxgm* h) {
+  for (auto& p : h->pipes)
+    if (int rc = pipe_complete(h, p)) return rc;
+  return 0;
+}
+
+// Pinned host buffer a kernel can write (its device-side address in *dev).
+int host_buf(emqxgm* h, uint32_t** p, uint64_t entries) {
+  HIPCHK(h, hipHostMalloc((void**)p, std::max<uint64_t>(entries, 16) * 4,
+                          hipHostMallocMapped | hipHostMallocPortable));
+  return 0;
+}
+
+int host_pipe_reserve(emqxgm* h, emqxgm::HostPipe& p, uint64_t n, uint64_t bytes, uint64_t fid) {
+  if (bytes > p.bytes_cap) {
+    if (p.d_bytes) (void)hipFree(p.d_bytes);
+    p.d_bytes = nullptr;
+    p.bytes_cap = 0;
+    const uint64_t cap = std::max<uint64_t>(bytes + bytes / 4, 1 << 20);
+    HIPCHK(h, hipMalloc((void**)&p.d_bytes, cap));
+    p.bytes_cap = cap;
+  }
+  if (n + 1 > p.off_cap) {
+    if (p.d_off) (void)hipFree(p.d_off);
+    p.d_off = nullptr;
+    p.off_cap = 0;
+    const uint64_t cap = std::max<uint64_t>(n + 1 + n / 4, 1 << 16);
+    HIPCHK(h, hipMalloc((void**)&p.d_off, cap * 4));
+    p.off_cap = cap;
+  }
+  if (n + 1 > p.row_cap) {
+    if (p.h_row) (void)hipHostFree(p.h_row);
+    if (p.h_exact) (void)hipHostFree(p.h_exact);
+    p.h_row = p.h_exact = nullptr;
+    p.row_cap = 0;
+    const uint64_t cap = std::max<uint64_t>(n + 1 + n / 4, 1 << 16);
+    int rc = 0;
+    if ((rc = host_buf(h, &p.h_row, cap)) || (rc = host_buf(h, &p.h_exact, cap))) return rc;
+    p.row_cap = cap;
+  }
+  if (fid > p.fid_cap) {
+    if (p.h_fid) (void)hipHostFree(p.h_fid);
+    p.h_fid = nullptr;
+    p.fid_cap = 0;
+    int rc = host_buf(h, &p.h_fid, fid);
+    if (rc) return rc;
+    p.fid_cap = fid;
+  }
+  return 0;
+}
+
+// The pass's results into the host pipe's pinned buffers, enqueued on its stream: by a copy
+// kernel writing host memory over PCIe (the pair count is read on the device, so nothing waits
+// for the host), or by hipMemcpyAsync for the fixed-size arrays (the filter ids then follow in
+// _wait, once their count is known).
+int host_pipe_copy_out(emqxgm* h, emqxgm::HostPipe& p) {
+  const Scratch& s = p.c.sc;
+  void *dr = nullptr, *de = nullptr, *df = nullptr;
+  HIPCHK(h, hipHostGetDevicePointer(&dr, p.h_row, 0));
+  HIPCHK(h, hipHostGetDevicePointer(&de, p.h_exact, 0));
+  HIPCHK(h, hipHostGetDevicePointer(&df, p.h_fid, 0));
+  if (h->host_out_mode == 1) {
+    CopyOut a{s.row, (uint32_t*)dr, p.n + 1, nullptr, p.n + 1};
+    CopyOut b{s.exact_id, (uint32_t*)de, p.n, nullptr, p.n};
+    CopyOut f{s.out, (uint32_t*)df, 0, s.ctl + CTL_TOTAL, (uint32_t)std::min<uint64_t>(p.fid_cap, s.p_cap)};
+    HIPCHK(h, launch_copy_out(a, b, f, p.c.stream));
+  } else {
+    HIPCHK(h, hipMemcpyAsync(p.h_row, s.row, ((size_t)p.n + 1) * 4, hipMemcpyDeviceToHost, p.c.stream));
+    HIPCHK(h, hipMemcpyAsync(p.h_exact, s.exact_id, (size_t)p.n * 4, hipMemcpyDeviceToHost, p.c.stream));
+  }
+  return 0;
+}
+
+// Completes an in-flight host pipe: checks the pass (redoing it synchronously when it has to be)
+// and makes sure every result array is in its pinned buffer.
+int host_pipe_complete(emqxgm* h, emqxgm::HostPipe& p) {
+  if (p.state != 1) return 0;
+  HIPCHK(h, hipStreamSynchronize(p.c.stream));
+  bool legacy = false;
+  int rc = pass_check(h, p.c, p.n, p.bytes_len, 0, legacy);
+  bool copied = h->host_out_mode == 1;
+  if (rc == 0) {
+    rc = pass_finish(h, p.c, p.n, false, &p.pairs, nullptr);
+  } else if (rc == 1) {
+    rc = run_device(h, p.c, p.d_bytes, p.d_off, p.n, p.bytes_len, &p.pairs);
+    copied = false;
+  }
+  p.c.epoch.reset();
+  if (rc < 0) {
+    p.state = 0;
+    return rc;
+  }
+  if (!copied || p.pairs > p.fid_cap) {
+    const Scratch& s = p.c.sc;
+    if ((rc = host_pipe_reserve(h, p, p.n, 0, p.pairs))) {
+      p.state = 0;
+      return rc;
+    }
+    HIPCHK(h, hipMemcpyAsync(p.h_row, s.row, ((size_t)p.n + 1) * 4, hipMemcpyDeviceToHost, p.c.stream));
+    HIPCHK(h, hipMemcpyAsync(p.h_exact, s.exact_id, (size_t)p.n * 4, hipMemcpyDeviceToHost, p.c.stream));
+  }
+  if (!copied || p.pairs > p.fid_cap || h->host_out_mode != 1) {
+    if (p.pairs)
+      HIPCHK(h, hipMemcpyAsync(p.h_fid, p.c.sc.out, (size_t)p.pairs * 4, hipMemcpyDeviceToHost,
+                               p.c.stream));
+    HIPCHK(h, hipStreamSynchronize(p.c.stream));
+  }
+  p.state = 2;
+  return 0;
+}
+
+void host_pipe_free(emqxgm::HostPipe& p) {
+  ctx_free(p.c);
+  if (p.d_bytes) (void)hipFree(p.d_bytes);
+  if (p.d_off) (void)hipFree(p.d_off);
+  for (uint32_t* q : {p.h_row, p.h_exact, p.h_fid})
+    if (q) (void)hipHostFree(q);
+  p = emqxgm::HostPipe();
+}
+
+// Writers hold wmu then pmu (exclusive) while they may grow the registry.
+struct WriterLock {
+  std::lock_guard<std::mutex> w;
+  std::unique_lock<std::shared_mutex> p;
+  explicit WriterLock(emqxgm* h) : w(h->wmu), p(h->pmu) {}
+};
+
 }  // namespace
 
 extern "C" {
@@ -1498,17 +1865,13 @@ int emqxgm_create(const emqxgm_cfg* cfg, emqxgm_t** out) {
     return -EIO;
   }
   if (hipSetDevice(h->cfg.device) != hipSuccess ||
-      hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete h;
+      hipStreamCreateWithFlags(&h->wstream, hipStreamNonBlocking) != hipSuccess ||
+      ctx_init(h, h->sync) != 0) {
+    emqxgm_destroy(h);
     return -EIO;
   }
-  for (auto& e : h->ev)
-    if (hipEventCreate(&e) != hipSuccess) {
-      delete h;
-      return -EIO;
-    }
   h->geom = walk_geometry(h->cfg.device, h->cfg.walk_wg_per_cu);
-  int rc = commit_locked(h);  // empty index
+  int rc = commit_locked(h);  // empty index: epoch 1
   if (rc) {
     emqxgm_destroy(h);
     return rc;
@@ -1520,38 +1883,29 @@ int emqxgm_create(const emqxgm_cfg* cfg, emqxgm_t** out) {
 void emqxgm_destroy(emqxgm_t* h) {
   if (!h) return;
   (void)hipSetDevice(h->cfg.device);
-  if (h->stream) (void)hipStreamSynchronize(h->stream);
-  for (auto& p : h->pipes) {
-    if (p.stream) {
-      (void)hipStreamSynchronize(p.stream);
-      (void)hipStreamDestroy(p.stream);
-    }
-    for (auto& e : p.ev)
-      if (e) (void)hipEventDestroy(e);
-    free_bufs(p.bufs);
-    if (p.sc.ctl_host) (void)hipHostFree(p.sc.ctl_host);
-  }
+  if (h->wstream) (void)hipStreamSynchronize(h->wstream);
+  for (auto& p : h->pipes) ctx_free(p.c);
+  for (auto& p : h->hpipes) host_pipe_free(p);
+  ctx_free(h->sync);
   for (auto* b : {&h->hp_row, &h->hp_fid, &h->hp_exact})
     if (b->p) (void)hipHostFree(b->p);
   if (h->d_row64) (void)hipFree(h->d_row64);
-  free_bufs(h->ix_bufs);
-  free_bufs(h->sc_bufs);
+  h->cur.reset();
+  h->graveyard.clear();
+  h->o_tab.reset();
+  h->o_fan.reset();
+  h->m_pool.o.reset();
+  h->m_foff.o.reset();
+  h->m_fver.o.reset();
   free_bufs(h->fan_bufs);
   free_bufs(h->fan_out_bufs);
-  free_bufs(h->fan_tab_bufs);
   if (h->d_patch.p) (void)hipFree(h->d_patch.p);
   if (h->h_stage) (void)hipHostFree(h->h_stage);
   if (h->patch_ev) (void)hipEventDestroy(h->patch_ev);
   if (h->d_rules.p) (void)hipFree(h->d_rules.p);
-  if (h->sc.ctl_host) (void)hipHostFree(h->sc.ctl_host);
-  if (h->d_pool.p) (void)hipFree(h->d_pool.p);
-  if (h->d_foff.p) (void)hipFree(h->d_foff.p);
-  if (h->d_fver.p) (void)hipFree(h->d_fver.p);
   if (h->d_in_bytes) (void)hipFree(h->d_in_bytes);
   if (h->d_in_off) (void)hipFree(h->d_in_off);
-  for (auto& e : h->ev)
-    if (e) (void)hipEventDestroy(e);
-  if (h->stream) (void)hipStreamDestroy(h->stream);
+  if (h->wstream) (void)hipStreamDestroy(h->wstream);
   delete h;
 }
 
@@ -1584,13 +1938,13 @@ static int route_ref_locked(emqxgm* h, const uint8_t* p, uint32_t len, uint32_t*
 
 int emqxgm_trie_insert(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t* id) {
   if (!h || (!filter && len)) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  WriterLock g(h);
   return trie_insert_locked(h, filter, len, id);
 }
 
 int emqxgm_trie_delete(emqxgm_t* h, const uint8_t* filter, uint32_t len) {
   if (!h || (!filter && len)) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  WriterLock g(h);
   const uint32_t i = find_id(h, filter, len, false);
   if (i != NONE && h->filters[i].in_trie) {  // absent filter: no-op (emqx_trie.erl:139-144)
     h->filters[i].in_trie = 0;
@@ -1603,13 +1957,13 @@ int emqxgm_trie_delete(emqxgm_t* h, const uint8_t* filter, uint32_t len) {
 
 int emqxgm_route_ref(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t* id) {
   if (!h || (!filter && len)) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  WriterLock g(h);
   return route_ref_locked(h, filter, len, id);
 }
 
 int emqxgm_route_unref(emqxgm_t* h, const uint8_t* filter, uint32_t len) {
   if (!h || (!filter && len)) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  WriterLock g(h);
   const uint32_t i = find_id(h, filter, len, false);
   if (i == NONE || h->filters[i].route_refs == 0) return -ENOENT;
   if (--h->filters[i].route_refs == 0) {
@@ -1627,7 +1981,7 @@ int emqxgm_route_add(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t 
   if (!h || (!filter && len) || len > 65535 || node == NONE ||
       (group != NONE && (group & EMQXGM_DEST_GROUP)))
     return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  WriterLock g(h);
   if (h->filters.size() >= 0x7FFFFFFFu) return -E2BIG;
   const uint32_t i = find_id(h, filter, len, true);
   auto& v = h->rdest[i];
@@ -1651,7 +2005,7 @@ int emqxgm_route_add(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t 
 int emqxgm_route_delete(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t node,
                         uint32_t group) {
   if (!h || (!filter && len)) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  WriterLock g(h);
   const uint32_t i = find_id(h, filter, len, false);
   if (i == NONE) return 0;
   auto it = h->rdest.find(i);
@@ -1677,7 +2031,7 @@ int emqxgm_route_delete(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32
 
 int emqxgm_set_local_node(emqxgm_t* h, uint32_t node) {
   if (!h) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  std::lock_guard<std::mutex> g(h->wmu);
   if (h->local_node != node) {
     h->local_node = node;
     h->fan_rebuild = true;
@@ -1688,7 +2042,7 @@ int emqxgm_set_local_node(emqxgm_t* h, uint32_t node) {
 
 int emqxgm_subscriber_add(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t sub) {
   if (!h || (!filter && len) || len > 65535) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  WriterLock g(h);
   if (h->filters.size() >= 0x7FFFFFFFu) return -E2BIG;
   const uint32_t i = find_id(h, filter, len, true);
   auto& v = h->lsubs[i];
@@ -1702,7 +2056,7 @@ int emqxgm_subscriber_add(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint
 
 int emqxgm_subscriber_delete(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t sub) {
   if (!h || (!filter && len)) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  WriterLock g(h);
   const uint32_t i = find_id(h, filter, len, false);
   if (i == NONE) return 0;
   auto it = h->lsubs.find(i);
@@ -1719,7 +2073,7 @@ int emqxgm_subscriber_delete(emqxgm_t* h, const uint8_t* filter, uint32_t len, u
 int emqxgm_trie_insert_many(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets,
                             uint64_t n, uint32_t* ids) {
   if (!h || !offsets || (!bytes && n)) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  WriterLock g(h);
   for (uint64_t i = 0; i < n; ++i) {
     const uint64_t b = offsets[i], e = offsets[i + 1];
     if (e < b || e - b > 65535) return -EINVAL;
@@ -1732,7 +2086,7 @@ int emqxgm_trie_insert_many(emqxgm_t* h, const uint8_t* bytes, const uint64_t* o
 int emqxgm_route_ref_many(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
                           uint32_t* ids) {
   if (!h || !offsets || (!bytes && n)) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  WriterLock g(h);
   for (uint64_t i = 0; i < n; ++i) {
     const uint64_t b = offsets[i], e = offsets[i + 1];
     if (e < b || e - b > 65535) return -EINVAL;
@@ -1744,7 +2098,7 @@ int emqxgm_route_ref_many(emqxgm_t* h, const uint8_t* bytes, const uint64_t* off
 
 int emqxgm_commit(emqxgm_t* h, uint64_t* epoch) {
   if (!h) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  std::lock_guard<std::mutex> g(h->wmu);
   int rc = 0;
   if (h->dirty) rc = commit_locked(h);
   if (epoch) *epoch = h->epoch;
@@ -1753,20 +2107,20 @@ int emqxgm_commit(emqxgm_t* h, uint64_t* epoch) {
 
 int emqxgm_trie_empty(emqxgm_t* h) {
   if (!h) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
-  return h->ix.trie_empty ? 1 : 0;
+  std::lock_guard<std::mutex> g(h->emu);
+  return h->cur->ix.trie_empty ? 1 : 0;
 }
 
 int emqxgm_trie_member(emqxgm_t* h, const uint8_t* filter, uint32_t len) {
   if (!h || (!filter && len)) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  std::shared_lock<std::shared_mutex> g(h->pmu);
   const uint32_t i = find_id(h, filter, len, false);
   return (i != NONE && h->filters[i].trie_committed) ? 1 : 0;
 }
 
 int emqxgm_lookup_id(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t* id) {
   if (!h || !id || (!filter && len)) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  std::shared_lock<std::shared_mutex> g(h->pmu);
   const uint32_t i = find_id(h, filter, len, false);
   if (i == NONE) return -ENOENT;
   *id = i;
@@ -1775,101 +2129,91 @@ int emqxgm_lookup_id(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t*
 
 int emqxgm_filter_bytes(emqxgm_t* h, uint32_t id, const uint8_t** p, uint32_t* len) {
   if (!h || !p || !len) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  std::shared_lock<std::shared_mutex> g(h->pmu);
   if (id >= h->filters.size()) return -ENOENT;
   *p = h->pool.data() + h->filters[id].off;
   *len = h->filters[id].len;
   return 0;
 }
 
+int emqxgm_filter_copy(emqxgm_t* h, uint32_t id, uint8_t* buf, uint32_t cap, uint32_t* len) {
+  if (!h || !len || (!buf && cap)) return -EINVAL;
+  std::shared_lock<std::shared_mutex> g(h->pmu);
+  if (id >= h->filters.size()) return -ENOENT;
+  const Filter& f = h->filters[id];
+  *len = f.len;
+  if (f.len > cap) return -ENOSPC;
+  if (f.len) memcpy(buf, h->pool.data() + f.off, f.len);
+  return 0;
+}
+
+int emqxgm_filters_copy(emqxgm_t* h, const uint32_t* ids, uint64_t n, uint8_t* buf, uint64_t cap,
+                        uint64_t* offsets) {
+  if (!h || !offsets || (n && !ids) || (!buf && cap)) return -EINVAL;
+  std::shared_lock<std::shared_mutex> g(h->pmu);
+  uint64_t need = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (ids[i] >= h->filters.size()) return -ENOENT;
+    need += h->filters[ids[i]].len;
+  }
+  offsets[0] = 0;
+  if (need > cap) {
+    offsets[n] = need;
+    return -ENOSPC;
+  }
+  uint64_t o = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    const Filter& f = h->filters[ids[i]];
+    if (f.len) memcpy(buf + o, h->pool.data() + f.off, f.len);
+    o += f.len;
+    offsets[i + 1] = o;
+  }
+  return 0;
+}
+
 int emqxgm_match_device(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_offsets, uint32_t n,
                         uint64_t bytes_len, emqxgm_dev_out* out) {
   if (!h || !out || (!d_offsets && n)) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  std::lock_guard<std::mutex> g(h->mmu);
   if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
   uint32_t pairs = 0;
-  int rc = run_device(h, d_bytes, d_offsets, n, bytes_len, &pairs);
+  int rc = run_device(h, h->sync, d_bytes, d_offsets, n, bytes_len, &pairs);
+  h->sync.epoch.reset();
   if (rc) return rc;
   out->n = n;
   out->n_pairs = pairs;
-  out->row_ptr = h->sc.row;
-  out->filter_id = h->sc.out;
-  out->exact_id = h->sc.exact_id;
-  out->n_words = h->sc.nw;
+  out->row_ptr = h->sync.sc.row;
+  out->filter_id = h->sync.sc.out;
+  out->exact_id = h->sync.sc.exact_id;
+  out->n_words = h->sync.sc.nw;
   return 0;
 }
-
-// ---- pipelined passes ----
-namespace {
-// Runs the single-pass code on a pipe: swaps the pipe's scratch, stream and events with the
-// handle's own for the lifetime of the object.
-struct OnPipe {
-  emqxgm* h;
-  emqxgm::Pipe& p;
-  OnPipe(emqxgm* h_, emqxgm::Pipe& p_) : h(h_), p(p_) { swap(); }
-  ~OnPipe() { swap(); }
-  void swap() {
-    std::swap(h->sc, p.sc);
-    std::swap(h->sc_bufs, p.bufs);
-    std::swap(h->stream, p.stream);
-    for (int i = 0; i < 4; ++i) std::swap(h->ev[i], p.ev[i]);
-  }
-};
-
-// Completes an in-flight pass (stream drained, checked, redone synchronously if it has to be).
-int pipe_complete(emqxgm* h, emqxgm::Pipe& p) {
-  if (p.state != 1) return 0;
-  OnPipe on(h, p);
-  HIPCHK(h, hipStreamSynchronize(h->stream));
-  bool legacy = false;
-  int rc = pass_check(h, p.n, p.bytes_len, 0, legacy);
-  if (rc < 0) {
-    p.state = 0;
-    return rc;
-  }
-  rc = rc == 0 ? pass_finish(h, p.n, false, &p.pairs, nullptr)
-               : run_device(h, p.d_bytes, p.d_off, p.n, p.bytes_len, &p.pairs);
-  p.state = rc ? 0 : 2;
-  return rc;
-}
-
-int drain_pipes(emqxgm* h) {
-  for (auto& p : h->pipes)
-    if (int rc = pipe_complete(h, p)) return rc;
-  return 0;
-}
-}  // namespace
 
 int emqxgm_match_device_submit(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_offsets,
                                uint32_t n, uint64_t bytes_len, uint64_t* ticket) {
   if (!h || !ticket || (!d_offsets && n)) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  std::lock_guard<std::mutex> g(h->mmu);
   if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
   const uint64_t tk = h->next_ticket;
   emqxgm::Pipe& p = h->pipes[tk % EMQXGM_PIPES];
   if (p.state == 1) {
-    h->err = "pipe busy: wait for the ticket submitted EMQXGM_PIPES submissions ago";
+    set_err(h, "pipe busy: wait for the ticket submitted EMQXGM_PIPES submissions ago");
     return -EBUSY;
   }
-  if (!p.stream) {
-    HIPCHK(h, hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking));
-    for (auto& e : p.ev) HIPCHK(h, hipEventCreate(&e));
-  }
-  {
-    OnPipe on(h, p);
-    int rc = pass_prepare(h, n, bytes_len);
-    if (rc < 0) return rc;
-    p.d_bytes = d_bytes;
-    p.d_off = d_offsets;
-    p.n = n;
-    p.bytes_len = bytes_len;
-    p.pairs = 0;
-    if (rc == 2) {
-      p.state = 2;  // empty batch: already complete
-    } else {
-      if ((rc = pass_enqueue(h, d_bytes, d_offsets, n, false, false))) return rc;
-      p.state = 1;
-    }
+  int rc = ctx_init(h, p.c);
+  if (rc) return rc;
+  rc = pass_prepare(h, p.c, n, bytes_len);
+  if (rc < 0) return rc;
+  p.d_bytes = d_bytes;
+  p.d_off = d_offsets;
+  p.n = n;
+  p.bytes_len = bytes_len;
+  p.pairs = 0;
+  if (rc == 2) {
+    p.state = 2;  // empty batch: already complete
+  } else {
+    if ((rc = pass_submit(h, p.c, d_bytes, d_offsets, n, false, false))) return rc;
+    p.state = 1;
   }
   p.ticket = tk;
   h->next_ticket += 1;
@@ -1879,11 +2223,11 @@ int emqxgm_match_device_submit(emqxgm_t* h, const uint8_t* d_bytes, const uint32
 
 int emqxgm_match_device_wait(emqxgm_t* h, uint64_t ticket, emqxgm_dev_out* out) {
   if (!h || !out) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  std::lock_guard<std::mutex> g(h->mmu);
   if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
   emqxgm::Pipe& p = h->pipes[ticket % EMQXGM_PIPES];
   if (ticket == 0 || p.ticket != ticket || p.state == 0) {
-    h->err = "unknown ticket, or its result was already taken / overwritten";
+    set_err(h, "unknown ticket, or its result was already taken / overwritten");
     return -ENOENT;
   }
   int rc = pipe_complete(h, p);
@@ -1891,18 +2235,77 @@ int emqxgm_match_device_wait(emqxgm_t* h, uint64_t ticket, emqxgm_dev_out* out) 
   p.state = 0;
   out->n = p.n;
   out->n_pairs = p.pairs;
-  out->row_ptr = p.sc.row;
-  out->filter_id = p.sc.out;
-  out->exact_id = p.sc.exact_id;
-  out->n_words = p.sc.nw;
+  out->row_ptr = p.c.sc.row;
+  out->filter_id = p.c.sc.out;
+  out->exact_id = p.c.sc.exact_id;
+  out->n_words = p.c.sc.nw;
+  return 0;
+}
+
+int emqxgm_match_batch_submit(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets,
+                              uint32_t n, uint64_t* ticket) {
+  if (!h || !ticket || !offsets || offsets[0] != 0 || (!bytes && offsets[n])) return -EINVAL;
+  if (n > h->cfg.batch_max) return -E2BIG;
+  std::lock_guard<std::mutex> g(h->mmu);
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
+  const uint64_t tk = h->next_hticket;
+  emqxgm::HostPipe& p = h->hpipes[tk % EMQXGM_HOST_PIPES];
+  if (p.state == 1) {
+    set_err(h, "host pipe busy: wait for the ticket submitted EMQXGM_HOST_PIPES submissions ago");
+    return -EBUSY;
+  }
+  const uint64_t nb = offsets[n];
+  int rc = ctx_init(h, p.c);
+  if (rc) return rc;
+  rc = pass_prepare(h, p.c, n, nb);
+  if (rc < 0) return rc;
+  if ((rc = host_pipe_reserve(h, p, n, std::max<uint64_t>(nb, 1), p.c.sc.p_cap))) return rc;
+  p.n = n;
+  p.bytes_len = nb;
+  p.pairs = 0;
+  if (n == 0) {
+    p.h_row[0] = 0;
+    p.state = 2;
+  } else {
+    if (nb) HIPCHK(h, hipMemcpyAsync(p.d_bytes, bytes, nb, hipMemcpyHostToDevice, p.c.stream));
+    HIPCHK(h, hipMemcpyAsync(p.d_off, offsets, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, p.c.stream));
+    if ((rc = pass_submit(h, p.c, p.d_bytes, p.d_off, n, false, false)) ||
+        (rc = host_pipe_copy_out(h, p)))
+      return rc;
+    p.state = 1;
+  }
+  p.ticket = tk;
+  h->next_hticket += 1;
+  *ticket = tk;
+  return 0;
+}
+
+int emqxgm_match_batch_wait(emqxgm_t* h, uint64_t ticket, emqxgm_batch_out* out) {
+  if (!h || !out) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mmu);
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
+  emqxgm::HostPipe& p = h->hpipes[ticket % EMQXGM_HOST_PIPES];
+  if (ticket == 0 || p.ticket != ticket || p.state == 0) {
+    set_err(h, "unknown ticket, or its result was already taken / overwritten");
+    return -ENOENT;
+  }
+  int rc = host_pipe_complete(h, p);
+  if (rc) return rc;
+  p.state = 0;
+  out->n = p.n;
+  out->n_pairs = p.pairs;
+  out->row_ptr = p.h_row;
+  out->filter_id = p.h_fid;
+  out->exact_id = p.h_exact;
   return 0;
 }
 
 int emqxgm_match_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets, uint32_t n,
                        emqxgm_out* out) {
   if (!h || !out || (!offsets && n)) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  std::lock_guard<std::mutex> g(h->mmu);
   if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
+  PassCtx& c = h->sync;
   // results land in pinned host buffers of the handle by D2H copies (u64 row pointers are built
   // on the device): no host-side conversion or initialisation per topic
   int rc = 0;
@@ -1926,11 +2329,13 @@ int emqxgm_match_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offset
     }
     if ((rc = ensure_input(h, std::max<uint64_t>(b1 - b0, 1), (uint64_t)m + 1))) return rc;
     if (b1 > b0)
-      HIPCHK(h, hipMemcpyAsync(h->d_in_bytes, bytes + b0, b1 - b0, hipMemcpyHostToDevice, h->stream));
+      HIPCHK(h, hipMemcpyAsync(h->d_in_bytes, bytes + b0, b1 - b0, hipMemcpyHostToDevice, c.stream));
     HIPCHK(h, hipMemcpyAsync(h->d_in_off, loff.data(), ((size_t)m + 1) * 4, hipMemcpyHostToDevice,
-                             h->stream));
+                             c.stream));
     uint32_t pairs = 0;
-    if ((rc = run_device(h, h->d_in_bytes, h->d_in_off, m, b1 - b0, &pairs))) return rc;
+    rc = run_device(h, c, h->d_in_bytes, h->d_in_off, m, b1 - b0, &pairs);
+    c.epoch.reset();
+    if (rc) return rc;
     if ((uint64_t)m + 1 > h->row64_cap) {
       if (h->d_row64) (void)hipFree(h->d_row64);
       h->d_row64 = nullptr;
@@ -1940,15 +2345,15 @@ int emqxgm_match_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offset
     }
     if ((rc = pinned_reserve(h, h->hp_fid, std::max<size_t>((total + pairs) * 4, 4), true)))
       return rc;
-    HIPCHK(h, launch_row64(h->sc.row, total, h->d_row64, m + 1, h->stream));
+    HIPCHK(h, launch_row64(c.sc.row, total, h->d_row64, m + 1, c.stream));
     HIPCHK(h, hipMemcpyAsync(row + i0, h->d_row64, ((size_t)m + 1) * 8, hipMemcpyDeviceToHost,
-                             h->stream));
-    HIPCHK(h, hipMemcpyAsync((uint32_t*)h->hp_exact.p + i0, h->sc.exact_id, (size_t)m * 4,
-                             hipMemcpyDeviceToHost, h->stream));
+                             c.stream));
+    HIPCHK(h, hipMemcpyAsync((uint32_t*)h->hp_exact.p + i0, c.sc.exact_id, (size_t)m * 4,
+                             hipMemcpyDeviceToHost, c.stream));
     if (pairs)
-      HIPCHK(h, hipMemcpyAsync((uint32_t*)h->hp_fid.p + total, h->sc.out, (size_t)pairs * 4,
-                               hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+      HIPCHK(h, hipMemcpyAsync((uint32_t*)h->hp_fid.p + total, c.sc.out, (size_t)pairs * 4,
+                               hipMemcpyDeviceToHost, c.stream));
+    HIPCHK(h, hipStreamSynchronize(c.stream));
     total += pairs;
   }
   out->n = n;
@@ -1975,8 +2380,9 @@ void emqxgm_host_free(emqxgm_t* h, void* p) {
 int emqxgm_publish_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets, uint32_t n,
                          emqxgm_publish_out* out) {
   if (!h || !out || (!offsets && n)) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  std::lock_guard<std::mutex> g(h->mmu);
   if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
+  PassCtx& c = h->sync;
   h->h_rp.assign((size_t)n + 1, 0);
   h->h_dp.assign((size_t)n + 1, 0);
   h->h_rf.clear();
@@ -1997,13 +2403,18 @@ int emqxgm_publish_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offs
     int rc = ensure_input(h, std::max<uint64_t>(b1 - b0, 1), (uint64_t)m + 1);
     if (rc) return rc;
     if (b1 > b0)
-      HIPCHK(h, hipMemcpyAsync(h->d_in_bytes, bytes + b0, b1 - b0, hipMemcpyHostToDevice, h->stream));
+      HIPCHK(h, hipMemcpyAsync(h->d_in_bytes, bytes + b0, b1 - b0, hipMemcpyHostToDevice, c.stream));
     HIPCHK(h, hipMemcpyAsync(h->d_in_off, loff.data(), ((size_t)m + 1) * 4, hipMemcpyHostToDevice,
-                             h->stream));
+                             c.stream));
     uint32_t pairs = 0, nr = 0, nd = 0;
-    if ((rc = run_device(h, h->d_in_bytes, h->d_in_off, m, b1 - b0, &pairs)) ||
-        (rc = run_fanout(h, m, &nr, &nd)))
-      return rc;
+    // the match and the fan-out must read one epoch: redo both if a commit came in between
+    for (;;) {
+      rc = run_device(h, c, h->d_in_bytes, h->d_in_off, m, b1 - b0, &pairs);
+      if (!rc) rc = run_fanout(h, m, &nr, &nd);
+      if (rc != 1) break;
+    }
+    c.epoch.reset();
+    if (rc) return rc;
     const FanScratch& f = h->fs;
     const uint64_t rbase = h->h_rf.size(), dbase = h->h_df.size();
     h->h_rf.resize(rbase + nr);
@@ -2011,17 +2422,17 @@ int emqxgm_publish_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offs
     h->h_df.resize(dbase + nd);
     h->h_ds.resize(dbase + nd);
     std::vector<uint32_t> rp(m + 1), dp(m + 1);
-    HIPCHK(h, hipMemcpyAsync(rp.data(), f.rp, ((size_t)m + 1) * 4, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(h, hipMemcpyAsync(dp.data(), f.dp, ((size_t)m + 1) * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipMemcpyAsync(rp.data(), f.rp, ((size_t)m + 1) * 4, hipMemcpyDeviceToHost, c.stream));
+    HIPCHK(h, hipMemcpyAsync(dp.data(), f.dp, ((size_t)m + 1) * 4, hipMemcpyDeviceToHost, c.stream));
     if (nr) {
-      HIPCHK(h, hipMemcpyAsync(h->h_rf.data() + rbase, f.o_rf, (size_t)nr * 4, hipMemcpyDeviceToHost, h->stream));
-      HIPCHK(h, hipMemcpyAsync(h->h_rd.data() + rbase, f.o_rd, (size_t)nr * 4, hipMemcpyDeviceToHost, h->stream));
+      HIPCHK(h, hipMemcpyAsync(h->h_rf.data() + rbase, f.o_rf, (size_t)nr * 4, hipMemcpyDeviceToHost, c.stream));
+      HIPCHK(h, hipMemcpyAsync(h->h_rd.data() + rbase, f.o_rd, (size_t)nr * 4, hipMemcpyDeviceToHost, c.stream));
     }
     if (nd) {
-      HIPCHK(h, hipMemcpyAsync(h->h_df.data() + dbase, f.o_df, (size_t)nd * 4, hipMemcpyDeviceToHost, h->stream));
-      HIPCHK(h, hipMemcpyAsync(h->h_ds.data() + dbase, f.o_ds, (size_t)nd * 4, hipMemcpyDeviceToHost, h->stream));
+      HIPCHK(h, hipMemcpyAsync(h->h_df.data() + dbase, f.o_df, (size_t)nd * 4, hipMemcpyDeviceToHost, c.stream));
+      HIPCHK(h, hipMemcpyAsync(h->h_ds.data() + dbase, f.o_ds, (size_t)nd * 4, hipMemcpyDeviceToHost, c.stream));
     }
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipStreamSynchronize(c.stream));
     for (uint32_t i = 0; i <= m; ++i) {
       h->h_rp[i0 + i] = rbase + rp[i];
       h->h_dp[i0 + i] = dbase + dp[i];
@@ -2042,16 +2453,18 @@ int emqxgm_publish_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offs
 int emqxgm_walk_census(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_offsets, uint32_t n,
                        uint64_t bytes_len, uint64_t out[6]) {
   if (!h || !out || (!d_offsets && n)) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  std::lock_guard<std::mutex> g(h->mmu);
   if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
   uint32_t pairs = 0;
   memset(out, 0, 6 * sizeof(uint64_t));
-  return run_device(h, d_bytes, d_offsets, n, bytes_len, &pairs, out);
+  int rc = run_device(h, h->sync, d_bytes, d_offsets, n, bytes_len, &pairs, out);
+  h->sync.epoch.reset();
+  return rc;
 }
 
 static int grow_buf(emqxgm* h, DevBuf& b, uint64_t bytes) {
   if (bytes <= b.bytes && b.p) return 0;
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->sync.stream));
   if (b.p) (void)hipFree(b.p);
   b = DevBuf();
   const uint64_t cap = std::max<uint64_t>(bytes + bytes / 2, 4096);
@@ -2071,7 +2484,7 @@ int emqxgm_match_rules(emqxgm_t* h, const uint8_t* name_bytes, const uint32_t* n
     if (name_offsets[i + 1] < name_offsets[i]) return -EINVAL;
   for (uint32_t i = 0; i < n_rules; ++i)
     if (rule_offsets[i + 1] < rule_offsets[i]) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  std::lock_guard<std::mutex> g(h->mmu);
   if (n == 0) return 0;
   if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
   // one device buffer: [names | name offsets | rules | rule offsets | flags | out]
@@ -2083,7 +2496,7 @@ int emqxgm_match_rules(emqxgm_t* h, const uint8_t* name_bytes, const uint32_t* n
   int rc = grow_buf(h, h->d_rules, total);
   if (rc) return rc;
   uint8_t* d = (uint8_t*)h->d_rules.p;
-  hipStream_t s = h->stream;
+  hipStream_t s = h->sync.stream;
   if (nb) HIPCHK(h, hipMemcpyAsync(d, name_bytes, nb, hipMemcpyHostToDevice, s));
   HIPCHK(h, hipMemcpyAsync(d + o_no, name_offsets, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s));
   if (rb) HIPCHK(h, hipMemcpyAsync(d + o_rb, rule_bytes, rb, hipMemcpyHostToDevice, s));
@@ -2100,16 +2513,16 @@ int emqxgm_match_rules(emqxgm_t* h, const uint8_t* name_bytes, const uint32_t* n
 
 int emqxgm_set_profiling(emqxgm_t* h, int on) {
   if (!h) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  std::lock_guard<std::mutex> g(h->mmu);
   h->profiling = on != 0;
   return 0;
 }
 
 int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
   if (!h || !key) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
   if (strcmp(key, "walk_wg_per_cu") == 0) {
     if (value < 1 || value > 16) return -EINVAL;
+    std::lock_guard<std::mutex> g(h->mmu);
     if (int rc = drain_pipes(h)) return rc;  // in-flight passes use the old geometry
     h->cfg.walk_wg_per_cu = (uint32_t)value;
     h->geom = walk_geometry(h->cfg.device, h->cfg.walk_wg_per_cu);
@@ -2117,12 +2530,21 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
   }
   if (strcmp(key, "leaf_prune") == 0) {  // 1 (default): the walk skips leaf-only children
     if (value < 0 || value > 1) return -EINVAL;
-    if (int rc = drain_pipes(h)) return rc;
-    h->ix.leafp_mask = value ? CF_HMASK : 0u;
+    std::lock_guard<std::mutex> g(h->mmu);
+    h->leafp_mask = value ? CF_HMASK : 0u;
+    return 0;
+  }
+  if (strcmp(key, "host_out") == 0) {  // host pipes' result copy: 1 kernel, 0 hipMemcpyAsync
+    if (value < 0 || value > 1) return -EINVAL;
+    std::lock_guard<std::mutex> g(h->mmu);
+    for (auto& p : h->hpipes)
+      if (p.state == 1) return -EBUSY;
+    h->host_out_mode = (uint32_t)value;
     return 0;
   }
   if (strcmp(key, "delta_commit") == 0) {
     if (value < 0 || value > 2) return -EINVAL;
+    std::lock_guard<std::mutex> g(h->wmu);
     h->delta_mode = (uint32_t)value;
     return 0;
   }
@@ -2131,11 +2553,17 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
 
 int emqxgm_get_stats(emqxgm_t* h, emqxgm_stats* st) {
   if (!h || !st) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->mu);
+  std::lock_guard<std::mutex> g(h->stmu);
   *st = h->st;
   return 0;
 }
 
-const char* emqxgm_last_error(emqxgm_t* h) { return h ? h->err.c_str() : "null handle"; }
+const char* emqxgm_last_error(emqxgm_t* h) {
+  static thread_local std::string copy;
+  if (!h) return "null handle";
+  std::lock_guard<std::mutex> g(h->errmu);
+  copy = h->err;
+  return copy.c_str();
+}
 
 }  // extern "C"

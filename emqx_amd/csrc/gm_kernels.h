@@ -173,6 +173,17 @@ hipError_t launch_scatter(Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_
 hipError_t launch_verify_scatter(const uint8_t* bytes, const uint32_t* off, const DevIndex& ix,
                                  Scratch& sc, uint32_t n, hipStream_t s);
 hipError_t launch_fixup(Scratch& sc, uint32_t n, hipStream_t s);
+// A result array copied into pinned host memory by a kernel (PCIe writes from the GPU): its
+// count is n, or min(*n_dev, cap) when n_dev is set (a pass's pair total, read on the device, so
+// nothing on the host sizes the copy).  dst is the device-side address of the host buffer.
+struct CopyOut {
+  const uint32_t* src;
+  uint32_t* dst;
+  uint32_t n;
+  const uint32_t* n_dev;
+  uint32_t cap;
+};
+hipError_t launch_copy_out(const CopyOut& a, const CopyOut& b, const CopyOut& c, hipStream_t s);
 // out[i] = base + row[i], i < m (u64 CSR row pointers of the host API, built on the device)
 hipError_t launch_row64(const uint32_t* row, uint64_t base, uint64_t* out, uint32_t m,
                         hipStream_t s);

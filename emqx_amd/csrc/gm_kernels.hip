@@ -182,6 +182,18 @@ __global__ __launch_bounds__(WG) void k_row64(const uint32_t* row, uint64_t base
   for (uint32_t i = blockIdx.x * WG + threadIdx.x; i < m; i += gridDim.x * WG) out[i] = base + row[i];
 }
 
+// Three result arrays into pinned host memory (blockIdx.y picks one): 16-B stores over the
+// body, the ragged tail by the first block.
+__global__ __launch_bounds__(WG) void k_copy_out(CopyOut a0, CopyOut a1, CopyOut a2) {
+  const CopyOut d = blockIdx.y == 0 ? a0 : blockIdx.y == 1 ? a1 : a2;
+  const uint32_t n = d.n_dev ? min(*d.n_dev, d.cap) : d.n;
+  const uint32_t nv = n >> 2;
+  const uint4* s4 = (const uint4*)d.src;
+  uint4* d4 = (uint4*)d.dst;
+  for (uint32_t i = blockIdx.x * WG + threadIdx.x; i < nv; i += gridDim.x * WG) d4[i] = s4[i];
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3u)) d.dst[4 * nv + threadIdx.x] = d.src[4 * nv + threadIdx.x];
+}
+
 uint32_t grid_for(uint64_t items, uint32_t cap_blocks) {
   uint64_t b = (items + WG - 1) / WG;
   if (b == 0) b = 1;
@@ -354,6 +366,11 @@ hipError_t launch_fixup(Scratch& sc, uint32_t n, hipStream_t s) {
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_compact_rows, dim3(grid_for(n, 4096)), dim3(WG), 0, s, sc.row, sc.out,
                      sc.row2, sc.out2, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_copy_out(const CopyOut& a, const CopyOut& b, const CopyOut& c, hipStream_t s) {
+  hipLaunchKernelGGL(k_copy_out, dim3(512, 3), dim3(WG), 0, s, a, b, c);
   return hipGetLastError();
 }
 

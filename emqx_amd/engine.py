@@ -17,6 +17,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libemqx_gpumatch.so")
 NONE = 0xFFFFFFFF
+ABI_VERSION = 2  # include/emqx_gpumatch.h EMQXGM_ABI_VERSION
 
 
 class EngineError(RuntimeError):
@@ -49,6 +50,11 @@ class _PubOut(C.Structure):
                 ("deliver_sub", C.POINTER(C.c_uint32))]
 
 
+class _BatchOut(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("n_pairs", C.c_uint32), ("row_ptr", C.POINTER(C.c_uint32)),
+                ("filter_id", C.POINTER(C.c_uint32)), ("exact_id", C.POINTER(C.c_uint32))]
+
+
 class _RetOut(C.Structure):
     _fields_ = [("n", C.c_uint32), ("n_ids", C.c_uint64), ("ptr", C.POINTER(C.c_uint64)),
                 ("id", C.POINTER(C.c_uint32))]
@@ -63,7 +69,8 @@ class _Stats(C.Structure):
                 ("topics", C.c_uint64), ("pairs", C.c_uint64), ("rejected_pairs", C.c_uint64),
                 ("reruns", C.c_uint64), ("walk_ms", C.c_double), ("walk_launches", C.c_uint64),
                 ("total_ms", C.c_double), ("full_commits", C.c_uint64),
-                ("delta_commits", C.c_uint64), ("last_commit_ms", C.c_double)]
+                ("delta_commits", C.c_uint64), ("last_commit_ms", C.c_double),
+                ("tok_ms", C.c_double), ("tok_launches", C.c_uint64)]
 
 
 # name -> (restype, argtypes): exactly the entry points declared in include/emqx_gpumatch.h
@@ -86,12 +93,16 @@ SYMBOLS = {
     "emqxgm_trie_member": (C.c_int, [_P, C.c_char_p, C.c_uint32]),
     "emqxgm_lookup_id": (C.c_int, [_P, C.c_char_p, C.c_uint32, _U32P]),
     "emqxgm_filter_bytes": (C.c_int, [_P, C.c_uint32, C.POINTER(_U8P), _U32P]),
+    "emqxgm_filter_copy": (C.c_int, [_P, C.c_uint32, _P, C.c_uint32, _U32P]),
+    "emqxgm_filters_copy": (C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, _P]),
     "emqxgm_match_batch": (C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(_Out)]),
     "emqxgm_match_device": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, C.POINTER(_DevOut)]),
     "emqxgm_match_device_submit": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, _U64P]),
     "emqxgm_host_alloc": (C.c_void_p, [_P, C.c_uint64]),
     "emqxgm_host_free": (None, [_P, C.c_void_p]),
     "emqxgm_match_device_wait": (C.c_int, [_P, C.c_uint64, C.POINTER(_DevOut)]),
+    "emqxgm_match_batch_submit": (C.c_int, [_P, _P, _P, C.c_uint32, _U64P]),
+    "emqxgm_match_batch_wait": (C.c_int, [_P, C.c_uint64, C.POINTER(_BatchOut)]),
     "emqxgm_walk_census": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, _U64P]),
     "emqxgm_route_add": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32]),
     "emqxgm_route_delete": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32]),
@@ -129,7 +140,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.emqxgm_abi_version() != 1:
+    if lib.emqxgm_abi_version() != ABI_VERSION:
         raise ImportError("emqx_gpumatch ABI mismatch")
     return lib
 
@@ -275,6 +286,8 @@ class Engine:
 
     def publish(self, topics: Sequence[bytes]) -> PublishResult:
         buf, off = pack(list(topics), np.uint64)
+        if len(buf) > 0xFFFFFFFF:
+            raise EngineError("batch larger than 4 GiB: split it")
         off32 = np.ascontiguousarray(off, dtype=np.uint32)
         n = len(off32) - 1
         o = _PubOut()
@@ -323,11 +336,31 @@ class Engine:
         return None if rc == -errno.ENOENT else (self._check(rc, "lookup_id") or i.value)
 
     def filter_bytes(self, fid: int) -> bytes:
-        p = _U8P()
+        """The bytes of filter id `fid`, copied under the engine's registry lock
+        (emqxgm_filter_copy: a pointer into the registry could dangle once a writer grows it)."""
         n = C.c_uint32()
-        self._check(self._lib.emqxgm_filter_bytes(self._h, fid, C.byref(p), C.byref(n)),
-                    "filter_bytes")
-        return C.string_at(p, n.value)
+        buf = C.create_string_buffer(256)
+        rc = self._lib.emqxgm_filter_copy(self._h, fid, buf, len(buf), C.byref(n))
+        if rc == -errno.ENOSPC:
+            buf = C.create_string_buffer(n.value)
+            rc = self._lib.emqxgm_filter_copy(self._h, fid, buf, len(buf), C.byref(n))
+        self._check(rc, "filter_copy")
+        return buf.raw[:n.value]
+
+    def filters_bytes(self, ids) -> List[bytes]:
+        """The bytes of many filter ids at once (emqxgm_filters_copy)."""
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        off = np.zeros(len(ids) + 1, np.uint64)
+        cap = 64 * max(1, len(ids))
+        for _ in range(2):
+            buf = np.empty(max(cap, 1), np.uint8)
+            rc = self._lib.emqxgm_filters_copy(self._h, _ptr(ids), len(ids), _ptr(buf), cap, _ptr(off))
+            if rc != -errno.ENOSPC:
+                break
+            cap = int(off[-1])
+        self._check(rc, "filters_copy")
+        raw = buf.tobytes()
+        return [raw[int(off[i]):int(off[i + 1])] for i in range(len(ids))]
 
     # ---- match ----
     def match_packed(self, buf: np.ndarray, off: np.ndarray, copy: bool = True) -> MatchResult:
@@ -388,6 +421,34 @@ class Engine:
                     "match_device_wait")
         return DeviceResult(o.n, o.n_pairs, o.row_ptr or 0, o.filter_id or 0, o.exact_id or 0,
                             o.n_words or 0)
+
+    HOST_PIPES = 3  # EMQXGM_HOST_PIPES
+
+    def match_batch_submit(self, buf: np.ndarray, off: np.ndarray) -> int:
+        """emqxgm_match_batch_submit: host-in pass (H2D, device pass, results to pinned host
+        memory) enqueued on one of HOST_PIPES streams.  `buf` / `off` (uint8 / uint32, off[0] ==
+        0) must stay alive and unchanged until the wait: keep a reference."""
+        assert off.dtype == np.uint32 and buf.dtype == np.uint8
+        t = C.c_uint64(0)
+        self._check(self._lib.emqxgm_match_batch_submit(self._h, _ptr(buf), _ptr(off), len(off) - 1,
+                                                        C.byref(t)), "match_batch_submit")
+        return int(t.value)
+
+    def match_batch_wait(self, ticket: int, copy: bool = True) -> MatchResult:
+        """emqxgm_match_batch_wait: the host-resident result (row pointers as uint64 when copied;
+        copy=False gives views of the pipe's pinned buffers, u32 rows, valid until ticket +
+        HOST_PIPES is submitted)."""
+        o = _BatchOut()
+        self._check(self._lib.emqxgm_match_batch_wait(self._h, ticket, C.byref(o)),
+                    "match_batch_wait")
+        n = o.n
+        row = np.ctypeslib.as_array(o.row_ptr, shape=(n + 1,))
+        fid = (np.ctypeslib.as_array(o.filter_id, shape=(o.n_pairs,)) if o.n_pairs
+               else np.zeros(0, np.uint32))
+        ex = np.ctypeslib.as_array(o.exact_id, shape=(n,)) if n else np.zeros(0, np.uint32)
+        if copy:
+            return MatchResult(row.astype(np.uint64), fid.copy(), ex.copy())
+        return MatchResult(row, fid, ex)
 
     def walk_census(self, d_bytes: int, d_off: int, n: int, bytes_len: int) -> dict:
         """Instrumented pass: {'states': sum S(t), 'slot_loads', 'pairs', 'words',

@@ -37,12 +37,25 @@
  * exceeds the device layout limits: 2^27 trie nodes, 2^31 filters).  There is no CPU fallback:
  * a device failure is reported, never silently recomputed on the host.
  *
- * Ownership: input buffers are borrowed for the duration of the call.  Output arrays in
- * emqxgm_out / emqxgm_dev_out are owned by the engine and stay valid until the next match
- * call on the same handle or emqxgm_destroy.
+ * Ownership: input buffers are borrowed for the duration of the call (the pipelined forms:
+ * until the matching _wait returns).  Output arrays in emqxgm_out / emqxgm_dev_out are owned by
+ * the engine and stay valid until the next match call on the same handle or emqxgm_destroy;
+ * pipelined results as documented at their _submit.  Device inputs (emqxgm_match_device*) must
+ * be complete in HBM when the call is made: the engine's streams do not wait for the caller's
+ * (synchronise the stream that produced them first); the host-in forms copy their input
+ * themselves.
  *
- * Threading: add/remove/commit and match calls are serialised by a per-handle lock; match
- * always reads the last committed epoch.
+ * Threading (the reference reads with read_concurrency while writers commit in mria
+ * transactions, emqx_trie.erl:70-75, emqx_router_utils.erl:74-135):
+ *   - writers (insert/delete/route/subscriber calls, emqxgm_commit) are serialised by one writer
+ *     lock;
+ *   - every match call reads the last committed epoch and never waits for a writer: a commit
+ *     builds the next index beside the current one (a full build: seconds at 10M filters) and
+ *     swaps it in atomically; a small delta is patched in place on the device, ordered on the GPU
+ *     after the passes already enqueued and before every later one.  A pass that started before
+ *     the swap completes against the epoch it started on;
+ *   - match calls serialise among themselves (one pass context per call kind); filter_bytes,
+ *     filter_copy, lookup_id, trie_member and trie_empty only take a shared read lock.
  */
 #ifndef EMQX_GPUMATCH_H
 #define EMQX_GPUMATCH_H
@@ -58,7 +71,7 @@ extern "C" {
 #define EMQXGM_DEST_GROUP 0x80000000u /* dest handle bit: a shared-subscription group */
 #define EMQXGM_RULE_EQ 1u    /* rule flag: {eq, Filter} -- the name must equal the filter */
 #define EMQXGM_RULE_WORDS 2u /* rule flag: match/2 on word lists (no '$' clauses) */
-#define EMQXGM_ABI_VERSION 1
+#define EMQXGM_ABI_VERSION 2
 
 typedef struct emqxgm emqxgm_t;
 
@@ -112,6 +125,8 @@ typedef struct emqxgm_stats {
   uint64_t full_commits;    /* commits that rebuilt the device index */
   uint64_t delta_commits;   /* commits that patched it in place (small deltas) */
   double last_commit_ms;    /* host wall time of the last commit (build/patch + upload) */
+  double tok_ms;            /* summed tokenizer-kernel time (HIP events), if profiling is on */
+  uint64_t tok_launches;
 } emqxgm_stats;
 
 int emqxgm_abi_version(void);
@@ -136,7 +151,15 @@ int emqxgm_trie_empty(emqxgm_t* h);
 int emqxgm_trie_member(emqxgm_t* h, const uint8_t* filter, uint32_t len);
 
 int emqxgm_lookup_id(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t* id);
+/* Pointer to filter id's bytes in the engine's registry: valid until the next call that adds a
+ * filter string (insert / route / subscriber calls may grow the registry).  Prefer the copies. */
 int emqxgm_filter_bytes(emqxgm_t* h, uint32_t id, const uint8_t** p, uint32_t* len);
+/* Copy of filter id's bytes into buf (cap bytes): *len = its length; -ENOSPC if cap < *len. */
+int emqxgm_filter_copy(emqxgm_t* h, uint32_t id, uint8_t* buf, uint32_t cap, uint32_t* len);
+/* The filters ids[0..n) packed into buf: filter i = buf[offsets[i] .. offsets[i+1]) (offsets has
+ * n+1 entries).  -ENOSPC if cap is too small (offsets[n] = the bytes needed). */
+int emqxgm_filters_copy(emqxgm_t* h, const uint32_t* ids, uint64_t n, uint8_t* buf, uint64_t cap,
+                        uint64_t* offsets);
 
 /* Match n topics: topic i = bytes[offsets[i] .. offsets[i+1]), offsets has n+1 entries. */
 int emqxgm_match_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets, uint32_t n,
@@ -167,6 +190,30 @@ void emqxgm_host_free(emqxgm_t* h, void* p);
 int emqxgm_match_device_submit(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_offsets,
                                uint32_t n, uint64_t bytes_len, uint64_t* ticket);
 int emqxgm_match_device_wait(emqxgm_t* h, uint64_t ticket, emqxgm_dev_out* out);
+
+/* Pipelined host-in / host-out form of emqxgm_match_batch: the call a NIF batcher makes (the
+ * reference's publishers call match_routes concurrently from every scheduler,
+ * emqx_broker.erl:231).  _submit enqueues, on one of EMQXGM_HOST_PIPES streams, the copy of the
+ * batch into HBM, the whole device pass and the copy of its result into pinned host memory, and
+ * returns at once; _wait(ticket) completes it.  With several tickets in flight one batch's
+ * upload, another's pass and a third's download overlap.  The batch: n <= cfg.batch_max topics,
+ * topic i = bytes[offsets[i] .. offsets[i+1]), offsets[0] == 0 (-EINVAL otherwise); bytes and
+ * offsets stay untouched until the wait (pinned memory from emqxgm_host_alloc gives full-speed
+ * copies).  The result (batch-local u32 row pointers, trie filter ids, exact ids) lives in
+ * pinned buffers of the pipe and stays valid until ticket + EMQXGM_HOST_PIPES is submitted;
+ * submitting that ticket before this one was waited for returns -EBUSY.  Results are identical
+ * to emqxgm_match_batch's. */
+#define EMQXGM_HOST_PIPES 3
+typedef struct emqxgm_batch_out {
+  uint32_t n;
+  uint32_t n_pairs;
+  const uint32_t* row_ptr;   /* [n+1] offsets into filter_id */
+  const uint32_t* filter_id; /* [n_pairs] matched trie filter ids */
+  const uint32_t* exact_id;  /* [n] route key equal to the topic, or EMQXGM_NONE */
+} emqxgm_batch_out;
+int emqxgm_match_batch_submit(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets,
+                              uint32_t n, uint64_t* ticket);
+int emqxgm_match_batch_wait(emqxgm_t* h, uint64_t ticket, emqxgm_batch_out* out);
 
 /* ---- publish fan-out (emqx_broker.erl:218-355) -------------------------------------------
  * Routes with dest identity: a plain route {Filter, Node} passes group = EMQXGM_NONE; a shared-
@@ -265,7 +312,9 @@ int emqxgm_walk_census(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_of
                        uint32_t n, uint64_t bytes_len, uint64_t out[6]);
 
 int emqxgm_set_profiling(emqxgm_t* h, int on);
-/* Runtime tuning knobs: "walk_wg_per_cu" (persistent walk workgroups per CU);
+/* Runtime tuning knobs: "walk_wg_per_cu" (persistent walk workgroups per CU); "leaf_prune"
+ * (1 default: depth-code pruning in the walk, 0 off); "host_out" (host pipes copy results to the
+ * host with a kernel, 1 default, or with hipMemcpyAsync, 0);
  * "delta_commit": 0 = every commit rebuilds the index, 1 = small deltas are patched in place
  * (default), 2 = every delta that fits the tables' load bounds is patched in place. */
 int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value);

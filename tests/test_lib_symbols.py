@@ -30,7 +30,8 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in _declared() if not hasattr(lib, n)]
     assert not missing, missing
     lib.emqxgm_abi_version.restype = ctypes.c_int
-    assert lib.emqxgm_abi_version() == 1
+    from emqx_amd.engine import ABI_VERSION
+    assert lib.emqxgm_abi_version() == ABI_VERSION
 
 
 def test_python_binding_covers_header():
