@@ -12,8 +12,10 @@ N>1 is launched by the driver with torch.distributed.run (one rank per GPU).  ``
 no collective on the data path); ``--shard filters`` = the north-star layout (filters split by
 hash, batch broadcast + results gathered with RCCL every step).
 
-Rank 0 prints one JSON line.  ``roofline`` is for the dominant kernel (k_walk): algorithmic
-bytes per launch (DESIGN.md "Roofline") over its HIP-event-measured average duration.
+Rank 0 prints one JSON line.  ``roofline`` is for the step's dominant kernel (HIP-event timed,
+one pass at a time): for the trie walk / exact probe, random 64-B line accesses per second
+against the measured random-gather ceiling, with SURVEY 8d algorithmic bytes and PMC counter
+bytes beside it as fractions of the 8 TB/s HBM peak (DESIGN.md "Roofline").
 ``cpu_baseline`` is the C++ restatement of the reference's emqx_trie match (oracle/ref_trie.cpp)
 timed on this host's cores on a bounded sample of the same topics (rank 0, N=1 only).
 """
@@ -198,19 +200,20 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 
-    launches = s1["walk_launches"] - s0["walk_launches"]
-    walk_ms = (s1["walk_ms"] - s0["walk_ms"]) / max(1, launches)
+    launches = s1["tok_launches"] - s0["tok_launches"]
+    walks = s1["walk_launches"] - s0["walk_launches"]
+    tok_ms = (s1["tok_ms"] - s0["tok_ms"]) / max(1, launches)
+    exact_ms = (s1["exact_ms"] - s0["exact_ms"]) / max(1, launches)
+    walk_ms = (s1["walk_ms"] - s0["walk_ms"]) / max(1, walks)
     pipe_ms = (s1["total_ms"] - s0["total_ms"]) / max(1, launches)
-    # algorithmic bytes of one k_walk launch (DESIGN.md "Roofline"): per topic its 64-B record
-    # (header + level tokens) and a 4-B match count, 3 x 16-B edge probes per matched trie
-    # state (SURVEY 8d's 48*S(t)), and a 16-B staged (topic, filter, rank) record per match.
-    walk_bytes = (64 + 4) * w.nt + 48 * census["states"] + 16 * census["pairs"]
-    achieved = walk_bytes / (walk_ms * 1e-3) / 1e9 if walk_ms > 0 else 0.0
     topics_total = (w.nt * world) if args.shard == "topics" else w.nt
     compulsory = int(w.toff[-1]) + 4 * w.nt + 8 * census["pairs"]
     value = topics_total / (elapsed / args.steps)
+    pmc = _pmc(args.cfg, w.nt)
+    roofline = _roofline(w, census, pmc, tok_ms, exact_ms, walk_ms, pipe_ms)
+    roofline["compulsory_bytes_per_batch"] = int(compulsory)
+    roofline["compulsory_frac"] = round(compulsory / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4)
 
-    traffic = _pmc_traffic(args.cfg, w.nt)
     cpu = _cpu_baseline(w, args, cpu_job) if cpu_job is not None else None
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e:
@@ -288,21 +291,7 @@ def main():
                     "value": round(topics_total / (sync_ms * 1e-3), 1), "ms_per_step": round(sync_ms, 4)}),
                 "pairs_per_s": round(census["pairs"] * (topics_total / w.nt) / (elapsed / args.steps), 1),
             },
-            "roofline": {
-                "kernel": "k_walk",
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                # SURVEY 8d's compulsory-only bytes (topic bytes + offset + an 8-B pair per match)
-                # over the whole step, against the same peak
-                "compulsory_bytes_per_batch": int(compulsory),
-                "compulsory_frac": round(compulsory / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "walk_ms_per_launch": round(walk_ms, 4),
-                "algorithmic_bytes_per_launch": int(walk_bytes),
-            },
+            "roofline": roofline,
             "cpu_baseline": cpu,
             "end_to_end": e2e,
         }
@@ -346,17 +335,102 @@ def _reorder_topics(w, how):
     return dataclasses.replace(w, tbytes=tbytes, toff=off)
 
 
-def _pmc_traffic(cfg, nt):
-    """HBM bytes per k_walk launch from the committed rocprofv3 PMC summary, if present."""
-    p = os.path.join(ROOT, "profiles", f"pmc_walk_cfg{cfg}.json")
-    try:
-        with open(p) as f:
-            d = json.load(f)
-        if int(d.get("topics", -1)) == nt:
-            return d.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
-    return None
+# Random 64-B line accesses per second the memory system sustains for a table beyond the L2
+# (tools/gather_bench.hip, profiles/r01/gather_sizes.txt: 2 GiB table, 64-B lines, 52.1-53.0 G/s;
+# 64-192 MiB tables 53-58 G/s) and for an L2-resident one (8 MiB: 99-109 G/s).
+RANDOM_LINES_PEAK = 53.0e9
+RANDOM_LINES_L2 = 104.0e9
+
+
+def _pmc(cfg, nt):
+    """Per-kernel PMC summary of this config from profiles/ (HBM bytes and L2 hits/misses per
+    launch, tools/pmc_traffic.py), if one was committed for this batch size."""
+    for name in (f"pmc_cfg{cfg}.json", f"pmc_walk_cfg{cfg}.json"):
+        p = os.path.join(ROOT, "profiles", name)
+        try:
+            with open(p) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if int(d.get("topics", -1)) != nt:
+            continue
+        if "kernels" in d:
+            return {k: dict(v, source=f"profiles/{name}") for k, v in d["kernels"].items()}
+        return {"k_walk": {"hbm_bytes_per_launch": d.get("hbm_bytes_per_launch"),
+                           "tcc_hit": d.get("tcc_hit"), "tcc_miss": d.get("tcc_miss"),
+                           "source": f"profiles/{name}"}}
+    return {}
+
+
+def _roofline(w, census, pmc, tok_ms, exact_ms, walk_ms, pipe_ms):
+    """Roofline of the step's dominant kernel (by HIP-event time, one pass at a time).
+
+    k_walk and k_exact are dependent random gathers: the binding resource is the rate of random
+    64-B line accesses (RANDOM_LINES_PEAK), not HBM bandwidth.  `achieved` is the kernel's
+    random line accesses (k_walk: edge-bucket loads counted by the census pass; k_exact: one
+    bucket line per name) per second; beside it the SURVEY 8d algorithmic bytes and the PMC
+    counter bytes as fractions of the 8 TB/s HBM peak, and the PMC L2-miss lines per second
+    against RANDOM_LINES_PEAK.  k_tok streams: bound HBM."""
+    kernels = {"k_tok": tok_ms, "k_exact": exact_ms, "k_walk": walk_ms}
+    dom = max(kernels, key=lambda k: kernels[k])
+    post = max(0.0, pipe_ms - tok_ms - exact_ms - walk_ms)
+    ms = kernels[dom]
+    sec = ms * 1e-3 if ms > 0 else float("inf")
+    nt = w.nt
+    p = pmc.get(dom, {})
+    traffic = p.get("hbm_bytes_per_launch")
+    out = {"kernel": dom}
+    if dom == "k_tok":
+        # topic bytes + offsets in; 64-B record, level count and exact id out per topic
+        alg = int(w.toff[-1]) + 4 * (nt + 1) + (64 + 4 + 4) * nt
+        ach = alg / sec / 1e9
+        out.update({"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "algorithmic_bytes_per_launch": alg})
+    else:
+        if dom == "k_walk":
+            lines = census["slot_loads"]
+            # SURVEY 8d: per topic its 64-B record + 4-B count, 3 x 16-B edge probes per matched
+            # trie state, a 16-B staged pair per match; the pruned walk never loads the states
+            # the depth codes rule out (shown apart)
+            alg = (64 + 4) * nt + 48 * census["states"] + 16 * census["pairs"]
+            pruned = 48 * (census["states"] - census.get("states_visited", census["states"]))
+        else:
+            lines = nt
+            alg = int(w.toff[-1]) + 8 * nt + 64 * nt + 4 * nt
+            pruned = 0
+        ach = lines / sec
+        out.update({
+            "bound": "random-access", "achieved": round(ach / 1e9, 2),
+            "peak": RANDOM_LINES_PEAK / 1e9, "unit": "G lines/s",
+            "frac": round(ach / RANDOM_LINES_PEAK, 4), "traffic": traffic,
+            "random_lines_per_launch": int(lines),
+            "peak_source": "profiles/r01/gather_sizes.txt (tools/gather_bench.hip, 2 GiB table, "
+                           "dependent random 64-B loads)",
+            "hbm_algorithmic": {"bytes_per_launch": int(alg), "pruned_state_bytes": int(pruned),
+                                "achieved_GBs": round(alg / sec / 1e9, 1),
+                                "frac": round(alg / sec / 1e9 / HBM_PEAK_GBS, 4)},
+        })
+        if traffic:
+            out["hbm_counter"] = {"bytes_per_launch": traffic,
+                                  "achieved_GBs": round(traffic / sec / 1e9, 1),
+                                  "frac": round(traffic / sec / 1e9 / HBM_PEAK_GBS, 4),
+                                  "source": p.get("source")}
+        if p.get("tcc_miss") is not None:
+            miss, hit = float(p["tcc_miss"]), float(p.get("tcc_hit") or 0.0)
+            model = miss / RANDOM_LINES_PEAK + hit / RANDOM_LINES_L2
+            out["l2_lines"] = {"miss_per_launch": miss, "hit_per_launch": hit,
+                               "miss_rate_G": round(miss / sec / 1e9, 2),
+                               "frac_miss_lines": round(miss / sec / RANDOM_LINES_PEAK, 4),
+                               # time the misses and hits would take at the measured gather
+                               # ceilings, over the kernel's time
+                               "frac_mixed_ceiling": round(model / sec, 4),
+                               "source": p.get("source")}
+    out["kernels_ms"] = {"k_tok": round(tok_ms, 4), "k_exact": round(exact_ms, 4),
+                         "k_walk": round(walk_ms, 4), "verify+scan+scatter": round(post, 4),
+                         "pass": round(pipe_ms, 4)}
+    out["walk_ms_per_launch"] = round(walk_ms, 4)
+    return out
 
 
 class _CpuIndexJob:
@@ -381,6 +455,7 @@ class _CpuIndexJob:
 def _cpu_baseline(w, args, job):
     """The reference algorithm (C++ restatement of emqx_trie match_compact with an ordered-set
     index, oracle/ref_trie.cpp) on this host's cores, over a bounded sample of the topics."""
+    # the GPU box gives each GPU a 16-CPU share (nproc / os.cpu_count() show the whole host)
     threads = args.cpu_threads or min(16, os.cpu_count() or 1)
     ref, build_s = job.wait()
     n = min(w.nt, 20000)
@@ -391,7 +466,15 @@ def _cpu_baseline(w, args, job):
         dt, _ = ref.time_match(w.tbytes, w.toff[: n2 + 1], threads)
         n = n2
     log(f"cpu baseline: index build {build_s:.1f}s, {n} topics in {dt:.2f}s on {threads} threads")
+    model = "?"
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next(ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
     return {"value": round(n / dt, 1), "unit": "topics/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "host_cpus": os.cpu_count(),
+            "index_build_s": round(build_s, 1),
             "sample": f"first {n} topics of the same batch against the same {w.nf} filters "
                       f"(emqx_trie match_compact restated in C++, std::map ordered set), "
                       f"{dt:.1f}s wall"}

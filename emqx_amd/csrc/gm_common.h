@@ -127,11 +127,20 @@ constexpr uint32_t LIST_MULTI = 0x80000000u;  // tw/tn value is a multi[] index
 GM_HD uint64_t edge_slot(uint32_t parent, uint64_t tok, uint64_t mask) {
   return fmix64(tok ^ ((uint64_t)parent * 0x9e3779b97f4a7c15ull)) & mask;
 }
-// Exact route-key table: buckets of XBUCKET 16-B entries {hash.lo, hash.hi, fid, len}, filled
-// in order (linear probing over buckets); exact_slot gives the home bucket.  An empty entry has
-// fid == NONE; a deleted one {0, 0, TOMB, 0xFFFFFFFF} (a length no key has) never matches.
-constexpr uint32_t XBUCKET = 4;
+// Exact route-key table: 64-B buckets (one line) of XBUCKET 32-B entries, filled in order
+// (linear probing over buckets); exact_slot gives the home bucket.  An entry carries the key's
+// first XINL bytes, so a probe for a key of up to XINL bytes is decided by the one line it loads
+// (no dependent load of a verification record):
+//   e0 = {h32 (high half of the key hash), fid, len, key bytes 0..3}
+//   e1 = {key bytes 4..7, 8..11, 12..15, 16..19}   (zero past len)
+// A longer key's inline prefix and hash filter the candidates and its full bytes (verification
+// record / string pool) confirm.  An empty entry has fid == NONE, a deleted one fid == TOMB.
+constexpr uint32_t XBUCKET = 2;
+constexpr uint32_t XENT_U4 = 2;
+constexpr uint32_t XINL = 20;
 GM_HD uint64_t exact_slot(uint64_t fh, uint64_t mask) { return fmix64(fh + 0x632be59bd9b4e019ull) & mask; }
+// k_tok's exact_id marker for a wildcard name whose route-key probe k_exact still has to run
+constexpr uint32_t X_WILDPEND = 0xFFFFFFFDu;
 
 // Filter verification record (64 B per filter id): {u32 len, 60 bytes of the filter}; the
 // bytes of longer filters are read from the string pool.

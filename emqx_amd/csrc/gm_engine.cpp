@@ -193,7 +193,7 @@ struct PassCtx {
   Scratch sc;
   std::vector<DevBuf> bufs;
   hipStream_t stream = nullptr;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // start, probe, walk, end, tok
   hipEvent_t done = nullptr;  // recorded after each pass enqueued here (guarded by emqxgm::emu)
   bool done_rec = false;
   EpochP epoch;               // epoch of the pass last enqueued here (kept until it completes)
@@ -342,7 +342,10 @@ struct emqxgm {
   std::mutex wmu, emu, mmu, stmu, errmu;
   std::shared_mutex pmu;
   emqxgm_cfg cfg{};
-  hipStream_t wstream = nullptr;  // writer stream: patch uploads and k_patch
+  // writer stream (patch uploads, k_patch): the sync context's stream.  HIP maps streams onto
+  // GPU_MAX_HW_QUEUES (4) hardware queues; a stream of its own pushed a pipe onto a shared queue
+  // and serialised the two pipelined passes (profiles/r02: pipelined step 0.374 vs 0.312 ms)
+  hipStream_t wstream = nullptr;
   std::string err;
 
   // ---- registry (pending state) ----
@@ -469,6 +472,14 @@ uint64_t str_hash(const uint8_t* p, uint32_t len) {
   uint64_t x = FNV_OFF;
   for (uint32_t i = 0; i < len; ++i) x = fnv_step(x, p[i]);
   return fmix64(x);
+}
+
+// The 32-B exact-table entry of a route key (gm_common.h "Exact route-key table").
+void xent(uint64_t fh, uint32_t id, const uint8_t* p, uint32_t len, uint4 e[XENT_U4]) {
+  uint32_t w[5] = {0, 0, 0, 0, 0};
+  memcpy(w, p, std::min<uint32_t>(len, XINL));
+  e[0] = make_uint4((uint32_t)(fh >> 32), id, len, w[0]);
+  e[1] = make_uint4(w[1], w[2], w[3], w[4]);
 }
 
 bool is_wild(const uint8_t* p, uint32_t len) {  // emqx_topic:wildcard/1
@@ -788,7 +799,7 @@ void commit_stats(emqxgm* h, double ms, bool delta) {
   h->st.edge_slots = m.ecap;
   h->st.exact_slots = (m.xcap_p + m.xcap_w) * XBUCKET;
   h->st.max_depth = m.max_depth;
-  h->st.device_bytes = m.ecap * SLOT_U4 * 16 + (m.xcap_p + m.xcap_w) * XBUCKET * 16 + m.tn_cap * 4 +
+  h->st.device_bytes = m.ecap * SLOT_U4 * 16 + (m.xcap_p + m.xcap_w) * XBUCKET * XENT_U4 * 16 + m.tn_cap * 4 +
                        m.fv_cap * 4 + h->pool.size() + (h->filters.size() + 1) * 8 +
                        h->filters.size() * VREC;
   h->st.last_commit_ms = ms;
@@ -926,7 +937,8 @@ int commit_full(emqxgm* h) {
   m.xocc.assign(xcap * XBUCKET / 64 + 1, 0ull);
   m.xtomb.assign(xcap * XBUCKET / 64 + 1, 0ull);
   m.xpos.assign(nf, NONE);
-  std::vector<uint4> xslots(xcap * XBUCKET, make_uint4(0u, 0u, NONE, 0u));
+  std::vector<uint4> xslots(xcap * XBUCKET * XENT_U4, make_uint4(0u, 0u, 0u, 0u));
+  for (uint64_t e = 0; e < xcap * XBUCKET; ++e) xslots[XENT_U4 * e].y = NONE;
   for (uint32_t id = 0; id < h->filters.size(); ++id) {
     const Filter& f = h->filters[id];
     if (!f.route_refs) continue;
@@ -935,10 +947,10 @@ int commit_full(emqxgm* h) {
     uint64_t b = m.xhome(w, fh);
     for (;;) {
       uint32_t j = 0;
-      while (j < XBUCKET && xslots[b * XBUCKET + j].z != NONE) ++j;
+      while (j < XBUCKET && xslots[XENT_U4 * (b * XBUCKET + j)].y != NONE) ++j;
       if (j < XBUCKET) {
         const uint64_t e = b * XBUCKET + j;
-        xslots[e] = make_uint4((uint32_t)fh, (uint32_t)(fh >> 32), id, f.len);
+        xent(fh, id, h->pool.data() + f.off, f.len, &xslots[XENT_U4 * e]);
         bset(m.xocc, e);
         m.xpos[id] = (uint32_t)e;
         break;
@@ -1021,7 +1033,10 @@ int commit_delta(emqxgm* h) {
   const uint64_t fmask =
       h->cfg.full_hash_bits >= 64 ? ~0ull : ((1ull << h->cfg.full_hash_bits) - 1ull);
   std::unordered_map<uint64_t, uint32_t> epatch;  // edge slot -> node (NONE: TOMB)
-  std::unordered_map<uint64_t, uint4> xpatch;     // exact entry -> content
+  struct XE {
+    uint4 e[XENT_U4];
+  };
+  std::unordered_map<uint64_t, XE> xpatch;        // exact entry -> content
   std::vector<uint32_t> dirty;                    // nodes whose slot / side entry changed
   std::vector<uint32_t> fv_words;  // changed words of the verify bitmap
   std::vector<uint64_t> toks;
@@ -1136,7 +1151,7 @@ int commit_delta(emqxgm* h) {
     const uint32_t e = m.xpos[id];
     if (e == NONE) return 1;
     bset(m.xtomb, e);
-    xpatch[e] = make_uint4(0u, 0u, TOMB, 0xFFFFFFFFu);
+    xpatch[e] = XE{{make_uint4(0u, TOMB, 0u, 0u), make_uint4(0u, 0u, 0u, 0u)}};
     m.xpos[id] = NONE;
     m.n_route -= 1;
     m.nroute(h->filters[id].wild) -= 1;
@@ -1161,7 +1176,7 @@ int commit_delta(emqxgm* h) {
       }
       b = m.xnext(w, b);
     }
-    xpatch[e] = make_uint4((uint32_t)fh, (uint32_t)(fh >> 32), id, f.len);
+    xent(fh, id, h->pool.data() + f.off, f.len, xpatch[e].e);
     m.xpos[id] = (uint32_t)e;
     m.n_route += 1;
     m.nroute(w) += 1;
@@ -1187,7 +1202,7 @@ int commit_delta(emqxgm* h) {
     if (p.second != NONE) m.node_slot(p.second, sl);
     pl.add(m.d_edges + 8 * p.first, sl, 8);
   }
-  for (const auto& p : xpatch) pl.add(m.d_exact + 4 * p.first, &p.second, 4);
+  for (const auto& p : xpatch) pl.add(m.d_exact + 4 * XENT_U4 * p.first, p.second.e, 4 * XENT_U4);
   for (uint32_t n : tn_nodes) pl.add(m.d_tn + n, &m.tn[n], 1);
   std::sort(fv_words.begin(), fv_words.end());
   fv_words.erase(std::unique(fv_words.begin(), fv_words.end()), fv_words.end());
@@ -1342,7 +1357,7 @@ int ensure_scratch(emqxgm* h, PassCtx& c, uint32_t n, uint64_t words, uint32_t p
   HIPCHK(h, hipStreamSynchronize(c.stream));
   const uint32_t ncap = std::max(n, s.n_cap);
   const uint64_t wcap = std::max(words, s.w_cap);
-  const uint32_t pcap = std::max(pairs, s.p_cap);
+  const uint32_t pcap = (std::max(pairs, s.p_cap) + STAGE_CHUNK - 1) / STAGE_CHUNK * STAGE_CHUNK;
   const uint32_t scap = std::max(spill_need, s.spill_items);
   free_bufs(c.bufs);
   if (s.ctl_host) {
@@ -1361,6 +1376,7 @@ int ensure_scratch(emqxgm* h, PassCtx& c, uint32_t n, uint64_t words, uint32_t p
       (rc = dev_alloc(h, c, (void**)&s.rej, (size_t)ncap * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.exact_id, (size_t)ncap * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.stg, (size_t)pcap * 16)) ||
+      (rc = dev_alloc(h, c, (void**)&s.chk, (size_t)(pcap / STAGE_CHUNK + 1) * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.out, (size_t)pcap * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.out2, (size_t)pcap * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.scan_tmp, (size_t)stw * 4)) ||
@@ -1420,7 +1436,8 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
   hipStream_t st = c.stream;
   DevIndex ix = E.ix;
   ix.leafp_mask = h->leafp_mask;
-  HIPCHK(h, hipStreamWaitEvent(st, E.ready, 0));  // the epoch's uploads / patches have landed
+  // the epoch's uploads / patches must have landed (a full build's have: its wait is skipped)
+  if (hipEventQuery(E.ready) != hipSuccess) HIPCHK(h, hipStreamWaitEvent(st, E.ready, 0));
   if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[0], st));
   HIPCHK(h, hipMemsetAsync(s.ctl, 0, CTL_N * 4, st));
   if (census)
@@ -1428,6 +1445,8 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
                              (CENSUS_N + 3 * (h->geom.lanes / 64)) * sizeof(unsigned long long),
                              st));
   HIPCHK(h, launch_tok(d_bytes, d_off, n, ix, s, st));
+  if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[4], st));
+  HIPCHK(h, launch_exact(d_bytes, d_off, n, ix, s, st));
   if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[1], st));
   if (ix.trie_empty) {
     HIPCHK(h, hipMemsetAsync(s.row, 0, (size_t)(n + 1) * 4, st));
@@ -1522,11 +1541,12 @@ int pass_check(emqxgm* h, PassCtx& c, uint32_t n, uint64_t bytes_len, int attemp
 int pass_finish(emqxgm* h, PassCtx& c, uint32_t n, bool legacy, uint32_t* pairs, uint64_t* census) {
   Scratch& s = c.sc;
   hipStream_t st = c.stream;
-  float tok = 0, walk = 0, all = 0;
+  float tok = 0, exact = 0, walk = 0, all = 0;
   const bool timed = h->profiling;
   const bool walked = !c.epoch->ix.trie_empty;
   if (timed) {
-    HIPCHK(h, hipEventElapsedTime(&tok, c.ev[0], c.ev[1]));
+    HIPCHK(h, hipEventElapsedTime(&tok, c.ev[0], c.ev[4]));
+    HIPCHK(h, hipEventElapsedTime(&exact, c.ev[4], c.ev[1]));
     if (walked) HIPCHK(h, hipEventElapsedTime(&walk, c.ev[1], c.ev[2]));
     HIPCHK(h, hipEventElapsedTime(&all, c.ev[0], c.ev[3]));
   }
@@ -1543,6 +1563,7 @@ int pass_finish(emqxgm* h, PassCtx& c, uint32_t n, bool legacy, uint32_t* pairs,
     if (timed) {
       h->st.tok_ms += tok;
       h->st.tok_launches += 1;
+      h->st.exact_ms += exact;
       if (walked) {
         h->st.walk_ms += walk;
         h->st.walk_launches += 1;
@@ -1865,11 +1886,11 @@ int emqxgm_create(const emqxgm_cfg* cfg, emqxgm_t** out) {
     return -EIO;
   }
   if (hipSetDevice(h->cfg.device) != hipSuccess ||
-      hipStreamCreateWithFlags(&h->wstream, hipStreamNonBlocking) != hipSuccess ||
       ctx_init(h, h->sync) != 0) {
     emqxgm_destroy(h);
     return -EIO;
   }
+  h->wstream = h->sync.stream;
   h->geom = walk_geometry(h->cfg.device, h->cfg.walk_wg_per_cu);
   int rc = commit_locked(h);  // empty index: epoch 1
   if (rc) {
@@ -1883,7 +1904,6 @@ int emqxgm_create(const emqxgm_cfg* cfg, emqxgm_t** out) {
 void emqxgm_destroy(emqxgm_t* h) {
   if (!h) return;
   (void)hipSetDevice(h->cfg.device);
-  if (h->wstream) (void)hipStreamSynchronize(h->wstream);
   for (auto& p : h->pipes) ctx_free(p.c);
   for (auto& p : h->hpipes) host_pipe_free(p);
   ctx_free(h->sync);
@@ -1905,7 +1925,6 @@ void emqxgm_destroy(emqxgm_t* h) {
   if (h->d_rules.p) (void)hipFree(h->d_rules.p);
   if (h->d_in_bytes) (void)hipFree(h->d_in_bytes);
   if (h->d_in_off) (void)hipFree(h->d_in_off);
-  if (h->wstream) (void)hipStreamDestroy(h->wstream);
   delete h;
 }
 

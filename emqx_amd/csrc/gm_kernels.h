@@ -19,7 +19,7 @@ struct DevIndex {
   const uint32_t* rt_dst = nullptr;  // aggre entries (dest handles)
   const uint32_t* dl_sub = nullptr;  // local deliveries (subscriber ids)
   uint32_t fan_nf = 0;
-  // exact route-key buckets of XBUCKET {hash.lo, hash.hi, fid, len}: plain (non-wildcard) keys
+  // exact route-key buckets (gm_common.h "Exact route-key table"): plain (non-wildcard) keys
   // in buckets [0, xmask], wildcard keys in [xwbase, xwbase + xwmask]
   const uint4* exact = nullptr;
   uint64_t xmask = 0;             // plain region bucket count - 1
@@ -52,7 +52,8 @@ struct Scratch {
   uint32_t* rej = nullptr;    // [n]   rejected pairs per topic
   uint32_t* exact_id = nullptr;  // [n]
   uint32_t p_cap = 0;   // pair staging capacity
-  uint4* stg = nullptr;       // staged pairs {topic (NONE: unused), filter, rank | REJ_BIT, 0}
+  uint4* stg = nullptr;       // staged pairs {topic, filter, rank | REJ_BIT, 0}, CH-slot chunks
+  uint32_t* chk = nullptr;    // per staged chunk: pairs in it (written by the walk)
   uint32_t o_cap = 0;
   uint32_t* out = nullptr;    // [pairs] CSR filter ids
   uint32_t* out2 = nullptr;   // legacy fix-up target
@@ -92,6 +93,7 @@ constexpr uint32_t CENSUS_N = 4;
 constexpr uint32_t WALK_SHARDS = 8;
 constexpr uint32_t CTL_CLAIM_STRIDE = 32;
 
+constexpr uint32_t STAGE_CHUNK = 1024;  // staged-pair slots a walk wave reserves per atomic
 constexpr uint32_t REJ_BIT = 0x80000000u;
 constexpr uint32_t REJ_SCAN_MAX = 4096;  // rejects the deferred scatter handles in-line
 constexpr uint32_t WALK_LDS_STACK = 6;   // walk probe items per lane kept in LDS (rest spill)
@@ -113,9 +115,13 @@ hipError_t launch_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* 
                        uint32_t* total_dst, hipStream_t s);
 uint32_t scan_tmp_words(uint32_t n);
 // tokenise: levels (nw), 64-B topic records (rec: first REC_TOKS tokens inline), tokens of
-// deeper levels (wh, at off[t] + t + level), exact route-key ids (exact_id, NONE if absent)
+// deeper levels (wh, at off[t] + t + level); exact route-key ids (exact_id, NONE if absent)
+// of wildcard names when there are no plain keys, else X_WILDPEND marks for launch_exact
 hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
                       Scratch& sc, hipStream_t s);
+// exact route-key ids of every name (after launch_tok; a no-op when there are no plain keys)
+hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
+                        Scratch& sc, hipStream_t s);
 
 // Per-batch scratch of the publish fan-out (gm_fanout.inc).
 struct FanScratch {

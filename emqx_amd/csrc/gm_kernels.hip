@@ -1,8 +1,9 @@
 // gm_kernels.hip -- gfx950 (MI355X, CDNA4) kernels of the batched MQTT publish-match pipeline.
 //
 // Pipeline for one batch of N published topics (DESIGN.md "Kernels"):
-//   k_tok            levels, level tokens, wildcard/'$' flags, exact route-key probe
-//                    (one fused pass per 256-topic tile)                        (gm_tok.inc)
+//   k_tok            levels, level tokens, wildcard/'$' flags (one pass per 256-topic tile)
+//   k_exact          exact route-key probe of every name, when there are plain route keys
+//                                                                                (gm_tok.inc)
 //   k_walk           persistent trie walk, matches staged as (topic, filter, rank) (gm_walk.inc)
 //   k_verify         byte re-check of pairs whose filter has a hashed token   (gm_verify.inc)
 //   k_scan_*         per-topic match counts -> CSR row pointers
@@ -18,7 +19,7 @@ namespace gm {
 namespace {
 
 constexpr uint32_t WG = 256;
-constexpr uint32_t CH = 1024;     // staged-pair slots reserved per wave per atomic
+constexpr uint32_t CH = STAGE_CHUNK;  // staged-pair slots reserved per wave per atomic
 constexpr uint32_t TBLK = 128;    // topics claimed per wave per atomic
 constexpr uint32_t SCAN_ITEMS = 16;
 constexpr uint32_t SCAN_TILE = WG * SCAN_ITEMS;
@@ -234,6 +235,18 @@ hipError_t launch_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* 
   return hipGetLastError();
 }
 
+static ExactArgs exact_args(const DevIndex& ix) {
+  ExactArgs x;
+  x.exact = ix.exact;
+  x.xmask = ix.xmask;
+  x.xwbase = ix.xwbase;
+  x.xwmask = ix.xwmask;
+  x.fbytes = ix.fbytes;
+  x.foff = ix.foff;
+  x.full_mask = ix.full_mask;
+  return x;
+}
+
 hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
                       Scratch& sc, hipStream_t s) {
   if (n == 0) return hipSuccess;
@@ -245,21 +258,20 @@ hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, con
   a.wh = sc.wh;
   a.rec = sc.rec;
   a.exact_id = sc.exact_id;
-  a.exact = ix.exact;
-  a.xmask = ix.xmask;
-  a.fbytes = ix.fbytes;
-  a.foff = ix.foff;
-  a.fver = ix.fver;
   a.test_mask = ix.test_mask;
-  a.full_mask = ix.full_mask;
-  a.xwbase = ix.xwbase;
-  a.xwmask = ix.xwmask;
-  a.plain_empty = ix.plain_empty;
   a.wild_empty = ix.wild_empty;
   if (ix.plain_empty)
-    hipLaunchKernelGGL(k_tok<false>, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a);
+    hipLaunchKernelGGL(k_tok<false>, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a, exact_args(ix));
   else
-    hipLaunchKernelGGL(k_tok<true>, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a);
+    hipLaunchKernelGGL(k_tok<true>, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a, exact_args(ix));
+  return hipGetLastError();
+}
+
+hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
+                        Scratch& sc, hipStream_t s) {
+  if (n == 0 || ix.plain_empty) return hipSuccess;
+  hipLaunchKernelGGL(k_exact, dim3(grid_for(n, 1u << 20)), dim3(WG), 0, s, bytes, off, n,
+                     sc.exact_id, exact_args(ix), ix.wild_empty);
   return hipGetLastError();
 }
 
@@ -280,6 +292,7 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   a.ctl = sc.ctl;
   a.cnt = sc.cnt;
   a.stg = sc.stg;
+  a.chk = sc.chk;
   a.pcap = sc.p_cap;
   a.spill = sc.spill;
   a.spill_items = sc.spill_items;
@@ -314,6 +327,7 @@ hipError_t launch_verify(const uint8_t* bytes, const uint32_t* off, const DevInd
   a.fver = ix.fver;
   a.fvbits = ix.fvbits;
   a.stg = sc.stg;
+  a.chk = sc.chk;
   a.pcap = sc.p_cap;
   a.cnt = sc.cnt;
   a.rej = sc.rej;
@@ -328,6 +342,7 @@ hipError_t launch_scatter(Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_
   (void)n;
   ScatterArgs a;
   a.stg = sc.stg;
+  a.chk = sc.chk;
   a.pcap = sc.p_cap;
   a.row = sc.row;
   a.rej = sc.rej;
@@ -350,6 +365,7 @@ hipError_t launch_verify_scatter(const uint8_t* bytes, const uint32_t* off, cons
   a.foff = ix.foff;
   a.fvbits = ix.fvbits;
   a.stg = sc.stg;
+  a.chk = sc.chk;
   a.pcap = sc.p_cap;
   a.row = sc.row;
   a.out = sc.out;

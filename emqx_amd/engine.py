@@ -70,7 +70,8 @@ class _Stats(C.Structure):
                 ("reruns", C.c_uint64), ("walk_ms", C.c_double), ("walk_launches", C.c_uint64),
                 ("total_ms", C.c_double), ("full_commits", C.c_uint64),
                 ("delta_commits", C.c_uint64), ("last_commit_ms", C.c_double),
-                ("tok_ms", C.c_double), ("tok_launches", C.c_uint64)]
+                ("tok_ms", C.c_double), ("tok_launches", C.c_uint64),
+                ("exact_ms", C.c_double)]
 
 
 # name -> (restype, argtypes): exactly the entry points declared in include/emqx_gpumatch.h

@@ -127,6 +127,7 @@ typedef struct emqxgm_stats {
   double last_commit_ms;    /* host wall time of the last commit (build/patch + upload) */
   double tok_ms;            /* summed tokenizer-kernel time (HIP events), if profiling is on */
   uint64_t tok_launches;
+  double exact_ms;          /* summed exact route-key probe time (k_exact; 0 without plain keys) */
 } emqxgm_stats;
 
 int emqxgm_abi_version(void);

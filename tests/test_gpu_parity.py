@@ -427,6 +427,69 @@ def test_cfg4_exact_heavy_10m(emqx):
     assert (res.exact_id != emqx.NONE).mean() > 0.85
 
 
+def test_cfg4_full_size(emqx):
+    """BASELINE config 4 at its stated size: 100M exact dev/{id:09}/state route keys + 1M
+    wildcards, one 1M-topic batch.  Checked by properties over the whole batch and bit-exactly on
+    a 50k sample:
+    * the generator defines the exact key set (key i is dev/{i:09}/state, registered in order, so
+      its id is i): every topic's exact id is its own key's id, or NONE for an id past the keys;
+    * the hit rate is the generator's 90%;
+    * every exact hit's filter bytes are the topic's bytes;
+    * rows have no duplicate pair;
+    * a 50k-topic sample: trie rows and exact hits equal the C++ oracle's (built on the 1M
+      wildcards and the sample's keys; compared by filter bytes)."""
+    import workloads
+    w = workloads.generate(4)
+    n_wild = w.nf // 101
+    n_exact = w.nf - n_wild
+    eng = emqx.Engine()
+    eng.route_ref_many(w.fbytes, w.foff)
+    wi = np.arange(n_exact, w.nf)
+    wb, wo = _sample_filters(w, wi)
+    eng.trie_insert_many(wb, wo)
+    eng.commit()
+    res = eng.match_packed(w.tbytes, w.toff)
+    assert _rows_unique(res)
+    # topic t = b"dev/" + 9 digits + b"/state": its id from the digits
+    tb = w.tbytes.reshape(w.nt, 19)
+    assert np.all(np.diff(w.toff.astype(np.int64)) == 19)
+    digits = (tb[:, 4:13].astype(np.int64) - ord("0"))
+    ids = (digits * (10 ** np.arange(8, -1, -1, dtype=np.int64))).sum(1)
+    want = np.where(ids < n_exact, ids, emqx.NONE).astype(np.uint32)
+    assert np.array_equal(res.exact_id, want)
+    rate = float((res.exact_id != emqx.NONE).mean())
+    assert 0.89 < rate < 0.91, rate
+    hits = np.nonzero(res.exact_id != emqx.NONE)[0][::97]
+    assert eng.filters_bytes(res.exact_id[hits]) == [w.topic(int(i)) for i in hits]
+    # 50k-topic sample against the oracle
+    idx = np.arange(0, w.nt, 20)
+    sb, so = _sample_packed(w, idx)
+    ref = RefIndex(True)
+    ref.add_many(wb, wo, np.full(len(wi), 3, np.uint8))
+    keys = sorted({w.topic(int(i)) for i in idx if ids[i] < n_exact})
+    kb, ko = emqx.engine.pack(keys)
+    ref.add_many(kb, ko, np.full(len(keys), 2, np.uint8))
+    row, rid, rex = ref.match(sb, so, threads=16)
+    ref_names = [wb[int(wo[j]):int(wo[j + 1])].tobytes() for j in range(len(wi))] + keys
+    for j, i in enumerate(idx):
+        got = sorted(eng.filters_bytes(res.filter_id[res.row_ptr[i]:res.row_ptr[i + 1]]))
+        assert got == sorted(ref_names[int(f)] for f in rid[row[j]:row[j + 1]]), w.topic(int(i))
+        ex = int(res.exact_id[i])
+        assert (ex == emqx.NONE) == (int(rex[j]) == emqx.NONE)
+        if ex != emqx.NONE:
+            assert eng.filter_bytes(ex) == ref_names[int(rex[j])]
+    eng.close()
+
+
+def _sample_filters(w, idx):
+    lens = (w.foff[idx + 1] - w.foff[idx]).astype(np.int64)
+    off = np.zeros(len(idx) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    starts = w.foff[idx].astype(np.int64)
+    pos = np.repeat(starts - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(lens.sum())
+    return w.fbytes[pos], off
+
+
 def test_cfg4_slice_long_words(emqx):
     """cfg4 shape (dev/{id:09}/state exact keys + wildcards): 9-byte levels get hashed tokens,
     so these pairs go through byte verification in production mode."""
