@@ -444,6 +444,7 @@ struct emqxgm {
   PatchList patches;
   DevBuf d_patch;                   // device copy of the staged patch list
   DevBuf d_rules;                   // emqxgm_match_rules inputs and output
+  DevBuf d_merge;                   // emqxgm_merge pointer table and scratch
   uint8_t* h_stage = nullptr;       // pinned host staging of the patch list
   uint64_t h_stage_bytes = 0;
   hipEvent_t patch_ev = nullptr;    // the last patch upload + launch
@@ -1923,6 +1924,7 @@ void emqxgm_destroy(emqxgm_t* h) {
   if (h->h_stage) (void)hipHostFree(h->h_stage);
   if (h->patch_ev) (void)hipEventDestroy(h->patch_ev);
   if (h->d_rules.p) (void)hipFree(h->d_rules.p);
+  if (h->d_merge.p) (void)hipFree(h->d_merge.p);
   if (h->d_in_bytes) (void)hipFree(h->d_in_bytes);
   if (h->d_in_off) (void)hipFree(h->d_in_off);
   delete h;
@@ -2466,6 +2468,50 @@ int emqxgm_publish_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offs
   out->deliver_ptr = h->h_dp.data();
   out->deliver_filter = h->h_df.data();
   out->deliver_sub = h->h_ds.data();
+  return 0;
+}
+
+static int grow_buf(emqxgm* h, DevBuf& b, uint64_t bytes);
+
+int emqxgm_export(emqxgm_t* h, const emqxgm_dev_out* r, const uint32_t* id_map, uint32_t* row,
+                  uint32_t* fid, uint32_t* exact) {
+  if (!h || !r || !row || (r->n && !exact) || (r->n_pairs && !fid)) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mmu);
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
+  hipStream_t s = h->sync.stream;
+  HIPCHK(h, launch_export(r->row_ptr, r->filter_id, r->exact_id, r->n, r->n_pairs, id_map, row, fid,
+                          exact, s));
+  HIPCHK(h, hipStreamSynchronize(s));
+  return 0;
+}
+
+int emqxgm_merge(emqxgm_t* h, uint32_t parts, const uint32_t* const* rows,
+                 const uint32_t* const* fids, const uint32_t* const* exacts, uint32_t n,
+                 uint32_t* out_row, uint32_t* out_fid, uint32_t* out_exact, uint32_t* n_pairs) {
+  if (!h || !out_row || (parts && (!rows || !fids || !exacts)) || (n && !out_exact)) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mmu);
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
+  hipStream_t s = h->sync.stream;
+  const uint64_t tw = scan_tmp_words(std::max<uint32_t>(n, 1));
+  const uint64_t need = (3ull * parts + 1) * 8 + ((uint64_t)n + tw + 2) * 4;
+  if (int rc = grow_buf(h, h->d_merge, need)) return rc;
+  std::vector<const uint32_t*> pp(3ull * parts);
+  for (uint32_t i = 0; i < parts; ++i) {
+    pp[3 * i] = rows[i];
+    pp[3 * i + 1] = fids[i];
+    pp[3 * i + 2] = exacts[i];
+  }
+  uint8_t* d = (uint8_t*)h->d_merge.p;
+  uint32_t* cnt = (uint32_t*)(d + (3ull * parts + 1) * 8);
+  uint32_t* total = cnt + n;
+  uint32_t* tmp = total + 2;
+  if (parts) HIPCHK(h, hipMemcpyAsync(d, pp.data(), pp.size() * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(h, launch_merge((const uint32_t* const*)d, parts, n, cnt, tmp, out_row, out_fid, out_exact,
+                         total, s));
+  uint32_t tot = 0;
+  if (n) HIPCHK(h, hipMemcpyAsync(&tot, total, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(h, hipStreamSynchronize(s));
+  if (n_pairs) *n_pairs = tot;
   return 0;
 }
 

@@ -190,6 +190,15 @@ struct CopyOut {
   uint32_t cap;
 };
 hipError_t launch_copy_out(const CopyOut& a, const CopyOut& b, const CopyOut& c, hipStream_t s);
+// Filter-sharded layout: a shard's result copied with its ids mapped to global ids (map NULL:
+// identity), and np shards' results merged (parts: np x {row, fid, exact} device pointers, in
+// device memory); cnt/tmp: scratch of n / scan_tmp_words(n) words; *total = merged pairs.
+hipError_t launch_export(const uint32_t* row, const uint32_t* fid, const uint32_t* exact, uint32_t n,
+                         uint32_t pairs, const uint32_t* map, uint32_t* orow, uint32_t* ofid,
+                         uint32_t* oexact, hipStream_t s);
+hipError_t launch_merge(const uint32_t* const* parts, uint32_t np, uint32_t n, uint32_t* cnt,
+                        uint32_t* tmp, uint32_t* orow, uint32_t* ofid, uint32_t* oexact,
+                        uint32_t* total, hipStream_t s);
 // out[i] = base + row[i], i < m (u64 CSR row pointers of the host API, built on the device)
 hipError_t launch_row64(const uint32_t* row, uint64_t base, uint64_t* out, uint32_t m,
                         hipStream_t s);

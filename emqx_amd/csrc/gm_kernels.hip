@@ -195,6 +195,52 @@ __global__ __launch_bounds__(WG) void k_copy_out(CopyOut a0, CopyOut a1, CopyOut
   if (blockIdx.x == 0 && threadIdx.x < (n & 3u)) d.dst[4 * nv + threadIdx.x] = d.src[4 * nv + threadIdx.x];
 }
 
+// ---- filter-sharded layout: results of one shard exported with global ids, and the
+// shards' rows merged topic by topic (the shards are disjoint: nothing to dedupe) ----
+
+__global__ __launch_bounds__(WG) void k_export(const uint32_t* row, const uint32_t* fid,
+                                               const uint32_t* exact, uint32_t n, uint32_t pairs,
+                                               const uint32_t* map, uint32_t* orow,
+                                               uint32_t* ofid, uint32_t* oexact) {
+  const uint32_t m = max(n + 1, pairs);
+  for (uint32_t i = blockIdx.x * WG + threadIdx.x; i < m; i += gridDim.x * WG) {
+    if (i <= n) orow[i] = row[i];
+    if (i < n) {
+      const uint32_t e = exact[i];
+      oexact[i] = (map && e != NONE) ? map[e] : e;
+    }
+    if (i < pairs) ofid[i] = map ? map[fid[i]] : fid[i];
+  }
+}
+
+// parts[3 * r + {0, 1, 2}] = shard r's {row, fid, exact}
+__global__ __launch_bounds__(WG) void k_merge_count(const uint32_t* const* parts, uint32_t np,
+                                                    uint32_t n, uint32_t* cnt, uint32_t* exact) {
+  for (uint32_t t = blockIdx.x * WG + threadIdx.x; t < n; t += gridDim.x * WG) {
+    uint32_t c = 0, e = NONE;
+    for (uint32_t r = 0; r < np; ++r) {
+      const uint32_t* row = parts[3 * r];
+      c += row[t + 1] - row[t];
+      e = min(e, parts[3 * r + 2][t]);  // a route key lives on exactly one shard
+    }
+    cnt[t] = c;
+    exact[t] = e;
+  }
+}
+
+__global__ __launch_bounds__(WG) void k_merge_fill(const uint32_t* const* parts, uint32_t np,
+                                                   uint32_t n, const uint32_t* orow,
+                                                   uint32_t* ofid) {
+  for (uint32_t t = blockIdx.x * WG + threadIdx.x; t < n; t += gridDim.x * WG) {
+    uint32_t d = orow[t];
+    for (uint32_t r = 0; r < np; ++r) {
+      const uint32_t* row = parts[3 * r];
+      const uint32_t* fid = parts[3 * r + 1];
+      for (uint32_t i = row[t], e = row[t + 1]; i < e; ++i) ofid[d++] = fid[i];
+    }
+  }
+}
+
 uint32_t grid_for(uint64_t items, uint32_t cap_blocks) {
   uint64_t b = (items + WG - 1) / WG;
   if (b == 0) b = 1;
@@ -382,6 +428,27 @@ hipError_t launch_fixup(Scratch& sc, uint32_t n, hipStream_t s) {
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_compact_rows, dim3(grid_for(n, 4096)), dim3(WG), 0, s, sc.row, sc.out,
                      sc.row2, sc.out2, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_export(const uint32_t* row, const uint32_t* fid, const uint32_t* exact, uint32_t n,
+                         uint32_t pairs, const uint32_t* map, uint32_t* orow, uint32_t* ofid,
+                         uint32_t* oexact, hipStream_t s) {
+  hipLaunchKernelGGL(k_export, dim3(grid_for((uint64_t)n + 1 + pairs, 8192)), dim3(WG), 0, s, row,
+                     fid, exact, n, pairs, map, orow, ofid, oexact);
+  return hipGetLastError();
+}
+
+hipError_t launch_merge(const uint32_t* const* parts, uint32_t np, uint32_t n, uint32_t* cnt,
+                        uint32_t* tmp, uint32_t* orow, uint32_t* ofid, uint32_t* oexact,
+                        uint32_t* total, hipStream_t s) {
+  if (n == 0) return hipMemsetAsync(orow, 0, 4, s);
+  hipLaunchKernelGGL(k_merge_count, dim3(grid_for(n, 8192)), dim3(WG), 0, s, parts, np, n, cnt,
+                     oexact);
+  hipError_t e = launch_scan(cnt, orow, n, tmp, total, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_merge_fill, dim3(grid_for(n, 8192)), dim3(WG), 0, s, parts, np, n, orow,
+                     ofid);
   return hipGetLastError();
 }
 

@@ -1,22 +1,31 @@
 """Multi-GPU layouts of the match path (one process per GPU, torch.distributed).
 
 ``shard="filters"`` (the north-star layout): the subscription set is partitioned by
-``hash(filter) mod G``; every rank holds the trie + route keys of its shard.  Per batch, rank 0
-broadcasts the packed topic batch (RCCL over xGMI), each rank matches it against its shard,
-and the per-rank CSR results are gathered to rank 0 and merged (a topic's row is the union of
-its rows on every shard; shards are disjoint, so there is nothing to dedupe).
+``hash(filter) mod G``; every rank holds the trie + route keys of its shard.  Per batch:
+
+1. rank 0 broadcasts the packed topic batch (RCCL over xGMI);
+2. every rank matches it against its shard on its GPU and exports the CSR with its local filter
+   ids mapped to global ids (``emqxgm_export``, one kernel);
+3. the ranks' pair counts are exchanged with one all_gather of G integers, and rank 0 receives
+   each rank's CSR with sized point-to-point receives (``batch_isend_irecv``: grouped
+   send/recv, each rank's list crosses xGMI once, only to rank 0);
+4. rank 0 merges the G CSRs topic by topic in a HIP kernel (``emqxgm_merge``: shards are
+   disjoint, nothing to dedupe; a topic's exact route key lives on exactly one shard).
+
+Host synchronisations per step: the batch size on the receiving ranks (step 1), the match pass
+itself, and the pair counts on rank 0 (step 3).
 
 ``shard="topics"`` (replicas): every rank holds the whole index (it fits: SURVEY 8e capacity
 note) and matches its own batch; no collective is on the data path.
 
-The collective code is device-agnostic: with the gloo backend the same functions run on CPU
-tensors, which is how tests/test_dist.py covers world_size 2 without a GPU (there the per-rank
-matcher is injected by the test).
+The collective code (broadcast_batch, gather_to_root) is device-agnostic: with the gloo backend
+it runs on CPU tensors, which is how tests/test_dist.py covers world_size 2 without a GPU (the
+per-rank matcher and the merge there are the test's own).  The merge (merge_parts) is HIP only.
 """
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Optional
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -51,85 +60,136 @@ def filter_shards(fbytes: np.ndarray, foff: np.ndarray, world: int) -> np.ndarra
     return (h % np.uint64(world)).astype(np.int64)
 
 
-@dataclass
-class Merged:
-    row_ptr: torch.Tensor    # int64 [n+1]
-    filter_id: torch.Tensor  # int64 [pairs] global filter ids
-    exact_id: torch.Tensor   # int64 [n] global id or NONE
+def _comm_on_cpu(group=None) -> bool:
+    """gloo moves CPU tensors only (its CUDA support stops at a few collectives): a gloo
+    rehearsal of the N>1 path stages its messages through host memory."""
+    return dist.get_backend(group) == "gloo"
 
 
 def broadcast_batch(tbytes: Optional[torch.Tensor], toff: Optional[torch.Tensor], device,
                     src: int = 0, group=None):
     """Rank `src` broadcasts the packed topic batch (u8 bytes, i32 offsets) to every rank."""
-    meta = torch.zeros(2, dtype=torch.int64, device=device)
+    cpu = _comm_on_cpu(group)
+    cdev = "cpu" if cpu else device
+    meta = torch.zeros(2, dtype=torch.int64, device=cdev)
     if dist.get_rank(group) == src:
         meta[0] = tbytes.numel()
         meta[1] = toff.numel()
     dist.broadcast(meta, src, group=group)
     nb, no = int(meta[0]), int(meta[1])
     if dist.get_rank(group) != src:
-        tbytes = torch.empty(nb, dtype=torch.uint8, device=device)
-        toff = torch.empty(no, dtype=torch.int32, device=device)
+        tbytes = torch.empty(nb, dtype=torch.uint8, device=cdev)
+        toff = torch.empty(no, dtype=torch.int32, device=cdev)
+    else:
+        tbytes, toff = tbytes.to(cdev), toff.to(cdev)
     if nb:
         dist.broadcast(tbytes, src, group=group)
     dist.broadcast(toff, src, group=group)
-    return tbytes, toff
+    return tbytes.to(device), toff.to(device)
 
 
-def gather_merge(row: torch.Tensor, gid: torch.Tensor, exact: torch.Tensor, dst: int = 0,
-                 group=None) -> Optional[Merged]:
-    """Gather each rank's CSR (row int64[n+1], gid int64[pairs], exact int64[n]) to `dst` and
-    merge rows topic by topic.  Returns the merged result on `dst`, None elsewhere."""
+Part = Tuple[torch.Tensor, torch.Tensor, torch.Tensor]  # (row [n+1], fid [pairs], exact [n])
+
+
+def gather_to_root(row: torch.Tensor, fid: torch.Tensor, exact: torch.Tensor, n_pairs: int,
+                   root: int = 0, group=None) -> Optional[List[Part]]:
+    """Each rank's CSR (int32 row [n+1], fid [>= n_pairs], exact [n]) to `root`: the pair counts
+    with one all_gather of G integers, then sized point-to-point receives on the root only.
+    Returns on the root the G parts in rank order (its own included), None elsewhere."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    device = row.device
-    n = row.numel() - 1
-    sizes = torch.tensor([gid.numel()], dtype=torch.int64, device=device)
-    all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
-    dist.all_gather(all_sizes, sizes, group=group)
-    maxp = int(max(int(s) for s in all_sizes))
-    pad = torch.full((maxp,), -1, dtype=torch.int64, device=device)
-    pad[: gid.numel()] = gid
-    rows = [torch.zeros_like(row) for _ in range(world)]
-    gids = [torch.zeros_like(pad) for _ in range(world)]
-    exs = [torch.zeros_like(exact) for _ in range(world)]
-    # all_gather works on every backend (gloo and RCCL); only dst keeps the merge
-    dist.all_gather(rows, row, group=group)
-    dist.all_gather(gids, pad, group=group)
-    dist.all_gather(exs, exact, group=group)
-    if rank != dst:
+    dev = row.device
+    cpu = _comm_on_cpu(group)
+    cdev = "cpu" if cpu else dev
+    cnt = torch.tensor([n_pairs], dtype=torch.int64, device=cdev)
+    allc = [torch.zeros(1, dtype=torch.int64, device=cdev) for _ in range(world)]
+    dist.all_gather(allc, cnt, group=group)
+    fid = fid[:n_pairs]
+    if rank != root:
+        ops = [dist.P2POp(dist.isend, row.to(cdev), root, group),
+               dist.P2POp(dist.isend, exact.to(cdev), root, group)]
+        if n_pairs:
+            ops.append(dist.P2POp(dist.isend, fid.to(cdev), root, group))
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
         return None
-    counts = torch.stack([r[1:] - r[:-1] for r in rows])          # [world, n]
-    total = counts.sum(0)
-    out_row = torch.zeros(n + 1, dtype=torch.int64, device=device)
-    out_row[1:] = torch.cumsum(total, 0)
-    before = torch.cumsum(counts, 0) - counts                    # pairs of lower ranks per topic
-    out = torch.empty(int(out_row[-1]), dtype=torch.int64, device=device)
-    ar = torch.arange(n, device=device)
+    counts = [int(c) for c in torch.cat(allc).tolist()]
+    parts: List[Part] = []
+    ops = []
     for r in range(world):
-        c = counts[r]
-        p = int(all_sizes[r])
-        if p == 0:
+        if r == root:
+            parts.append((row, fid, exact))
             continue
-        topic = torch.repeat_interleave(ar, c)
-        j = torch.arange(p, device=device) - rows[r][:-1][topic]
-        out[out_row[:-1][topic] + before[r][topic] + j] = gids[r][:p]
-    ex = torch.stack(exs).min(0).values  # a route key lives on exactly one shard
-    return Merged(out_row, out, ex)
+        rr = torch.empty(row.numel(), dtype=row.dtype, device=cdev)
+        ee = torch.empty(exact.numel(), dtype=exact.dtype, device=cdev)
+        ff = torch.empty(counts[r], dtype=fid.dtype, device=cdev)
+        ops += [dist.P2POp(dist.irecv, rr, r, group), dist.P2POp(dist.irecv, ee, r, group)]
+        if counts[r]:
+            ops.append(dist.P2POp(dist.irecv, ff, r, group))
+        parts.append((rr, ff, ee))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    return [(a.to(dev), b.to(dev), c.to(dev)) for a, b, c in parts]
 
 
-def device_result_to_torch(engine, dres, device) -> tuple:
-    """Copy an engine's device-resident result into torch tensors on `device` (D2D)."""
-    import ctypes
-    hip = ctypes.CDLL("libamdhip64.so")
-    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-    n, p = dres.n, dres.n_pairs
-    row = torch.empty(n + 1, dtype=torch.int32, device=device)
-    fid = torch.empty(max(p, 1), dtype=torch.int32, device=device)
-    ex = torch.empty(max(n, 1), dtype=torch.int32, device=device)
-    for dst, src, nb in ((row, dres.row_ptr, (n + 1) * 4), (fid, dres.filter_id, p * 4),
-                         (ex, dres.exact_id, n * 4)):
-        if nb and hip.hipMemcpy(dst.data_ptr(), src, nb, 3) != 0:
-            raise RuntimeError("hipMemcpy D2D failed")
-    u32 = lambda t: t.to(torch.int64) & 0xFFFFFFFF  # noqa: E731
-    return u32(row), u32(fid[:p]), u32(ex[:n])
+@dataclass
+class Merged:
+    row_ptr: torch.Tensor    # int32 [n+1]
+    filter_id: torch.Tensor  # int32 [pairs] global filter ids (u32 bits)
+    exact_id: torch.Tensor   # int32 [n] global id or NONE (u32 bits)
+
+
+def merge_parts(eng, parts: Sequence[Part], n: int) -> Merged:
+    """Merge the shards' CSRs topic by topic on the device (emqxgm_merge, a HIP kernel)."""
+    dev = parts[0][0].device
+    if dev.type != "cuda":
+        raise RuntimeError("merge_parts runs on the GPU (emqxgm_merge); there is no CPU merge")
+    total = sum(int(p[1].numel()) for p in parts)
+    row = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    fid = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
+    ex = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    torch.cuda.current_stream(dev).synchronize()  # the parts came in on torch's streams
+    got = eng.merge([p[0].data_ptr() for p in parts],
+                    [p[1].data_ptr() if p[1].numel() else 0 for p in parts],
+                    [p[2].data_ptr() for p in parts], n, row.data_ptr(),
+                    fid.data_ptr() if total else 0, ex.data_ptr())
+    assert got == total, (got, total)
+    return Merged(row, fid[:total], ex[:n])
+
+
+class ShardedMatcher:
+    """The filter-sharded match step of one rank: `eng` holds this rank's filter
+    shard, `gid_map` (int32 device tensor) maps its local filter ids to global ids."""
+
+    def __init__(self, eng, gid_map: torch.Tensor, device, group=None, root: int = 0):
+        self.eng = eng
+        self.gid_map = gid_map
+        self.device = device
+        self.group = group
+        self.root = root
+        self._bufs = None
+
+    def _out(self, n: int, pairs: int):
+        cap_n, cap_p = (0, 0) if self._bufs is None else (self._bufs[2].numel(), self._bufs[1].numel())
+        if n + 1 > cap_n or pairs > cap_p:
+            self._bufs = (torch.empty(max(n + 1, cap_n), dtype=torch.int32, device=self.device),
+                          torch.empty(max(pairs, cap_p, 1), dtype=torch.int32, device=self.device),
+                          torch.empty(max(n + 1, cap_n), dtype=torch.int32, device=self.device))
+        row, fid, ex = self._bufs
+        return row[: n + 1], fid, ex[:n]
+
+    def step(self, tbytes: Optional[torch.Tensor] = None,
+             toff: Optional[torch.Tensor] = None) -> Optional[Merged]:
+        """One batch (given on the root): broadcast, match this shard, gather, merge on root."""
+        b, o = broadcast_batch(tbytes, toff, self.device, self.root, self.group)
+        n = o.numel() - 1
+        torch.cuda.current_stream(self.device).synchronize()  # the engine's stream reads them
+        r = self.eng.match_device(b.data_ptr(), o.data_ptr(), n, b.numel())
+        row, fid, ex = self._out(n, r.n_pairs)
+        self.eng.export(r, self.gid_map.data_ptr(), row.data_ptr(),
+                        fid.data_ptr() if r.n_pairs else 0, ex.data_ptr() if n else 0)
+        parts = gather_to_root(row, fid, ex, r.n_pairs, self.root, self.group)
+        if parts is None:
+            return None
+        return merge_parts(self.eng, parts, n)

@@ -105,6 +105,8 @@ SYMBOLS = {
     "emqxgm_match_batch_submit": (C.c_int, [_P, _P, _P, C.c_uint32, _U64P]),
     "emqxgm_match_batch_wait": (C.c_int, [_P, C.c_uint64, C.POINTER(_BatchOut)]),
     "emqxgm_walk_census": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, _U64P]),
+    "emqxgm_export": (C.c_int, [_P, C.POINTER(_DevOut), _P, _P, _P, _P]),
+    "emqxgm_merge": (C.c_int, [_P, C.c_uint32, _P, _P, _P, C.c_uint32, _P, _P, _P, _U32P]),
     "emqxgm_route_add": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32]),
     "emqxgm_route_delete": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32]),
     "emqxgm_set_local_node": (C.c_int, [_P, C.c_uint32]),
@@ -450,6 +452,28 @@ class Engine:
         if copy:
             return MatchResult(row.astype(np.uint64), fid.copy(), ex.copy())
         return MatchResult(row, fid, ex)
+
+    def export(self, r: "DeviceResult", id_map: int, row: int, fid: int, exact: int) -> None:
+        """emqxgm_export: copy a device-resident result into device buffers (pointers), ids
+        mapped through the device array id_map (0 = identity)."""
+        o = _DevOut(r.n, r.n_pairs, r.row_ptr or None, r.filter_id or None, r.exact_id or None,
+                    r.n_words or None)
+        self._check(self._lib.emqxgm_export(self._h, C.byref(o), C.c_void_p(id_map or None),
+                                            C.c_void_p(row), C.c_void_p(fid or None),
+                                            C.c_void_p(exact or None)), "export")
+
+    def merge(self, rows: Sequence[int], fids: Sequence[int], exacts: Sequence[int], n: int,
+              out_row: int, out_fid: int, out_exact: int) -> int:
+        """emqxgm_merge: merge per-shard device CSRs (device pointers) into out_*; returns the
+        merged pair count."""
+        k = len(rows)
+        arr = C.c_void_p * max(k, 1)
+        tot = C.c_uint32(0)
+        self._check(self._lib.emqxgm_merge(self._h, k, arr(*rows), arr(*[f or None for f in fids]),
+                                           arr(*exacts), n, C.c_void_p(out_row),
+                                           C.c_void_p(out_fid or None), C.c_void_p(out_exact or None),
+                                           C.byref(tot)), "merge")
+        return int(tot.value)
 
     def walk_census(self, d_bytes: int, d_off: int, n: int, bytes_len: int) -> dict:
         """Instrumented pass: {'states': sum S(t), 'slot_loads', 'pairs', 'words',

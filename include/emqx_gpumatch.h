@@ -304,6 +304,21 @@ typedef struct emqxgm_retain_out { /* host-resident, valid until the next call o
 int emqxgm_retain_match(emqxgm_retain_t* r, const uint8_t* bytes, const uint32_t* offsets,
                         uint32_t n, uint64_t now_ms, emqxgm_retain_out* out);
 
+/* ---- filter-sharded layout over several GPUs (the subscription set partitioned by
+ * filter, the topic batch broadcast, the per-GPU match lists gathered to one GPU) ----
+ * emqxgm_export copies a device-resident result (emqxgm_match_device / _wait) into the caller's
+ * device buffers (row [n+1], fid [n_pairs], exact [n]), mapping filter and exact ids through
+ * id_map (device u32 array, local id -> global id; NULL = identity; NONE stays NONE).
+ * emqxgm_merge merges `parts` such results of one batch (rows/fids/exacts: host arrays of device
+ * pointers) into one CSR on the handle's device: topic t's row is shard 0's row, then shard 1's,
+ * ...; its exact id the one shard's that has it.  out_fid holds the sum of the parts' pairs;
+ * *n_pairs = that sum.  Both calls return when the device work is complete. */
+int emqxgm_export(emqxgm_t* h, const emqxgm_dev_out* r, const uint32_t* id_map, uint32_t* row,
+                  uint32_t* fid, uint32_t* exact);
+int emqxgm_merge(emqxgm_t* h, uint32_t parts, const uint32_t* const* rows,
+                 const uint32_t* const* fids, const uint32_t* const* exacts, uint32_t n,
+                 uint32_t* out_row, uint32_t* out_fid, uint32_t* out_exact, uint32_t* n_pairs);
+
 /* Diagnostic pass (instrumented walk kernel, not the production launch): runs the device
  * match and returns out[0] = trie states matched (SURVEY 8d S(t) summed over the batch),
  * out[1] = edge slots loaded, out[2] = pairs, out[3] = levels (words) in the batch,

@@ -1,0 +1,148 @@
+"""The filter-sharded layout's device side (emqx_amd/dist.py): emqxgm_export (a
+shard's CSR with global ids) and emqxgm_merge (G shards merged topic by topic on the device),
+checked against tests/test_dist.py's restatement _ref_merge, and the whole ShardedMatcher step
+rehearsed with two ranks sharing this box's GPU (gloo: RCCL refuses two ranks on one device)
+against the unsharded oracle."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from tests.test_dist import _ref_merge, _subset
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def emqx():
+    assert torch.cuda.is_available(), "gpu tests need the MI355X"
+    import emqx_amd
+    return emqx_amd
+
+
+def _rand_part(rng, n, nf, has_exact):
+    cnt = rng.integers(0, 5, n)
+    row = np.zeros(n + 1, np.uint32)
+    np.cumsum(cnt, out=row[1:])
+    fid = rng.integers(0, nf, int(row[-1])).astype(np.uint32)
+    ex = np.where(has_exact, rng.integers(0, nf, n), 0xFFFFFFFF).astype(np.uint32)
+    t = lambda a: torch.from_numpy(a.view(np.int32)).cuda()  # noqa: E731
+    return t(row), t(fid), t(ex)
+
+
+def test_merge_matches_reference(emqx):
+    from emqx_amd import dist as D
+    eng = emqx.Engine()
+    rng = np.random.default_rng(1)
+    for n, g in ((0, 2), (1, 1), (1000, 3), (70000, 8)):
+        owner = rng.integers(-1, g, n)  # which shard (if any) holds the topic's exact key
+        parts = [_rand_part(rng, n, 10 ** 6, owner == r) for r in range(g)]
+        m = D.merge_parts(eng, parts, n)
+        cpu = [tuple(x.cpu() for x in p) for p in parts]
+        row, fid, ex = _ref_merge(cpu, n)
+        assert np.array_equal(m.row_ptr.cpu().numpy().view(np.uint32).astype(np.int64), row)
+        assert np.array_equal(m.filter_id.cpu().numpy().view(np.uint32).astype(np.int64), fid)
+        assert np.array_equal(m.exact_id.cpu().numpy().view(np.uint32).astype(np.int64), ex)
+    eng.close()
+
+
+def test_export_maps_ids(emqx):
+    eng = emqx.Engine()
+    fs = [b"a/+", b"a/#", b"+/b", b"a/b"]
+    ids = [eng.trie_insert(f) for f in fs[:3]] + [eng.route_ref(fs[3])]
+    eng.commit()
+    topics = [b"a/b", b"a/c", b"x/b", b"q"]
+    buf, off = emqx.engine.pack(topics, np.uint32)
+    db = torch.from_numpy(buf).cuda()
+    do = torch.from_numpy(off.view(np.int32)).cuda()
+    torch.cuda.synchronize()
+    r = eng.match_device(db.data_ptr(), do.data_ptr(), len(topics), int(off[-1]))
+    gmap = np.full(max(ids) + 1, 0xFFFFFFFF, np.uint32)
+    gmap[ids] = [100, 200, 300, 400]
+    gm = torch.from_numpy(gmap.view(np.int32)).cuda()
+    row = torch.empty(len(topics) + 1, dtype=torch.int32, device="cuda")
+    fid = torch.empty(r.n_pairs, dtype=torch.int32, device="cuda")
+    ex = torch.empty(len(topics), dtype=torch.int32, device="cuda")
+    eng.export(r, gm.data_ptr(), row.data_ptr(), fid.data_ptr(), ex.data_ptr())
+    row, fid = row.cpu().numpy(), fid.cpu().numpy().view(np.uint32)
+    rows = [sorted(fid[row[i]:row[i + 1]].tolist()) for i in range(len(topics))]
+    assert rows == [[100, 200, 300], [100, 200], [300], []]
+    assert ex.cpu().numpy().view(np.uint32).tolist() == [400, 0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF]
+    eng.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import workloads
+        from emqx_amd import Engine
+        from emqx_amd import dist as D
+        from oracle.cref import RefIndex
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        w = workloads.generate(2, 30000, 5000)
+        mine = np.nonzero(D.filter_shards(w.fbytes, w.foff, world) == rank)[0]
+        fb, fo = _subset(w, mine)
+        eng = Engine()
+        rid = eng.route_ref_many(fb, fo)
+        wsel = np.nonzero(w.fwild[mine])[0]
+        wb, wo = _subset(type("W", (), {"fbytes": fb, "foff": fo})(), wsel)
+        tid = eng.trie_insert_many(wb, wo)
+        eng.commit()
+        gid = np.full(int(max(rid.max(), tid.max(initial=0))) + 1, 0xFFFFFFFF, np.uint32)
+        gid[rid] = mine
+        gid[tid] = mine[wsel]
+        sm = D.ShardedMatcher(eng, torch.from_numpy(gid.view(np.int32)).to(dev), dev)
+        tb = torch.from_numpy(w.tbytes).to(dev) if rank == 0 else None
+        to = torch.from_numpy(w.toff.view(np.int32)).to(dev) if rank == 0 else None
+        for _ in range(2):  # twice: buffers are reused across steps
+            m = sm.step(tb, to)
+        if rank == 0:
+            full = RefIndex(True)
+            full.add_many(w.fbytes, w.foff, 2 + w.fwild)
+            frow, fids, fex = full.match(w.tbytes, w.toff)
+            row = m.row_ptr.cpu().numpy().astype(np.int64)
+            got = m.filter_id.cpu().numpy().view(np.uint32)
+            ok = np.array_equal(row, frow.astype(np.int64))
+            for t in range(w.nt):
+                a, b = int(frow[t]), int(frow[t + 1])
+                ok = ok and np.array_equal(np.sort(got[a:b]), fids[a:b])
+            ok = ok and np.array_equal(m.exact_id.cpu().numpy().view(np.uint32), fex)
+            q.put(("ok" if ok else "mismatch", int(frow[-1]), len(mine)))
+        else:
+            assert m is None
+        eng.close()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put(("error", repr(e), 0))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(400)
+def test_sharded_matcher_two_ranks_one_gpu(emqx):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(360)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    status, pairs, on_rank0 = q.get(timeout=5)
+    assert status == "ok", status
+    assert pairs > 0 and on_rank0 > 0
