@@ -8,10 +8,10 @@ The product is ``libemqx_gpumatch.so`` (gfx950 HIP kernels + host index builder 
 """
 from .broker import Broker  # noqa: F401
 from .engine import NONE, DeviceResult, Engine, EngineError, MatchResult, PublishResult  # noqa: F401
-from .router import Router  # noqa: F401
+from .router import Router, SessionRouter  # noqa: F401
 from .retainer import Retainer  # noqa: F401
 from .rules import TopicRules  # noqa: F401
 from .trie import Trie  # noqa: F401
 
 __all__ = ["Engine", "EngineError", "MatchResult", "DeviceResult", "PublishResult", "Trie",
-           "Router", "Broker", "TopicRules", "Retainer", "NONE"]
+           "Router", "SessionRouter", "Broker", "TopicRules", "Retainer", "NONE"]

@@ -135,6 +135,10 @@ GM_HD uint64_t edge_slot(uint32_t parent, uint64_t tok, uint64_t mask) {
 //   e1 = {key bytes 4..7, 8..11, 12..15, 16..19}   (zero past len)
 // A longer key's inline prefix and hash filter the candidates and its full bytes (verification
 // record / string pool) confirm.  An empty entry has fid == NONE, a deleted one fid == TOMB.
+// A bit per bucket (xovf) says whether some key whose probe passed it was placed beyond it: a
+// probe that finds neither its key nor an empty entry in a bucket goes on only if the bit is
+// set, so a miss costs its home bucket's line (plus the bit word, loaded beside it) even when
+// that bucket is full.  Bits are only set (a delta commit may leave one set after deletions).
 constexpr uint32_t XBUCKET = 2;
 constexpr uint32_t XENT_U4 = 2;
 constexpr uint32_t XINL = 20;

@@ -247,7 +247,7 @@ struct TrieModel {
   // table: plain (non-wildcard) keys in buckets [0, xcap_p), wildcard keys in [xcap_p,
   // xcap_p + xcap_w); a name can only equal a key of its own kind (same bytes, same words).
   std::vector<uint32_t> xpos;
-  std::vector<uint64_t> xocc, xtomb;
+  std::vector<uint64_t> xocc, xtomb, xovf;  // xovf: a bit per bucket (gm_common.h)
   uint64_t xcap_p = 0, xcap_w = 0, x_occ_p = 0, x_occ_w = 0, n_route_p = 0, n_route_w = 0;
   uint64_t xbase(bool w) const { return w ? xcap_p : 0; }
   uint64_t xcapr(bool w) const { return w ? xcap_w : xcap_p; }
@@ -259,7 +259,8 @@ struct TrieModel {
     return xbase(w) + ((b - xbase(w) + 1) & (xcapr(w) - 1));
   }
   // device tables patched in place (owned by emqxgm::o_tab)
-  uint32_t *d_edges = nullptr, *d_exact = nullptr, *d_tn = nullptr, *d_fv = nullptr;
+  uint32_t *d_edges = nullptr, *d_exact = nullptr, *d_tn = nullptr, *d_fv = nullptr,
+           *d_xovf = nullptr;
 
   uint32_t cf(uint32_t i) const {  // gm_common.h cf: id | flags
     uint32_t f = i;
@@ -937,6 +938,7 @@ int commit_full(emqxgm* h) {
   const uint64_t xcap = m.xcap_p + m.xcap_w;
   m.xocc.assign(xcap * XBUCKET / 64 + 1, 0ull);
   m.xtomb.assign(xcap * XBUCKET / 64 + 1, 0ull);
+  m.xovf.assign(xcap / 64 + 1, 0ull);
   m.xpos.assign(nf, NONE);
   std::vector<uint4> xslots(xcap * XBUCKET * XENT_U4, make_uint4(0u, 0u, 0u, 0u));
   for (uint64_t e = 0; e < xcap * XBUCKET; ++e) xslots[XENT_U4 * e].y = NONE;
@@ -956,6 +958,7 @@ int commit_full(emqxgm* h) {
         m.xpos[id] = (uint32_t)e;
         break;
       }
+      bset(m.xovf, b);  // the key goes on past this full bucket
       b = m.xnext(w, b);
     }
   }
@@ -972,7 +975,8 @@ int commit_full(emqxgm* h) {
       (rc = dev_upload(h, nbufs, multi, &nx.multi)) ||
       (rc = dev_upload(h, nbufs, tn_of, &nx.tn_of)) ||
       (rc = dev_upload(h, nbufs, m.fvbits, &nx.fvbits)) ||
-      (rc = dev_upload(h, nbufs, xslots, &nx.exact))) {
+      (rc = dev_upload(h, nbufs, xslots, &nx.exact)) ||
+      (rc = dev_upload(h, nbufs, m.xovf, (const uint64_t**)&nx.xovf))) {
     free_bufs(nbufs);
     return rc;
   }
@@ -980,6 +984,7 @@ int commit_full(emqxgm* h) {
   m.d_exact = (uint32_t*)nx.exact;
   m.d_tn = (uint32_t*)nx.tn_of;
   m.d_fv = (uint32_t*)nx.fvbits;
+  m.d_xovf = (uint32_t*)nx.xovf;
   nx.emask = m.nbk - 1;
   nx.xmask = m.xcap_p - 1;
   nx.xwbase = m.xcap_p;
@@ -1040,6 +1045,7 @@ int commit_delta(emqxgm* h) {
   std::unordered_map<uint64_t, XE> xpatch;        // exact entry -> content
   std::vector<uint32_t> dirty;                    // nodes whose slot / side entry changed
   std::vector<uint32_t> fv_words;  // changed words of the verify bitmap
+  std::vector<uint32_t> ovf_words; // changed words of the exact table's overflow bitmap
   std::vector<uint64_t> toks;
   std::vector<uint8_t> is_plus, is_hash;
   std::vector<uint32_t> path;
@@ -1175,6 +1181,10 @@ int commit_delta(emqxgm* h) {
           e = q;
         }
       }
+      if (e == DEAD && !bit(m.xovf, b)) {  // the key goes on past this full bucket
+        bset(m.xovf, b);
+        ovf_words.push_back((uint32_t)(b >> 5));
+      }
       b = m.xnext(w, b);
     }
     xent(fh, id, h->pool.data() + f.off, f.len, xpatch[e].e);
@@ -1208,6 +1218,12 @@ int commit_delta(emqxgm* h) {
   std::sort(fv_words.begin(), fv_words.end());
   fv_words.erase(std::unique(fv_words.begin(), fv_words.end()), fv_words.end());
   for (uint32_t w : fv_words) pl.add(m.d_fv + w, &m.fvbits[w], 1);
+  std::sort(ovf_words.begin(), ovf_words.end());
+  ovf_words.erase(std::unique(ovf_words.begin(), ovf_words.end()), ovf_words.end());
+  for (uint32_t w : ovf_words) {
+    const uint32_t v = (uint32_t)(m.xovf[w >> 1] >> (32 * (w & 1)));
+    pl.add(m.d_xovf + w, &v, 1);
+  }
   int rc = 0;
   if ((rc = upload_pool(h, &pl)) || (rc = fan_commit(h))) return rc;
 
@@ -1376,6 +1392,9 @@ int ensure_scratch(emqxgm* h, PassCtx& c, uint32_t n, uint64_t words, uint32_t p
       (rc = dev_alloc(h, c, (void**)&s.row2, (size_t)(ncap + 1) * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.rej, (size_t)ncap * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.exact_id, (size_t)ncap * 4)) ||
+      (rc = dev_alloc(h, c, (void**)&s.xbin, (size_t)ncap)) ||
+      (rc = dev_alloc(h, c, (void**)&s.xord, (size_t)ncap * 4)) ||
+      (rc = dev_alloc(h, c, (void**)&s.xcnt, 2 * (XBINS + 1) * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.stg, (size_t)pcap * 16)) ||
       (rc = dev_alloc(h, c, (void**)&s.chk, (size_t)(pcap / STAGE_CHUNK + 1) * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.out, (size_t)pcap * 4)) ||
@@ -1447,7 +1466,7 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
                              st));
   HIPCHK(h, launch_tok(d_bytes, d_off, n, ix, s, st));
   if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[4], st));
-  HIPCHK(h, launch_exact(d_bytes, d_off, n, ix, s, st));
+  HIPCHK(h, launch_exact(d_bytes, d_off, n, ix, s, h->geom, st));
   if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[1], st));
   if (ix.trie_empty) {
     HIPCHK(h, hipMemsetAsync(s.row, 0, (size_t)(n + 1) * 4, st));

@@ -22,6 +22,7 @@ struct DevIndex {
   // exact route-key buckets (gm_common.h "Exact route-key table"): plain (non-wildcard) keys
   // in buckets [0, xmask], wildcard keys in [xwbase, xwbase + xwmask]
   const uint4* exact = nullptr;
+  const uint32_t* xovf = nullptr;  // per bucket: keys were placed past it (gm_common.h)
   uint64_t xmask = 0;             // plain region bucket count - 1
   uint64_t xwbase = 0;            // first bucket of the wildcard-key region
   uint64_t xwmask = 0;            // wildcard region bucket count - 1
@@ -51,6 +52,9 @@ struct Scratch {
   uint32_t* row2 = nullptr;   // [n+1] (legacy fix-up)
   uint32_t* rej = nullptr;    // [n]   rejected pairs per topic
   uint32_t* exact_id = nullptr;  // [n]
+  uint8_t* xbin = nullptr;    // [n]   exact probe: table range (bin) of each name's home bucket
+  uint32_t* xord = nullptr;   // [n]   names in bin order
+  uint32_t* xcnt = nullptr;   // [2 * (XBINS + 1)] bin counts, then cursors
   uint32_t p_cap = 0;   // pair staging capacity
   uint4* stg = nullptr;       // staged pairs {topic, filter, rank | REJ_BIT, 0}, CH-slot chunks
   uint32_t* chk = nullptr;    // per staged chunk: pairs in it (written by the walk)
@@ -93,6 +97,8 @@ constexpr uint32_t CENSUS_N = 4;
 constexpr uint32_t WALK_SHARDS = 8;
 constexpr uint32_t CTL_CLAIM_STRIDE = 32;
 
+constexpr uint32_t XBIN_BITS = 6;  // exact probe over a huge table: 64 table ranges
+constexpr uint32_t XBINS = 1u << XBIN_BITS;
 constexpr uint32_t STAGE_CHUNK = 1024;  // staged-pair slots a walk wave reserves per atomic
 constexpr uint32_t REJ_BIT = 0x80000000u;
 constexpr uint32_t REJ_SCAN_MAX = 4096;  // rejects the deferred scatter handles in-line
@@ -121,7 +127,7 @@ hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, con
                       Scratch& sc, hipStream_t s);
 // exact route-key ids of every name (after launch_tok; a no-op when there are no plain keys)
 hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
-                        Scratch& sc, hipStream_t s);
+                        Scratch& sc, const WalkGeom& g, hipStream_t s);
 
 // Per-batch scratch of the publish fan-out (gm_fanout.inc).
 struct FanScratch {

@@ -25,6 +25,8 @@ constexpr uint32_t SCAN_ITEMS = 16;
 constexpr uint32_t SCAN_TILE = WG * SCAN_ITEMS;
 constexpr uint32_t TILE_BYTES = 16384;  // tokenizer LDS tile (256 topics)
 constexpr uint32_t TILE_CHUNKS = TILE_BYTES / 16 + 2;
+constexpr uint64_t XBIN_MIN_TABLE = 2ull << 30;  // exact tables beyond this are probed binned
+constexpr uint32_t XBIN_MIN_NAMES = 65536;
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
@@ -284,6 +286,7 @@ hipError_t launch_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* 
 static ExactArgs exact_args(const DevIndex& ix) {
   ExactArgs x;
   x.exact = ix.exact;
+  x.xovf = ix.xovf;
   x.xmask = ix.xmask;
   x.xwbase = ix.xwbase;
   x.xwmask = ix.xwmask;
@@ -314,10 +317,28 @@ hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, con
 }
 
 hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
-                        Scratch& sc, hipStream_t s) {
+                        Scratch& sc, const WalkGeom& g, hipStream_t s) {
   if (n == 0 || ix.plain_empty) return hipSuccess;
-  hipLaunchKernelGGL(k_exact, dim3(grid_for(n, 1u << 20)), dim3(WG), 0, s, bytes, off, n,
-                     sc.exact_id, exact_args(ix), ix.wild_empty);
+  const uint64_t buckets = ix.xwbase + ix.xwmask + 1;
+  if (buckets * 64ull <= XBIN_MIN_TABLE || n < XBIN_MIN_NAMES) {
+    hipLaunchKernelGGL(k_exact, dim3(grid_for(n, 1u << 20)), dim3(WG), 0, s, bytes, off, n,
+                       sc.exact_id, exact_args(ix), ix.wild_empty);
+    return hipGetLastError();
+  }
+  uint32_t bits = 0;
+  while ((1ull << bits) < buckets) ++bits;
+  const uint32_t shift = bits > XBIN_BITS ? bits - XBIN_BITS : 0u;
+  hipError_t e = hipMemsetAsync(sc.xcnt, 0, 2 * (XBINS + 1) * 4, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_xbin, dim3(grid_for(n, g.cus * 8)), dim3(WG), 0, s, bytes, off, n,
+                     sc.exact_id, exact_args(ix), ix.wild_empty, shift, sc.xbin, sc.xcnt);
+  hipLaunchKernelGGL(k_xoff, dim3(1), dim3(64), 0, s, sc.xcnt);
+  hipLaunchKernelGGL(k_xplace, dim3(grid_for(n, g.cus * 4)), dim3(WG), 0, s, sc.xbin, n, sc.xcnt,
+                     sc.xord);
+  // a quarter of the batch in flight at once: each sweep spans about a quarter of the table
+  hipLaunchKernelGGL(k_exact_binned, dim3(std::min<uint32_t>(g.cus * 4, grid_for(n, 1u << 20))),
+                     dim3(WG), 0, s, bytes, off, n, sc.exact_id, exact_args(ix), ix.wild_empty,
+                     sc.xord);
   return hipGetLastError();
 }
 

@@ -101,3 +101,41 @@ class Router:
                 routes += self.lookup_routes(fb(int(f)))
             out.append(routes)
         return out
+
+
+class SessionRouter(Router):
+    """``emqx_session_router`` (apps/emqx/src/emqx_session_router.erl), the router of persistent
+    sessions: the same route assembly over a second route bag (``emqx_session_route_ram/disc``)
+    whose wildcard filters live in the session trie (``emqx_trie:insert_session/1`` via
+    emqx_router_utils:insert_session_trie_route, :41-46; delete via delete_session_trie_route,
+    :54-71).  Dests are session ids.
+
+    * ``do_add_route(Topic, SessionID)``     emqx_session_router.erl:126-143
+    * ``do_delete_route(Topic, SessionID)``  :168-176
+    * ``match_routes(Topic)``                :146-151 (match_trie :154-159 reads the session
+      trie: [] when it is empty)
+    * ``delete_routes(SessionID, Topics)``   :162-163 (asynchronous there: a cast to the pool)
+
+    Given a :class:`emqx_amd.Trie`, the router writes that Trie's session table, so
+    ``Trie.match_session`` and this router read one index, as emqx_trie's session_trie() is the
+    table emqx_router_utils writes; otherwise it owns a second engine index."""
+
+    def __init__(self, trie=None, device: int = 0, **engine_kw):
+        engine = trie._session().engine if trie is not None else None
+        super().__init__(engine=engine, node=None, device=device, **engine_kw)
+        self.trie = trie
+
+    def do_add_route(self, topic: bytes, session_id: object) -> str:
+        return Router.add_route(self, topic, session_id)
+
+    def do_delete_route(self, topic: bytes, session_id: object) -> str:
+        return Router.delete_route(self, topic, session_id)
+
+    add_route = do_add_route
+    delete_route = do_delete_route
+
+    def delete_routes(self, session_id: object, topics: Sequence[bytes]) -> str:
+        for t in topics:
+            self.do_delete_route(t, session_id)
+        return "ok"
+

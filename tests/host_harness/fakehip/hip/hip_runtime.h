@@ -1,0 +1,62 @@
+// Host-only stand-in for the HIP runtime API, for the sanitizer harness of the engine's host
+// code (tests/host_harness).  TEST INFRASTRUCTURE: "device" memory is host memory, streams and
+// events are no-ops (every call completes at once), and the kernel launchers the engine calls
+// are CPU functions in fake_hip.cpp (k_patch really applies a delta commit's patches; the match
+// pipeline is not run here -- harness.cpp walks the committed tables on the CPU instead).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+typedef int hipError_t;
+enum { hipSuccess = 0, hipErrorInvalidDevice = 101, hipErrorUnknown = 999, hipErrorNotReady = 600 };
+typedef struct ihipStream_t* hipStream_t;
+typedef struct ihipEvent_t* hipEvent_t;
+enum hipMemcpyKind {
+  hipMemcpyHostToHost = 0,
+  hipMemcpyHostToDevice = 1,
+  hipMemcpyDeviceToHost = 2,
+  hipMemcpyDeviceToDevice = 3
+};
+#define hipStreamNonBlocking 1u
+#define hipEventDisableTiming 2u
+#define hipHostMallocDefault 0u
+#define hipHostMallocPortable 1u
+#define hipHostMallocMapped 2u
+
+struct uint2 {
+  uint32_t x, y;
+};
+struct uint4 {
+  uint32_t x, y, z, w;
+};
+static inline uint2 make_uint2(uint32_t x, uint32_t y) { return uint2{x, y}; }
+static inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
+  return uint4{x, y, z, w};
+}
+struct hipDeviceProp_t {
+  int multiProcessorCount;
+};
+
+hipError_t hipGetDeviceCount(int* n);
+hipError_t hipSetDevice(int d);
+hipError_t hipGetDeviceProperties(hipDeviceProp_t* p, int d);
+const char* hipGetErrorString(hipError_t e);
+hipError_t hipMalloc(void** p, size_t bytes);
+hipError_t hipFree(void* p);
+hipError_t hipHostMalloc(void** p, size_t bytes, unsigned flags);
+hipError_t hipHostFree(void* p);
+hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned flags);
+hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind k);
+hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind k, hipStream_t st);
+hipError_t hipMemsetAsync(void* d, int v, size_t n, hipStream_t st);
+hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned flags);
+hipError_t hipStreamDestroy(hipStream_t s);
+hipError_t hipStreamSynchronize(hipStream_t s);
+hipError_t hipStreamWaitEvent(hipStream_t s, hipEvent_t e, unsigned flags);
+hipError_t hipEventCreate(hipEvent_t* e);
+hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned flags);
+hipError_t hipEventDestroy(hipEvent_t e);
+hipError_t hipEventRecord(hipEvent_t e, hipStream_t s);
+hipError_t hipEventSynchronize(hipEvent_t e);
+hipError_t hipEventQuery(hipEvent_t e);
+hipError_t hipEventElapsedTime(float* ms, hipEvent_t a, hipEvent_t b);

@@ -74,19 +74,69 @@ def test_trie_suite_on_device(emqx, golden, compact):
         trie.engine.close()
 
 
-def test_session_trie_is_a_second_table(emqx):
-    """insert_session/match_session/delete_session/empty_session work on their own table
-    (emqx_trie.erl:117-176): the two tries never see each other's filters."""
+def test_session_router_churn_vs_oracle(emqx):
+    """emqx_session_router (emqx_session_router.erl:126-176) over the session trie
+    (emqx_trie.erl:117-176): random do_add_route / do_delete_route / delete_routes churn with
+    session ids as dests, beside a main Router taking its own churn.  After every commit the
+    session router's match_routes and Trie.match_session / empty_session equal the oracle's
+    Router on a second table (oracle/emqx_ref.py Router = emqx_router's route assembly over its
+    own bag and trie), and the main router's answers equal its own oracle: the two tables never
+    see each other's routes."""
+    rng = random.Random(17)
+    vocab = ["a", "b", "", "$s", "c", "long-word-%d"]
+
+    def word():
+        w = rng.choice(vocab)
+        return w % rng.randint(0, 2) if "%" in w else w
+
+    def filt():
+        d = rng.randint(1, 5)
+        return "/".join("#" if i == d - 1 and rng.random() < 0.2 else
+                        "+" if rng.random() < 0.35 else word() for i in range(d)).encode()
+
     trie = emqx.Trie()
-    trie.insert(b"a/+")
-    trie.insert_session(b"a/#")
-    trie.insert_session(b"b/+")
-    assert trie.match(b"a/b") == [b"a/+"]
-    assert sorted(trie.match_session(b"a/b")) == [b"a/#"]
-    assert trie.match_session(b"b/x") == [b"b/+"] and trie.match(b"b/x") == []
-    trie.delete_session(b"a/#")
-    trie.delete_session(b"b/+")
-    assert trie.empty_session() and not trie.empty()
+    srt = emqx.SessionRouter(trie)
+    main = emqx.Router()
+    ref_s, ref_m = R.Router(), R.Router()
+    filters = sorted({filt() for _ in range(300)})
+    sessions = [f"session-{i}" for i in range(12)]
+    topics = ["/".join(word() for _ in range(rng.randint(1, 6))).encode() for _ in range(400)]
+    topics += filters[:20]  # wildcard names: exact lookups only
+    live = []
+    for step in range(14):
+        for _ in range(rng.randint(20, 80)):
+            op = rng.random()
+            if op < 0.6 or not live:
+                f, sid = rng.choice(filters), rng.choice(sessions)
+                srt.do_add_route(f, sid)
+                ref_s.add_route(f, sid)
+                live.append((f, sid))
+            elif op < 0.9:
+                f, sid = live.pop(rng.randrange(len(live)))
+                srt.do_delete_route(f, sid)
+                ref_s.delete_route(f, sid)
+            else:  # a session goes away: delete_routes(SessionID, Subscriptions)
+                sid = rng.choice(sessions)
+                subs = [f for f, s in live if s == sid]
+                srt.delete_routes(sid, subs)
+                for f in subs:
+                    ref_s.delete_route(f, sid)
+                live = [(f, s) for f, s in live if s != sid]
+            if rng.random() < 0.3:
+                f = rng.choice(filters)
+                main.add_route(f, "node1")
+                ref_m.add_route(f, "node1")
+        got_s = srt.match_routes_batch(topics)
+        got_m = main.match_routes_batch(topics)
+        for i, t in enumerate(topics):
+            assert sorted(got_s[i]) == sorted(ref_s.match_routes(t)), (step, t)
+            assert sorted(got_m[i]) == sorted(ref_m.match_routes(t)), (step, t)
+            assert sorted(trie.match_session(t)) == sorted(ref_s.match_trie(t)), (step, t)
+        assert trie.empty_session() == ref_s.trie.empty()
+    for f, sid in list(live):
+        srt.do_delete_route(f, sid)
+    assert trie.empty_session() and srt.match_routes(b"a/b") == []
+    assert not main.engine.trie_empty() or ref_m.trie.empty()
 
 
 def test_router_suite_on_device(emqx, golden):
