@@ -278,6 +278,9 @@ def main():
                 "edge_slot_loads_per_batch": int(census["slot_loads"]),
                 "walk_lane_iterations_per_batch": int(census["lane_iters"]),
                 "walk_wave_iterations_per_batch": int(census["wave_iters"]),
+                # the pruned walk's edge-bucket loads by probed level (literal / '+' probes)
+                "edge_loads_by_level": {k: [int(x) for x in v[:max(1, _last_nz(v) + 1)]]
+                                        for k, v in census["loads_by_level"].items()},
                 "pipeline_ms_per_batch": round(pipe_ms, 4),
                 "passes_in_flight": eng.PIPES if pipelined else 1,
                 "one_pass_at_a_time": (None if sync_ms is None else {
@@ -351,6 +354,10 @@ def _filter_sharded_run(Engine, D, args, w, tb, to, rank, world, dev, local):
             "pairs_per_batch": pairs,
             "step": "rank 0's batch broadcast (RCCL), matched on each shard, pair counts "
                     "all-gathered, CSRs sent to rank 0 (grouped send/recv), merged by emqxgm_merge"}
+
+
+def _last_nz(v):
+    return max([i for i, x in enumerate(v) if x] or [0])
 
 
 def _subset(w, idx):

@@ -240,6 +240,7 @@ struct TrieModel {
   std::vector<uint64_t> occ, tomb;  // bitmaps over edge slots: used (live or TOMB), TOMB
   uint64_t nbk = 0, ecap = 0, n_occ = 0, n_edges = 0, tn_cap = 0, fv_cap = 0;
   std::vector<uint32_t> fvbits;
+  std::vector<uint32_t> multi;  // [count, fid...] lists of nodes shared by several filters
   bool needs_verify = false;
   uint32_t max_depth = 0;
   uint64_t n_trie = 0, n_route = 0;
@@ -374,6 +375,7 @@ struct emqxgm {
   PassCtx sync;                    // synchronous calls
   WalkGeom geom;
   uint32_t leafp_mask = CF_HMASK;  // depth-code pruning (tune "leaf_prune")
+  uint64_t census_depth[2 * CENSUS_DEPTHS] = {};  // the last census pass's loads per level
   uint8_t* d_in_bytes = nullptr;
   uint32_t* d_in_off = nullptr;
   uint64_t in_bytes_cap = 0, in_off_cap = 0;
@@ -808,6 +810,68 @@ void commit_stats(emqxgm* h, double ms, bool delta) {
   (delta ? h->st.delta_commits : h->st.full_commits) += 1;
 }
 
+// The device tables of a host model (its node slots, side array, verify bits, exact entries,
+// overflow bits, multi lists): generated from the model -- a full build and a snapshot load
+// share this -- uploaded into a new table set, and h->ix pointed at them.
+int upload_model(emqxgm* h, TrieModel& m) {
+  const uint64_t n_nodes = m.parent.size();
+  std::vector<uint4> eslots(SLOT_U4 * m.ecap, make_uint4(0u, 0u, 0u, 0u));
+  for (uint64_t i = 0; i < m.ecap; ++i)
+    eslots[SLOT_U4 * i] = make_uint4(0u, 0u, bit(m.tomb, i) ? TOMB : NONE, 0u);
+  for (uint32_t c = 1; c < n_nodes; ++c)
+    if (m.slot[c] != DEAD) m.node_slot(c, &eslots[SLOT_U4 * m.slot[c]]);
+  std::vector<uint32_t> tn_of(m.tn_cap, NONE);
+  for (size_t i = 0; i < n_nodes; ++i) tn_of[i] = m.tn[i];
+  const uint64_t fmask =
+      h->cfg.full_hash_bits >= 64 ? ~0ull : ((1ull << h->cfg.full_hash_bits) - 1ull);
+  const uint64_t xcap = m.xcap_p + m.xcap_w;
+  std::vector<uint4> xslots(xcap * XBUCKET * XENT_U4, make_uint4(0u, 0u, 0u, 0u));
+  for (uint64_t e = 0; e < xcap * XBUCKET; ++e) xslots[XENT_U4 * e].y = bit(m.xtomb, e) ? TOMB : NONE;
+  for (uint32_t id = 0; id < m.xpos.size(); ++id) {
+    if (m.xpos[id] == NONE) continue;
+    const Filter& f = h->filters[id];
+    const uint8_t* p = h->pool.data() + f.off;
+    xent(key_hash(p, f.len, fmask), id, p, f.len, &xslots[XENT_U4 * (uint64_t)m.xpos[id]]);
+  }
+  std::vector<DevBuf> nbufs;
+  DevIndex nx = h->ix;  // pool and fan-out pointers already set
+  int rc = 0;
+  if ((rc = dev_upload(h, nbufs, eslots, &nx.edges)) ||
+      (rc = dev_upload(h, nbufs, m.multi, &nx.multi)) ||
+      (rc = dev_upload(h, nbufs, tn_of, &nx.tn_of)) ||
+      (rc = dev_upload(h, nbufs, m.fvbits, &nx.fvbits)) ||
+      (rc = dev_upload(h, nbufs, xslots, &nx.exact)) ||
+      (rc = dev_upload(h, nbufs, m.xovf, (const uint64_t**)&nx.xovf))) {
+    free_bufs(nbufs);
+    return rc;
+  }
+  m.d_edges = (uint32_t*)nx.edges;
+  m.d_exact = (uint32_t*)nx.exact;
+  m.d_tn = (uint32_t*)nx.tn_of;
+  m.d_fv = (uint32_t*)nx.fvbits;
+  m.d_xovf = (uint32_t*)nx.xovf;
+  nx.emask = m.nbk - 1;
+  nx.xmask = m.xcap_p - 1;
+  nx.xwbase = m.xcap_p;
+  nx.xwmask = m.xcap_w - 1;
+  const uint32_t root_p = m.pchild[0];
+  nx.root_cf = m.cf(0);
+  nx.root_sig = m.sig[0];
+  nx.root_hf = m.hfd(0);
+  nx.root_pcf = root_p ? m.cf(root_p) : 0u;
+  nx.root_phf = root_p ? m.hfd(root_p) : NONE;
+  nx.test_mask = h->test_mask;
+  nx.needs_verify = m.needs_verify;
+  nx.full_mask = fmask;
+  nx.max_depth = m.max_depth;
+  nx.trie_empty = (m.n_trie == 0);
+  nx.plain_empty = (m.n_route_p == 0);
+  nx.wild_empty = (m.n_route_w == 0);
+  h->o_tab = std::make_shared<DevOwner>(std::move(nbufs));  // old tables live on with their epochs
+  h->ix = nx;
+  return 0;
+}
+
 // Full build of the device index from the pending registry; swaps it in and rebuilds the host
 // model (TrieModel) that later delta commits patch.
 int commit_full(emqxgm* h) {
@@ -896,6 +960,7 @@ int commit_full(emqxgm* h) {
     resolve(m.tn[i]);
   }
   m.n_edges = n_nodes - 1;
+  m.multi = std::move(multi);
   // 32-B slots in 64-B buckets (gm_common.h "edge slots"); load factor <= 1/EDGE_SLACK.  Each
   // slot carries its child's '+' child {cf, hf}, so the walk expands most '+' children
   // without a probe.
@@ -903,8 +968,6 @@ int commit_full(emqxgm* h) {
   m.nbk = m.ecap / EBUCKET;
   m.occ.assign(m.ecap / 64 + 1, 0ull);
   m.tomb.assign(m.ecap / 64 + 1, 0ull);
-  std::vector<uint4> eslots(SLOT_U4 * m.ecap, make_uint4(0u, 0u, 0u, 0u));
-  for (uint64_t i = 0; i < m.ecap; ++i) eslots[SLOT_U4 * i] = make_uint4(0u, 0u, NONE, 0u);
   for (uint32_t c = 1; c < n_nodes; ++c) {
     uint64_t b = edge_slot(m.parent[c], m.tok[c], m.nbk - 1), i;
     for (;;) {
@@ -918,13 +981,10 @@ int commit_full(emqxgm* h) {
     }
     bset(m.occ, i);
     m.slot[c] = i;
-    m.node_slot(c, &eslots[SLOT_U4 * i]);
   }
   m.n_occ = m.n_edges;
   // node side array with headroom for delta-commit growth
   m.tn_cap = n_nodes + std::max<uint64_t>(4096, n_nodes / 4);
-  std::vector<uint32_t> tn_of(m.tn_cap, NONE);
-  for (size_t i = 0; i < n_nodes; ++i) tn_of[i] = m.tn[i];
   m.fv_cap = m.fvbits.size() + std::max<uint64_t>(1024, m.fvbits.size() / 4);
   m.fvbits.resize(m.fv_cap, 0u);
 
@@ -940,8 +1000,6 @@ int commit_full(emqxgm* h) {
   m.xtomb.assign(xcap * XBUCKET / 64 + 1, 0ull);
   m.xovf.assign(xcap / 64 + 1, 0ull);
   m.xpos.assign(nf, NONE);
-  std::vector<uint4> xslots(xcap * XBUCKET * XENT_U4, make_uint4(0u, 0u, 0u, 0u));
-  for (uint64_t e = 0; e < xcap * XBUCKET; ++e) xslots[XENT_U4 * e].y = NONE;
   for (uint32_t id = 0; id < h->filters.size(); ++id) {
     const Filter& f = h->filters[id];
     if (!f.route_refs) continue;
@@ -950,10 +1008,9 @@ int commit_full(emqxgm* h) {
     uint64_t b = m.xhome(w, fh);
     for (;;) {
       uint32_t j = 0;
-      while (j < XBUCKET && xslots[XENT_U4 * (b * XBUCKET + j)].y != NONE) ++j;
+      while (j < XBUCKET && bit(m.xocc, b * XBUCKET + j)) ++j;
       if (j < XBUCKET) {
         const uint64_t e = b * XBUCKET + j;
-        xent(fh, id, h->pool.data() + f.off, f.len, &xslots[XENT_U4 * e]);
         bset(m.xocc, e);
         m.xpos[id] = (uint32_t)e;
         break;
@@ -964,46 +1021,9 @@ int commit_full(emqxgm* h) {
   }
   m.x_occ_p = m.n_route_p;
   m.x_occ_w = m.n_route_w;
-
-  // ---- upload and swap ----
   if (hipSetDevice(h->cfg.device) != hipSuccess) return fail(h, hipErrorInvalidDevice, "hipSetDevice");
   int rc = 0;
-  if ((rc = upload_pool(h, nullptr)) || (rc = fan_full(h))) return rc;
-  std::vector<DevBuf> nbufs;
-  DevIndex nx = h->ix;  // pool and fan-out pointers just set
-  if ((rc = dev_upload(h, nbufs, eslots, &nx.edges)) ||
-      (rc = dev_upload(h, nbufs, multi, &nx.multi)) ||
-      (rc = dev_upload(h, nbufs, tn_of, &nx.tn_of)) ||
-      (rc = dev_upload(h, nbufs, m.fvbits, &nx.fvbits)) ||
-      (rc = dev_upload(h, nbufs, xslots, &nx.exact)) ||
-      (rc = dev_upload(h, nbufs, m.xovf, (const uint64_t**)&nx.xovf))) {
-    free_bufs(nbufs);
-    return rc;
-  }
-  m.d_edges = (uint32_t*)nx.edges;
-  m.d_exact = (uint32_t*)nx.exact;
-  m.d_tn = (uint32_t*)nx.tn_of;
-  m.d_fv = (uint32_t*)nx.fvbits;
-  m.d_xovf = (uint32_t*)nx.xovf;
-  nx.emask = m.nbk - 1;
-  nx.xmask = m.xcap_p - 1;
-  nx.xwbase = m.xcap_p;
-  nx.xwmask = m.xcap_w - 1;
-  const uint32_t root_p = m.pchild[0];
-  nx.root_cf = m.cf(0);
-  nx.root_sig = m.sig[0];
-  nx.root_hf = m.hfd(0);
-  nx.root_pcf = root_p ? m.cf(root_p) : 0u;
-  nx.root_phf = root_p ? m.hfd(root_p) : NONE;
-  nx.test_mask = test_mask;
-  nx.needs_verify = m.needs_verify;
-  nx.full_mask = fmask;
-  nx.max_depth = m.max_depth;
-  nx.trie_empty = (m.n_trie == 0);
-  nx.plain_empty = (m.n_route_p == 0);
-  nx.wild_empty = (m.n_route_w == 0);
-  h->o_tab = std::make_shared<DevOwner>(std::move(nbufs));  // old tables live on with their epochs
-  h->ix = nx;
+  if ((rc = upload_pool(h, nullptr)) || (rc = fan_full(h)) || (rc = upload_model(h, m))) return rc;
   m.valid = true;
   h->tm = std::move(m);
   h->changed.clear();  // every filter's committed flags follow at publish (commit_locked)
@@ -1402,7 +1422,7 @@ int ensure_scratch(emqxgm* h, PassCtx& c, uint32_t n, uint64_t words, uint32_t p
       (rc = dev_alloc(h, c, (void**)&s.scan_tmp, (size_t)stw * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.ctl, CTL_N * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.census,
-                      (CENSUS_N + 3 * (h->geom.lanes / 64)) * sizeof(unsigned long long))) ||
+                      (CENSUS_HDR + 3 * (h->geom.lanes / 64)) * sizeof(unsigned long long))) ||
       (rc = dev_alloc(h, c, (void**)&s.spill, (size_t)scap * h->geom.lanes * sizeof(uint2))) ||
       (rc = dev_alloc(h, c, (void**)&s.rlist, (size_t)h->reject_cap * 8)))
     return rc;
@@ -1462,7 +1482,7 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
   HIPCHK(h, hipMemsetAsync(s.ctl, 0, CTL_N * 4, st));
   if (census)
     HIPCHK(h, hipMemsetAsync(s.census, 0,
-                             (CENSUS_N + 3 * (h->geom.lanes / 64)) * sizeof(unsigned long long),
+                             (CENSUS_HDR + 3 * (h->geom.lanes / 64)) * sizeof(unsigned long long),
                              st));
   HIPCHK(h, launch_tok(d_bytes, d_off, n, ix, s, st));
   if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[4], st));
@@ -1599,14 +1619,15 @@ int pass_finish(emqxgm* h, PassCtx& c, uint32_t n, bool legacy, uint32_t* pairs,
   if (census) {
     if (const char* wf = getenv("EMQXGM_WAVE_TIMES")) {  // diagnostic: per-wave timeline
       std::vector<unsigned long long> wt(3 * (h->geom.lanes / 64));
-      HIPCHK(h, hipMemcpy(wt.data(), s.census + CENSUS_N, wt.size() * 8, hipMemcpyDeviceToHost));
+      HIPCHK(h, hipMemcpy(wt.data(), s.census + CENSUS_HDR, wt.size() * 8, hipMemcpyDeviceToHost));
       if (FILE* fp = fopen(wf, "wb")) {
         fwrite(wt.data(), 8, wt.size(), fp);
         fclose(fp);
       }
     }
-    unsigned long long cv[CENSUS_N] = {0, 0, 0, 0};
+    unsigned long long cv[CENSUS_HDR] = {0};
     HIPCHK(h, hipMemcpy(cv, s.census, sizeof cv, hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < 2 * CENSUS_DEPTHS; ++i) h->census_depth[i] = cv[CENSUS_N + i];
     census[0] = cv[0];
     census[1] = cv[1];
     census[2] = *pairs;
@@ -2145,6 +2166,224 @@ int emqxgm_commit(emqxgm_t* h, uint64_t* epoch) {
   return rc;
 }
 
+// ---- index snapshot (SURVEY 5 "checkpoint / resume"): the committed registry and the host
+// model of the device index in one file, so a restart restores the index without rebuilding it
+// (the reference rebuilds its ram_copies route tables from peers, emqx_router.erl:78-92) ----
+}  // extern "C"
+namespace {
+
+constexpr uint64_t SNAP_MAGIC = 0x31534d47584d45ull;  // "EMXGMS1"
+constexpr uint32_t SNAP_VERSION = 1;
+
+struct SnapOut {
+  FILE* f;
+  bool ok = true;
+  void raw(const void* p, size_t n) { ok = ok && (n == 0 || fwrite(p, 1, n, f) == n); }
+  template <class T>
+  void pod(const T& v) { raw(&v, sizeof v); }
+  template <class T>
+  void vec(const std::vector<T>& v) {
+    pod<uint64_t>(v.size());
+    raw(v.data(), v.size() * sizeof(T));
+  }
+};
+
+struct SnapIn {
+  FILE* f;
+  bool ok = true;
+  void raw(void* p, size_t n) { ok = ok && (n == 0 || fread(p, 1, n, f) == n); }
+  template <class T>
+  void pod(T& v) { raw(&v, sizeof v); }
+  template <class T>
+  void vec(std::vector<T>& v) {
+    uint64_t n = 0;
+    pod(n);
+    if (!ok || n > (1ull << 40) / sizeof(T)) {
+      ok = false;
+      return;
+    }
+    v.resize(n);
+    raw(v.data(), n * sizeof(T));
+  }
+};
+
+template <class IO, class M>
+void snap_model(IO& io, M& m) {
+  io.vec(m.emap.ents);
+  io.pod(m.emap.mask);
+  io.pod(m.emap.used);
+  io.vec(m.parent);
+  io.vec(m.ref);
+  io.vec(m.nlit);
+  io.vec(m.pchild);
+  io.vec(m.hf);
+  io.vec(m.tw);
+  io.vec(m.tn);
+  io.vec(m.sig);
+  io.vec(m.hcode);
+  io.vec(m.tok);
+  io.vec(m.slot);
+  io.vec(m.occ);
+  io.vec(m.tomb);
+  io.pod(m.nbk);
+  io.pod(m.ecap);
+  io.pod(m.n_occ);
+  io.pod(m.n_edges);
+  io.pod(m.tn_cap);
+  io.pod(m.fv_cap);
+  io.vec(m.fvbits);
+  io.vec(m.multi);
+  io.pod(m.needs_verify);
+  io.pod(m.max_depth);
+  io.pod(m.n_trie);
+  io.pod(m.n_route);
+  io.vec(m.xpos);
+  io.vec(m.xocc);
+  io.vec(m.xtomb);
+  io.vec(m.xovf);
+  io.pod(m.xcap_p);
+  io.pod(m.xcap_w);
+  io.pod(m.x_occ_p);
+  io.pod(m.x_occ_w);
+  io.pod(m.n_route_p);
+  io.pod(m.n_route_w);
+}
+
+template <class Map, class IO>
+void snap_map_out(IO& io, const Map& mp) {
+  io.template pod<uint64_t>(mp.size());
+  for (const auto& kv : mp) {
+    io.pod(kv.first);
+    io.vec(kv.second);
+  }
+}
+
+template <class Map, class IO>
+void snap_map_in(IO& io, Map& mp) {
+  uint64_t n = 0;
+  io.pod(n);
+  for (uint64_t i = 0; io.ok && i < n; ++i) {
+    uint32_t k = 0;
+    io.pod(k);
+    io.vec(mp[k]);
+  }
+}
+
+}  // namespace
+extern "C" {
+
+int emqxgm_snapshot_save(emqxgm_t* h, const char* path) {
+  if (!h || !path) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->wmu);
+  int rc = 0;
+  if (h->dirty && (rc = commit_locked(h))) return rc;  // the file holds committed state only
+  if (!h->tm.valid) {
+    set_err(h, "no host model to save");
+    return -EINVAL;
+  }
+  FILE* f = fopen(path, "wb");
+  if (!f) return -errno;
+  SnapOut o{f};
+  o.pod(SNAP_MAGIC);
+  o.pod(SNAP_VERSION);
+  o.pod(h->cfg.word_hash_bits);
+  o.pod(h->cfg.full_hash_bits);
+  o.vec(h->pool);
+  o.vec(h->filters);
+  o.pod(h->n_trie_pending);
+  o.pod(h->n_route_pending);
+  o.pod(h->local_node);
+  snap_map_out(o, h->rdest);
+  snap_map_out(o, h->lsubs);
+  snap_model(o, h->tm);
+  o.pod(SNAP_MAGIC);
+  const bool ok = o.ok && fflush(f) == 0;
+  fclose(f);
+  if (!ok) {
+    set_err(h, "snapshot write failed");
+    return -EIO;
+  }
+  return 0;
+}
+
+int emqxgm_snapshot_load(emqxgm_t* h, const char* path) {
+  if (!h || !path) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->wmu);
+  if (!h->filters.empty() || h->dirty) {
+    set_err(h, "snapshot load needs a fresh handle");
+    return -EBUSY;
+  }
+  FILE* f = fopen(path, "rb");
+  if (!f) return -errno;
+  const auto t0 = std::chrono::steady_clock::now();
+  SnapIn in{f};
+  uint64_t magic = 0, magic2 = 0;
+  uint32_t ver = 0, whb = 0, fhb = 0;
+  in.pod(magic);
+  in.pod(ver);
+  in.pod(whb);
+  in.pod(fhb);
+  if (!in.ok || magic != SNAP_MAGIC || ver != SNAP_VERSION || whb != h->cfg.word_hash_bits ||
+      fhb != h->cfg.full_hash_bits) {
+    fclose(f);
+    set_err(h, "not a snapshot of this engine configuration");
+    return -EINVAL;
+  }
+  std::vector<uint8_t> pool;
+  std::vector<Filter> filters;
+  uint64_t ntp = 0, nrp = 0;
+  uint32_t local = NONE;
+  decltype(h->rdest) rdest;
+  decltype(h->lsubs) lsubs;
+  TrieModel m;
+  in.vec(pool);
+  in.vec(filters);
+  in.pod(ntp);
+  in.pod(nrp);
+  in.pod(local);
+  snap_map_in(in, rdest);
+  snap_map_in(in, lsubs);
+  snap_model(in, m);
+  in.pod(magic2);
+  fclose(f);
+  bool sane = in.ok && magic2 == SNAP_MAGIC && !m.parent.empty() && m.slot.size() == m.parent.size();
+  for (size_t i = 0; sane && i < filters.size(); ++i)
+    sane = filters[i].off + filters[i].len <= pool.size();
+  if (!sane) {
+    set_err(h, "snapshot truncated or corrupt");
+    return -EINVAL;
+  }
+  {
+    std::unique_lock<std::shared_mutex> pg(h->pmu);
+    h->pool.swap(pool);
+    h->filters.swap(filters);
+    h->slots.clear();
+    h->slot_mask = 0;
+    if (!h->filters.empty()) slots_grow(h);
+  }
+  h->n_trie_pending = ntp;
+  h->n_route_pending = nrp;
+  h->local_node = local;
+  h->rdest.swap(rdest);
+  h->lsubs.swap(lsubs);
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return fail(h, hipErrorInvalidDevice, "hipSetDevice");
+  int rc = 0;
+  h->foff_host.clear();
+  h->fver_host.clear();
+  if ((rc = patch_wait(h)) || (rc = upload_pool(h, nullptr)) || (rc = fan_full(h)) ||
+      (rc = upload_model(h, m)))
+    return rc;
+  m.valid = true;
+  h->tm = std::move(m);
+  h->changed.clear();
+  h->fan_changed.clear();
+  if ((rc = publish_epoch(h, false))) return rc;
+  h->dirty = false;
+  commit_stats(h, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
+               false);
+  return 0;
+}
+
 int emqxgm_trie_empty(emqxgm_t* h) {
   if (!h) return -EINVAL;
   std::lock_guard<std::mutex> g(h->emu);
@@ -2544,6 +2783,13 @@ int emqxgm_walk_census(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_of
   int rc = run_device(h, h->sync, d_bytes, d_offsets, n, bytes_len, &pairs, out);
   h->sync.epoch.reset();
   return rc;
+}
+
+int emqxgm_walk_census_levels(emqxgm_t* h, uint64_t* out, uint32_t n_out) {
+  if (!h || (!out && n_out)) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mmu);
+  for (uint32_t i = 0; i < n_out && i < 2 * CENSUS_DEPTHS; ++i) out[i] = h->census_depth[i];
+  return (int)(2 * CENSUS_DEPTHS);
 }
 
 static int grow_buf(emqxgm* h, DevBuf& b, uint64_t bytes) {

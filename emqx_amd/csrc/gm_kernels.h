@@ -90,6 +90,10 @@ enum : int {
 
 // diagnostic walk counters: states, slot loads, lane iterations, wave iterations
 constexpr uint32_t CENSUS_N = 4;
+// then edge-bucket loads per probed level (levels >= CENSUS_DEPTHS - 1 lumped), literal probes
+// at [CENSUS_N + d], '+' probes at [CENSUS_N + CENSUS_DEPTHS + d]; the per-wave timeline after
+constexpr uint32_t CENSUS_DEPTHS = 16;
+constexpr uint32_t CENSUS_HDR = CENSUS_N + 2 * CENSUS_DEPTHS;
 
 // The walk claims topics from WALK_SHARDS counters on separate 128-B lines (one hot counter
 // serialises at ~88 claims/us chip-wide); a wave starts on shard blockIdx % 8 (its XCD under

@@ -91,6 +91,8 @@ SYMBOLS = {
     "emqxgm_route_ref_many": (C.c_int, [_P, _P, _P, C.c_uint64, _P]),
     "emqxgm_commit": (C.c_int, [_P, _U64P]),
     "emqxgm_trie_empty": (C.c_int, [_P]),
+    "emqxgm_snapshot_save": (C.c_int, [_P, C.c_char_p]),
+    "emqxgm_snapshot_load": (C.c_int, [_P, C.c_char_p]),
     "emqxgm_trie_member": (C.c_int, [_P, C.c_char_p, C.c_uint32]),
     "emqxgm_lookup_id": (C.c_int, [_P, C.c_char_p, C.c_uint32, _U32P]),
     "emqxgm_filter_bytes": (C.c_int, [_P, C.c_uint32, C.POINTER(_U8P), _U32P]),
@@ -105,6 +107,7 @@ SYMBOLS = {
     "emqxgm_match_batch_submit": (C.c_int, [_P, _P, _P, C.c_uint32, _U64P]),
     "emqxgm_match_batch_wait": (C.c_int, [_P, C.c_uint64, C.POINTER(_BatchOut)]),
     "emqxgm_walk_census": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, _U64P]),
+    "emqxgm_walk_census_levels": (C.c_int, [_P, _U64P, C.c_uint32]),
     "emqxgm_export": (C.c_int, [_P, C.POINTER(_DevOut), _P, _P, _P, _P]),
     "emqxgm_merge": (C.c_int, [_P, C.c_uint32, _P, _P, _P, C.c_uint32, _P, _P, _P, _U32P]),
     "emqxgm_route_add": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32]),
@@ -327,6 +330,14 @@ class Engine:
         self._check(self._lib.emqxgm_commit(self._h, C.byref(e)), "commit")
         return e.value
 
+    def snapshot_save(self, path: str) -> None:
+        """emqxgm_snapshot_save: commit, then write the committed index to `path`."""
+        self._check(self._lib.emqxgm_snapshot_save(self._h, os.fsencode(path)), "snapshot_save")
+
+    def snapshot_load(self, path: str) -> None:
+        """emqxgm_snapshot_load: restore a snapshot into this fresh engine (no rebuild)."""
+        self._check(self._lib.emqxgm_snapshot_load(self._h, os.fsencode(path)), "snapshot_load")
+
     def trie_empty(self) -> bool:
         return bool(self._check(self._lib.emqxgm_trie_empty(self._h), "trie_empty"))
 
@@ -481,8 +492,11 @@ class Engine:
         out = (C.c_uint64 * 6)()
         self._check(self._lib.emqxgm_walk_census(self._h, C.c_void_p(d_bytes), C.c_void_p(d_off),
                                                  n, bytes_len, out), "walk_census")
+        lv = (C.c_uint64 * 32)()
+        self._check(self._lib.emqxgm_walk_census_levels(self._h, lv, 32), "walk_census_levels")
         return {"states": out[0], "slot_loads": out[1], "pairs": out[2], "words": out[3],
-                "lane_iters": out[4], "wave_iters": out[5]}
+                "lane_iters": out[4], "wave_iters": out[5],
+                "loads_by_level": {"literal": list(lv[:16]), "plus": list(lv[16:32])}}
 
     def match_rules(self, names: Sequence[bytes], rules: Sequence[bytes],
                     flags: Sequence[int]) -> np.ndarray:

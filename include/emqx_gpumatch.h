@@ -145,6 +145,14 @@ int emqxgm_trie_insert_many(emqxgm_t* h, const uint8_t* bytes, const uint64_t* o
 int emqxgm_route_ref_many(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets,
                           uint64_t n, uint32_t* ids /* nullable */);
 int emqxgm_commit(emqxgm_t* h, uint64_t* epoch /* nullable */);
+/* Index snapshot (the reference rebuilds its ram_copies route tables at start,
+ * emqx_router.erl:78-92): _save commits pending changes and writes the committed registry (filter
+ * strings, trie / route-key membership, routes, subscribers) and the host model of the device
+ * index to `path`; _load restores them into a fresh handle of the same configuration and
+ * publishes the index without rebuilding it (the device tables are generated from the model).
+ * -EBUSY: the handle is not fresh; -EINVAL: not a snapshot of this configuration. */
+int emqxgm_snapshot_save(emqxgm_t* h, const char* path);
+int emqxgm_snapshot_load(emqxgm_t* h, const char* path);
 /* 1 if the committed trie holds no filter, 0 otherwise (emqx_trie:empty/0). */
 int emqxgm_trie_empty(emqxgm_t* h);
 /* 1 if the committed trie holds exactly this filter key (emqx_trie:lookup_topic/2,
@@ -326,6 +334,9 @@ int emqxgm_merge(emqxgm_t* h, uint32_t parts, const uint32_t* const* rows,
  * wavefronts (one memory round trip each). */
 int emqxgm_walk_census(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_offsets,
                        uint32_t n, uint64_t bytes_len, uint64_t out[6]);
+/* The last census pass's edge-bucket loads by probed level: out[d] literal probes of level d,
+ * out[16 + d] '+' probes (levels >= 15 lumped into 15).  Returns the number of counters (32). */
+int emqxgm_walk_census_levels(emqxgm_t* h, uint64_t* out, uint32_t n_out);
 
 int emqxgm_set_profiling(emqxgm_t* h, int on);
 /* Runtime tuning knobs: "walk_wg_per_cu" (persistent walk workgroups per CU); "leaf_prune"

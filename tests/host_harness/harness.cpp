@@ -256,7 +256,23 @@ int main(int argc, char** argv) {
   std::set<std::string> in_trie, keyed;
   std::map<std::string, std::vector<std::pair<uint32_t, uint32_t>>> dests;
   uint64_t checks = 0;
+  const std::string snap = std::string(argc > 4 ? argv[4] : "/tmp") + "/emqxgm_harness_" +
+                           std::to_string(seed) + ".snap";
   for (int round = 0; round < rounds; ++round) {
+    if (round == rounds / 2) {
+      // snapshot round trip: the restored engine must answer the same and keep delta-committing
+      CHECK(emqxgm_snapshot_save(hd, snap.c_str()) == 0, "save: %s", hd->err.c_str());
+      emqxgm_destroy(hd);
+      hd = nullptr;
+      CHECK(emqxgm_create(&cfg, &hd) == 0, "create");
+      CHECK(emqxgm_snapshot_load(hd, snap.c_str()) == 0, "load: %s", hd->err.c_str());
+      emqxgm_t* other = nullptr;
+      CHECK(emqxgm_create(&cfg, &other) == 0, "create");
+      CHECK(emqxgm_trie_insert(other, (const uint8_t*)"a", 1, nullptr) == 0, "ins");
+      CHECK(emqxgm_snapshot_load(other, snap.c_str()) == -EBUSY, "load into a used handle");
+      emqxgm_destroy(other);
+      remove(snap.c_str());
+    }
     const int mode = (int)rnd(10);
     CHECK(emqxgm_tune(hd, "delta_commit", mode == 0 ? 0 : mode == 1 ? 2 : 1) == 0, "tune");
     const int ops = (int)(round == 0 ? 600 : 1 + rnd(120));

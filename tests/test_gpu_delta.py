@@ -178,3 +178,56 @@ def test_delta_publish_fanout_tables_follow(emqx):
     assert sorted(ent) == sorted([(b"t/1", b.node), (b"t/#", "other@node")])
     assert dl == [(b"t/1", "s2")]
     assert b.engine.stats()["delta_commits"] >= 2
+
+
+def test_snapshot_roundtrip(emqx, tmp_path):
+    """emqxgm_snapshot_save / _load: a fresh engine restored from a snapshot answers exactly as
+    the saved one (trie rows, exact ids, publish fan-out) and keeps taking delta commits."""
+    import workloads
+    w = workloads.generate(2, 30000, 20000)
+    eng = emqx.Engine()
+    eng.set_local_node(1)
+    eng.route_ref_many(w.fbytes, w.foff)
+    wi = np.nonzero(w.fwild)[0]
+    eng.trie_insert_many(*_subset(w, wi))
+    for i in range(0, w.nf, 97):
+        eng.route_add(w.filter(i), 1 + i % 2)
+        eng.subscriber_add(w.filter(i), i % 5)
+    eng.commit()
+    eng.trie_insert(b"#")  # a pending change: save commits it first
+    p = str(tmp_path / "idx.snap")
+    eng.snapshot_save(p)
+    want = eng.match_packed(w.tbytes, w.toff)
+    wpub = eng.publish([w.topic(i) for i in range(2000)])
+    got_eng = emqx.Engine()
+    got_eng.snapshot_load(p)
+    got = got_eng.match_packed(w.tbytes, w.toff)
+    assert np.array_equal(got.row_ptr, want.row_ptr)
+    assert np.array_equal(got.filter_id, want.filter_id)
+    assert np.array_equal(got.exact_id, want.exact_id)
+    gpub = got_eng.publish([w.topic(i) for i in range(2000)])
+    for a, b in ((gpub.route_ptr, wpub.route_ptr), (gpub.route_filter, wpub.route_filter),
+                 (gpub.route_dest, wpub.route_dest), (gpub.deliver_sub, wpub.deliver_sub)):
+        assert np.array_equal(a, b)
+    assert got_eng.stats()["n_trie_filters"] == eng.stats()["n_trie_filters"]
+    # delta commits continue on the restored model
+    for e in (eng, got_eng):
+        e.trie_delete(b"#")
+        e.trie_insert(b"l0w1/+/#")
+        e.commit()
+    assert got_eng.stats()["delta_commits"] >= 1
+    a, b = eng.match_packed(w.tbytes, w.toff), got_eng.match_packed(w.tbytes, w.toff)
+    assert np.array_equal(a.row_ptr, b.row_ptr) and np.array_equal(a.filter_id, b.filter_id)
+    with pytest.raises(emqx.EngineError):
+        got_eng.snapshot_load(p)  # not a fresh handle
+    eng.close()
+    got_eng.close()
+
+
+def _subset(w, idx):
+    lens = (w.foff[idx + 1] - w.foff[idx]).astype(np.int64)
+    off = np.zeros(len(idx) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    starts = w.foff[idx].astype(np.int64)
+    pos = np.repeat(starts - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(lens.sum())
+    return w.fbytes[pos], off

@@ -6,8 +6,9 @@ HIP runtime (device memory = host memory, k_patch applied on the CPU): random su
 unsubscribe / route-key / route / subscriber churn on a delta-committing engine and a rebuilding
 one, every commit's device tables walked on the CPU as k_walk walks them and compared with the
 oracle (oracle/ref_trie.cpp, restating emqx_trie.erl:113-144, 242-260, 282-348), the exact table
-probed as k_exact probes it, every fan-out entry compared with the registry.  Any sanitizer
-report or mismatch fails the run."""
+probed as k_exact probes it, every fan-out entry compared with the registry; halfway through,
+the delta-committing engine is saved to a snapshot and replaced by a fresh engine loaded from it.
+Any sanitizer report or mismatch fails the run."""
 import os
 import subprocess
 
@@ -37,16 +38,17 @@ def _build():
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("seed,rounds,hash_bits", [(11, 25, 0), (12, 12, 3)])
-def test_engine_host_code_under_asan_ubsan(seed, rounds, hash_bits):
+def test_engine_host_code_under_asan_ubsan(seed, rounds, hash_bits, tmp_path):
     exe = _build()
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
-    r = subprocess.run([exe, str(seed), str(rounds), str(hash_bits)], stdout=subprocess.PIPE,
-                       stderr=subprocess.STDOUT, text=True, env=env, timeout=540)
+    r = subprocess.run([exe, str(seed), str(rounds), str(hash_bits), str(tmp_path)],
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env,
+                       timeout=540)
     assert r.returncode == 0, r.stdout[-6000:]
     last = r.stdout.strip().splitlines()[-1].split()
     assert last[0] == "OK", r.stdout[-2000:]
     commits, delta, full, checks = map(int, last[1:])
-    assert delta + full >= commits and checks > 0
+    assert commits > 0 and checks > 0  # (the counts are the restored engine's: it replaced the first)
     if hash_bits == 0:
         assert delta > 0 and full > 0  # both commit paths ran
