@@ -498,7 +498,9 @@ bool is_wild(const uint8_t* p, uint32_t len) {  // emqx_topic:wildcard/1
 }
 
 void slots_grow(emqxgm* h) {
-  const uint64_t cap = std::max<uint64_t>(1024, (h->slot_mask + 1) * 2);
+  // at least twice the registered filters (a snapshot load re-indexes them all at once)
+  const uint64_t cap = std::max<uint64_t>(
+      std::max<uint64_t>(1024, (h->slot_mask + 1) * 2), pow2_at_least(4 * h->filters.size()));
   std::vector<uint32_t> ns(cap, 0);
   for (uint32_t id = 0; id < h->filters.size(); ++id) {
     const Filter& f = h->filters[id];

@@ -275,7 +275,7 @@ int main(int argc, char** argv) {
     }
     const int mode = (int)rnd(10);
     CHECK(emqxgm_tune(hd, "delta_commit", mode == 0 ? 0 : mode == 1 ? 2 : 1) == 0, "tune");
-    const int ops = (int)(round == 0 ? 600 : 1 + rnd(120));
+    const int ops = (int)(round == 0 ? 3000 : 1 + rnd(120));  // > 1024 filters registered
     for (int k = 0; k < ops; ++k) {
       // filters [0, 1000) take trie / route-key churn, [1000, ...) route + subscriber churn
       const uint64_t op = rnd(6);
