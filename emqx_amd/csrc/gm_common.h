@@ -122,6 +122,11 @@ GM_HD uint32_t cf_with_depth_code(uint32_t cf, uint32_t h) {
 }
 constexpr uint32_t CF_TW = 1u << 30;    // child terminates >=1 wildcard filter
 constexpr uint32_t CF_TN = 1u << 31;    // child terminates >=1 non-wildcard trie key
+// In the carried copy of a '+' child's cf (p.cf) bit 31 means something else: a '+' node never
+// ends a non-wildcard key (a path through '+' is a wildcard filter), so CF_TN is free there and
+// CF_PTW says "p.hf holds the child's terminal filters (tw), it has no '#' filter": the walk then
+// emits them without a '+' probe.
+constexpr uint32_t CF_PTW = 1u << 31;
 constexpr uint32_t LIST_MULTI = 0x80000000u;  // tw/tn value is a multi[] index
 
 GM_HD uint64_t edge_slot(uint32_t parent, uint64_t tok, uint64_t mask) {

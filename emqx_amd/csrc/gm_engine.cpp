@@ -276,8 +276,13 @@ struct TrieModel {
     const uint32_t p = pchild[c];
     sl[0] = make_uint4((uint32_t)tok[c], (uint32_t)(tok[c] >> 32),
                        parent[c] | ((uint32_t)sig[c] << SIG_SHIFT), cf(c));
-    sl[1] = make_uint4(hfd(c), tw[c], p ? cf(p) : 0u, p ? hfd(p) : NONE);
+    sl[1] = make_uint4(hfd(c), tw[c], p ? pcf(p) : 0u, p ? phf(p) : NONE);
   }
+  // the carried copy of '+' child p (gm_common.h CF_PTW): its '#' filter, or -- when it has
+  // none -- its terminal filters, flagged
+  bool ptw(uint32_t p) const { return hf[p] == NONE && tw[p] != NONE; }
+  uint32_t pcf(uint32_t p) const { return cf(p) | (ptw(p) ? CF_PTW : 0u); }
+  uint32_t phf(uint32_t p) const { return ptw(p) ? tw[p] : hfd(p); }
   uint32_t new_node(uint32_t par, uint64_t t) {
     const uint32_t c = (uint32_t)parent.size();
     parent.push_back(par);
@@ -435,7 +440,10 @@ struct emqxgm {
     uint64_t bytes_len = 0;
   } hpipes[EMQXGM_HOST_PIPES];
   uint64_t next_hticket = 1;
-  uint32_t host_out_mode = 1;  // results to the host: 1 = copy kernel, 0 = hipMemcpyAsync
+  // results to the host: 0 = hipMemcpyAsync (SDMA; default), 1 = copy kernel writing host
+  // memory over PCIe.  Measured on cfg3 (profiles/r02/pcie_e2e.json): 1.24 vs 1.02 G topics/s
+  // host-in/host-out -- the kernel's PCIe writes contend with the uploads
+  uint32_t host_out_mode = 0;
 
   // ---- delta commits (writer side) ----
   TrieModel tm;
@@ -860,8 +868,8 @@ int upload_model(emqxgm* h, TrieModel& m) {
   nx.root_cf = m.cf(0);
   nx.root_sig = m.sig[0];
   nx.root_hf = m.hfd(0);
-  nx.root_pcf = root_p ? m.cf(root_p) : 0u;
-  nx.root_phf = root_p ? m.hfd(root_p) : NONE;
+  nx.root_pcf = root_p ? m.pcf(root_p) : 0u;
+  nx.root_phf = root_p ? m.phf(root_p) : NONE;
   nx.test_mask = h->test_mask;
   nx.needs_verify = m.needs_verify;
   nx.full_mask = fmask;
@@ -1254,8 +1262,8 @@ int commit_delta(emqxgm* h) {
   ix.root_cf = m.cf(0);
   ix.root_sig = m.sig[0];
   ix.root_hf = m.hfd(0);
-  ix.root_pcf = root_p ? m.cf(root_p) : 0u;
-  ix.root_phf = root_p ? m.hfd(root_p) : NONE;
+  ix.root_pcf = root_p ? m.pcf(root_p) : 0u;
+  ix.root_phf = root_p ? m.phf(root_p) : NONE;
   ix.needs_verify = m.needs_verify;
   ix.max_depth = m.max_depth;
   ix.trie_empty = (m.n_trie == 0);
@@ -2866,7 +2874,7 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
     h->leafp_mask = value ? CF_HMASK : 0u;
     return 0;
   }
-  if (strcmp(key, "host_out") == 0) {  // host pipes' result copy: 1 kernel, 0 hipMemcpyAsync
+  if (strcmp(key, "host_out") == 0) {  // host pipes' result copy: 0 hipMemcpyAsync (default), 1 kernel
     if (value < 0 || value > 1) return -EINVAL;
     std::lock_guard<std::mutex> g(h->mmu);
     for (auto& p : h->hpipes)

@@ -25,7 +25,10 @@ constexpr uint32_t SCAN_ITEMS = 16;
 constexpr uint32_t SCAN_TILE = WG * SCAN_ITEMS;
 constexpr uint32_t TILE_BYTES = 16384;  // tokenizer LDS tile (256 topics)
 constexpr uint32_t TILE_CHUNKS = TILE_BYTES / 16 + 2;
-constexpr uint64_t XBIN_MIN_TABLE = 2ull << 30;  // exact tables beyond this are probed binned
+// Exact tables beyond this are probed binned (k_xbin ...).  Off for now: binning turned the
+// probe's per-name reads (offsets, bytes, exact id) into random gathers and cost more than the
+// TLB misses it saved (cfg4: 0.170 vs 0.086 ms, profiles/r02/).
+constexpr uint64_t XBIN_MIN_TABLE = ~0ull;
 constexpr uint32_t XBIN_MIN_NAMES = 65536;
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }

@@ -341,7 +341,7 @@ int emqxgm_walk_census_levels(emqxgm_t* h, uint64_t* out, uint32_t n_out);
 int emqxgm_set_profiling(emqxgm_t* h, int on);
 /* Runtime tuning knobs: "walk_wg_per_cu" (persistent walk workgroups per CU); "leaf_prune"
  * (1 default: depth-code pruning in the walk, 0 off); "host_out" (host pipes copy results to the
- * host with a kernel, 1 default, or with hipMemcpyAsync, 0);
+ * host with hipMemcpyAsync, 0 default, or with a kernel writing host memory, 1);
  * "delta_commit": 0 = every commit rebuilds the index, 1 = small deltas are patched in place
  * (default), 2 = every delta that fits the tables' load bounds is patched in place. */
 int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value);

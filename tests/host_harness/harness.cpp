@@ -119,11 +119,12 @@ struct CpuWalk {
     pcf = strip(pcf, d + 1);
     visit(cf, hf, tw, d, lit);
     if (!plus_ok || d >= n || !(cf & CF_PLUS)) return;
-    if (d + 1 == n && (pcf & CF_TW)) {
+    const bool ptw = (pcf & CF_PTW) != 0;  // the carried copy holds the child's tw, no hf
+    if (d + 1 == n && (pcf & CF_TW) && !ptw) {
       stk.push_back({IT_PLUS | (cf & CF_ID_MASK), d});
       return;
     }
-    visit(pcf, phf, NONE, d + 1, false);
+    visit(pcf & ~CF_PTW, ptw ? NONE : phf, ptw ? phf : NONE, d + 1, false);
     if (d + 1 < n && (pcf & CF_PLUS)) stk.push_back({IT_PLUS | (pcf & CF_ID_MASK), d + 1});
   }
   // the edge slot of (node, key): probes buckets like k_walk (a bucket with an empty slot ends)
