@@ -434,6 +434,8 @@ struct emqxgm {
     uint64_t bytes_cap = 0, off_cap = 0;
     uint32_t* h_row = nullptr;  // pinned results: row pointers [n+1], exact ids [n], filter ids
     uint32_t* h_exact = nullptr;
+    uint32_t* h_none = nullptr;  // [row_cap] all NONE: the exact ids of a batch without any hit
+    bool exact_none = false;
     uint32_t* h_fid = nullptr;
     uint64_t row_cap = 0, fid_cap = 0;  // entries
     uint32_t n = 0, pairs = 0;
@@ -444,6 +446,7 @@ struct emqxgm {
   // memory over PCIe.  Measured on cfg3 (profiles/r02/pcie_e2e.json): 1.24 vs 1.02 G topics/s
   // host-in/host-out -- the kernel's PCIe writes contend with the uploads
   uint32_t host_out_mode = 0;
+  uint64_t xrange_bytes = 0;  // emqxgm_tune("exact_range_kb")
 
   // ---- delta commits (writer side) ----
   TrieModel tm;
@@ -1422,9 +1425,7 @@ int ensure_scratch(emqxgm* h, PassCtx& c, uint32_t n, uint64_t words, uint32_t p
       (rc = dev_alloc(h, c, (void**)&s.row2, (size_t)(ncap + 1) * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.rej, (size_t)ncap * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.exact_id, (size_t)ncap * 4)) ||
-      (rc = dev_alloc(h, c, (void**)&s.xbin, (size_t)ncap)) ||
-      (rc = dev_alloc(h, c, (void**)&s.xord, (size_t)ncap * 4)) ||
-      (rc = dev_alloc(h, c, (void**)&s.xcnt, 2 * (XBINS + 1) * 4)) ||
+      (rc = dev_alloc(h, c, (void**)&s.xh, (size_t)ncap * 8)) ||
       (rc = dev_alloc(h, c, (void**)&s.stg, (size_t)pcap * 16)) ||
       (rc = dev_alloc(h, c, (void**)&s.chk, (size_t)(pcap / STAGE_CHUNK + 1) * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.out, (size_t)pcap * 4)) ||
@@ -1817,11 +1818,15 @@ int host_pipe_reserve(emqxgm* h, emqxgm::HostPipe& p, uint64_t n, uint64_t bytes
   if (n + 1 > p.row_cap) {
     if (p.h_row) (void)hipHostFree(p.h_row);
     if (p.h_exact) (void)hipHostFree(p.h_exact);
-    p.h_row = p.h_exact = nullptr;
+    delete[] p.h_none;
+    p.h_row = p.h_exact = p.h_none = nullptr;
     p.row_cap = 0;
     const uint64_t cap = std::max<uint64_t>(n + 1 + n / 4, 1 << 16);
     int rc = 0;
     if ((rc = host_buf(h, &p.h_row, cap)) || (rc = host_buf(h, &p.h_exact, cap))) return rc;
+    p.h_none = new (std::nothrow) uint32_t[cap];
+    if (!p.h_none) return -ENOMEM;
+    std::fill(p.h_none, p.h_none + cap, NONE);
     p.row_cap = cap;
   }
   if (fid > p.fid_cap) {
@@ -1837,8 +1842,10 @@ int host_pipe_reserve(emqxgm* h, emqxgm::HostPipe& p, uint64_t n, uint64_t bytes
 
 // The pass's results into the host pipe's pinned buffers, enqueued on its stream: by a copy
 // kernel writing host memory over PCIe (the pair count is read on the device, so nothing waits
-// for the host), or by hipMemcpyAsync for the fixed-size arrays (the filter ids then follow in
-// _wait, once their count is known).
+// for the host), or by hipMemcpyAsync for the row pointers (the filter ids then follow in _wait,
+// once their count is known, and so do the exact ids, only when some name has a route key:
+// CTL_XHIT; otherwise the batch's exact ids are a prefilled all-NONE buffer and nothing crosses
+// PCIe for them -- a 4M-topic batch's 16 MB).
 int host_pipe_copy_out(emqxgm* h, emqxgm::HostPipe& p) {
   const Scratch& s = p.c.sc;
   void *dr = nullptr, *de = nullptr, *df = nullptr;
@@ -1852,7 +1859,6 @@ int host_pipe_copy_out(emqxgm* h, emqxgm::HostPipe& p) {
     HIPCHK(h, launch_copy_out(a, b, f, p.c.stream));
   } else {
     HIPCHK(h, hipMemcpyAsync(p.h_row, s.row, ((size_t)p.n + 1) * 4, hipMemcpyDeviceToHost, p.c.stream));
-    HIPCHK(h, hipMemcpyAsync(p.h_exact, s.exact_id, (size_t)p.n * 4, hipMemcpyDeviceToHost, p.c.stream));
   }
   return 0;
 }
@@ -1864,33 +1870,44 @@ int host_pipe_complete(emqxgm* h, emqxgm::HostPipe& p) {
   HIPCHK(h, hipStreamSynchronize(p.c.stream));
   bool legacy = false;
   int rc = pass_check(h, p.c, p.n, p.bytes_len, 0, legacy);
-  bool copied = h->host_out_mode == 1;
+  // copy_out enqueued the row pointers behind the pass (both modes), the copy kernel (mode 1)
+  // the exact ids and up to fid_cap filter ids too; a redone pass copies everything here
+  bool rows_copied = true;
   if (rc == 0) {
     rc = pass_finish(h, p.c, p.n, false, &p.pairs, nullptr);
   } else if (rc == 1) {
     rc = run_device(h, p.c, p.d_bytes, p.d_off, p.n, p.bytes_len, &p.pairs);
-    copied = false;
+    rows_copied = false;
   }
   p.c.epoch.reset();
   if (rc < 0) {
     p.state = 0;
     return rc;
   }
-  if (!copied || p.pairs > p.fid_cap) {
-    const Scratch& s = p.c.sc;
-    if ((rc = host_pipe_reserve(h, p, p.n, 0, p.pairs))) {
-      p.state = 0;
-      return rc;
-    }
+  const Scratch& s = p.c.sc;
+  const bool mode1 = h->host_out_mode == 1;
+  const bool fids_copied = rows_copied && mode1 && p.pairs <= p.fid_cap;
+  if (p.pairs > p.fid_cap && (rc = host_pipe_reserve(h, p, p.n, 0, p.pairs))) {
+    p.state = 0;
+    return rc;
+  }
+  bool enq = false;
+  if (!rows_copied) {
     HIPCHK(h, hipMemcpyAsync(p.h_row, s.row, ((size_t)p.n + 1) * 4, hipMemcpyDeviceToHost, p.c.stream));
+    enq = true;
+  }
+  // a redone pass refreshed ctl_host
+  const bool exact_copied = rows_copied && mode1;
+  p.exact_none = !exact_copied && s.ctl_host[CTL_XHIT] == 0;
+  if (!exact_copied && !p.exact_none) {
     HIPCHK(h, hipMemcpyAsync(p.h_exact, s.exact_id, (size_t)p.n * 4, hipMemcpyDeviceToHost, p.c.stream));
+    enq = true;
   }
-  if (!copied || p.pairs > p.fid_cap || h->host_out_mode != 1) {
-    if (p.pairs)
-      HIPCHK(h, hipMemcpyAsync(p.h_fid, p.c.sc.out, (size_t)p.pairs * 4, hipMemcpyDeviceToHost,
-                               p.c.stream));
-    HIPCHK(h, hipStreamSynchronize(p.c.stream));
+  if (!fids_copied && p.pairs) {
+    HIPCHK(h, hipMemcpyAsync(p.h_fid, s.out, (size_t)p.pairs * 4, hipMemcpyDeviceToHost, p.c.stream));
+    enq = true;
   }
+  if (enq) HIPCHK(h, hipStreamSynchronize(p.c.stream));
   p.state = 2;
   return 0;
 }
@@ -1901,6 +1918,7 @@ void host_pipe_free(emqxgm::HostPipe& p) {
   if (p.d_off) (void)hipFree(p.d_off);
   for (uint32_t* q : {p.h_row, p.h_exact, p.h_fid})
     if (q) (void)hipHostFree(q);
+  delete[] p.h_none;
   p = emqxgm::HostPipe();
 }
 
@@ -1943,6 +1961,7 @@ int emqxgm_create(const emqxgm_cfg* cfg, emqxgm_t** out) {
   }
   h->wstream = h->sync.stream;
   h->geom = walk_geometry(h->cfg.device, h->cfg.walk_wg_per_cu);
+  h->geom.xrange_bytes = h->xrange_bytes;
   int rc = commit_locked(h);  // empty index: epoch 1
   if (rc) {
     emqxgm_destroy(h);
@@ -2585,7 +2604,7 @@ int emqxgm_match_batch_wait(emqxgm_t* h, uint64_t ticket, emqxgm_batch_out* out)
   out->n_pairs = p.pairs;
   out->row_ptr = p.h_row;
   out->filter_id = p.h_fid;
-  out->exact_id = p.h_exact;
+  out->exact_id = p.exact_none ? p.h_none : p.h_exact;
   return 0;
 }
 
@@ -2866,6 +2885,7 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
     if (int rc = drain_pipes(h)) return rc;  // in-flight passes use the old geometry
     h->cfg.walk_wg_per_cu = (uint32_t)value;
     h->geom = walk_geometry(h->cfg.device, h->cfg.walk_wg_per_cu);
+    h->geom.xrange_bytes = h->xrange_bytes;
     return 0;  // spill scratch is re-sized by the next match (ensure_scratch)
   }
   if (strcmp(key, "leaf_prune") == 0) {  // 1 (default): the walk skips leaf-only children
@@ -2880,6 +2900,14 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
     for (auto& p : h->hpipes)
       if (p.state == 1) return -EBUSY;
     h->host_out_mode = (uint32_t)value;
+    return 0;
+  }
+  if (strcmp(key, "exact_range_kb") == 0) {  // 0 (default): auto; > 0: probe in ranges of v KiB
+    if (value < 0 || value > (int64_t)1 << 32) return -EINVAL;
+    std::lock_guard<std::mutex> g(h->mmu);
+    if (int rc = drain_pipes(h)) return rc;  // in-flight passes read the geometry
+    h->xrange_bytes = (uint64_t)value << 10;
+    h->geom.xrange_bytes = h->xrange_bytes;
     return 0;
   }
   if (strcmp(key, "delta_commit") == 0) {

@@ -52,9 +52,7 @@ struct Scratch {
   uint32_t* row2 = nullptr;   // [n+1] (legacy fix-up)
   uint32_t* rej = nullptr;    // [n]   rejected pairs per topic
   uint32_t* exact_id = nullptr;  // [n]
-  uint8_t* xbin = nullptr;    // [n]   exact probe: table range (bin) of each name's home bucket
-  uint32_t* xord = nullptr;   // [n]   names in bin order
-  uint32_t* xcnt = nullptr;   // [2 * (XBINS + 1)] bin counts, then cursors
+  uint2* xh = nullptr;        // [n]   exact probe over a huge table: {home bucket, h32} per name
   uint32_t p_cap = 0;   // pair staging capacity
   uint4* stg = nullptr;       // staged pairs {topic, filter, rank | REJ_BIT, 0}, CH-slot chunks
   uint32_t* chk = nullptr;    // per staged chunk: pairs in it (written by the walk)
@@ -78,7 +76,7 @@ enum : int {
   CTL_PAIR_TOP = 1,   // staged pair slots reserved
   CTL_ANY_REJ = 2,    // a verification rejected some pair
   CTL_TOTAL = 3,      // total pairs (row[n]) copied here
-  CTL_WORDS = 4,      // (unused)
+  CTL_XHIT = 4,       // some name of the batch has an exact route key (else exact_id is all NONE)
   CTL_NREJ = 5,       // rejected pairs appended to rlist
   CTL_LEGACY = 6,     // deferred scatter could not place rejects: re-run with the fix-up path
   CTL_ERR = 7,        // walk item stack outgrew its spill: re-run with a larger spill
@@ -101,8 +99,6 @@ constexpr uint32_t CENSUS_HDR = CENSUS_N + 2 * CENSUS_DEPTHS;
 constexpr uint32_t WALK_SHARDS = 8;
 constexpr uint32_t CTL_CLAIM_STRIDE = 32;
 
-constexpr uint32_t XBIN_BITS = 6;  // exact probe over a huge table: 64 table ranges
-constexpr uint32_t XBINS = 1u << XBIN_BITS;
 constexpr uint32_t STAGE_CHUNK = 1024;  // staged-pair slots a walk wave reserves per atomic
 constexpr uint32_t REJ_BIT = 0x80000000u;
 constexpr uint32_t REJ_SCAN_MAX = 4096;  // rejects the deferred scatter handles in-line
@@ -116,6 +112,9 @@ struct WalkGeom {
   uint32_t blocks = 0;      // persistent workgroups
   uint32_t lanes = 0;       // blocks * 256
   uint32_t cus = 0;
+  // exact route-key probe in passes over bucket ranges of this many bytes (0: one pass; see
+  // launch_exact); set by the engine, emqxgm_tune("exact_range_kb")
+  uint64_t xrange_bytes = 0;
 };
 
 WalkGeom walk_geometry(int device, uint32_t wg_per_cu);

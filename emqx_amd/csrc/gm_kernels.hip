@@ -25,11 +25,20 @@ constexpr uint32_t SCAN_ITEMS = 16;
 constexpr uint32_t SCAN_TILE = WG * SCAN_ITEMS;
 constexpr uint32_t TILE_BYTES = 16384;  // tokenizer LDS tile (256 topics)
 constexpr uint32_t TILE_CHUNKS = TILE_BYTES / 16 + 2;
-// Exact tables beyond this are probed binned (k_xbin ...).  Off for now: binning turned the
-// probe's per-name reads (offsets, bytes, exact id) into random gathers and cost more than the
-// TLB misses it saved (cfg4: 0.170 vs 0.086 ms, profiles/r02/).
-constexpr uint64_t XBIN_MIN_TABLE = ~0ull;
-constexpr uint32_t XBIN_MIN_NAMES = 65536;
+// The route-key probe over a table beyond the TLB's reach: random lines over a 2-3 GiB table
+// come at ~52 G/s, over 4 GiB at 23 G/s and 8 GiB at 17 G/s (profiles/r02/gather_tlb.txt;
+// contiguous or 1-GiB-granule allocations change nothing, profiles/r02/gather_alloc.txt).  Two
+// ways to give the lines in flight a few ranges' translations were measured on cfg4 (100M keys,
+// 8.6 GB, 1M names) and are slower than one pass over the whole table (0.103 ms):
+//   * passes over 2-GiB bucket ranges (k_xhash + one k_exact_range per range, gm_tok.inc):
+//     0.015 + 5 x 0.031 ms -- each pass re-reads every name's hash and runs its names' chain
+//     of dependent loads (offsets, bytes, bucket) at a quarter of the lanes' occupancy;
+//   * names binned by range and probed in that order: 0.170 ms (random per-name gathers).
+// The ranged passes stay as an option (emqxgm_tune("exact_range_kb"), tested) and are never
+// chosen by default (XRANGE_MIN_TABLE).
+constexpr uint64_t XRANGE_MIN_TABLE = ~0ull;
+constexpr uint32_t XRANGE_MIN_NAMES = 65536;
+constexpr uint64_t XRANGE_DEFAULT = 2ull << 30;
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
@@ -310,6 +319,7 @@ hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, con
   a.wh = sc.wh;
   a.rec = sc.rec;
   a.exact_id = sc.exact_id;
+  a.ctl = sc.ctl;
   a.test_mask = ix.test_mask;
   a.wild_empty = ix.wild_empty;
   if (ix.plain_empty)
@@ -323,25 +333,22 @@ hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, c
                         Scratch& sc, const WalkGeom& g, hipStream_t s) {
   if (n == 0 || ix.plain_empty) return hipSuccess;
   const uint64_t buckets = ix.xwbase + ix.xwmask + 1;
-  if (buckets * 64ull <= XBIN_MIN_TABLE || n < XBIN_MIN_NAMES) {
+  const bool forced = g.xrange_bytes != 0;
+  const uint64_t rb = std::max<uint64_t>(1, (forced ? g.xrange_bytes : XRANGE_DEFAULT) / 64);
+  if ((!forced && (buckets * 64ull <= XRANGE_MIN_TABLE || n < XRANGE_MIN_NAMES)) ||
+      buckets >= NONE) {
     hipLaunchKernelGGL(k_exact, dim3(grid_for(n, 1u << 20)), dim3(WG), 0, s, bytes, off, n,
-                       sc.exact_id, exact_args(ix), ix.wild_empty);
+                       sc.exact_id, exact_args(ix), ix.wild_empty, sc.ctl);
     return hipGetLastError();
   }
-  uint32_t bits = 0;
-  while ((1ull << bits) < buckets) ++bits;
-  const uint32_t shift = bits > XBIN_BITS ? bits - XBIN_BITS : 0u;
-  hipError_t e = hipMemsetAsync(sc.xcnt, 0, 2 * (XBINS + 1) * 4, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_xbin, dim3(grid_for(n, g.cus * 8)), dim3(WG), 0, s, bytes, off, n,
-                     sc.exact_id, exact_args(ix), ix.wild_empty, shift, sc.xbin, sc.xcnt);
-  hipLaunchKernelGGL(k_xoff, dim3(1), dim3(64), 0, s, sc.xcnt);
-  hipLaunchKernelGGL(k_xplace, dim3(grid_for(n, g.cus * 4)), dim3(WG), 0, s, sc.xbin, n, sc.xcnt,
-                     sc.xord);
-  // a quarter of the batch in flight at once: each sweep spans about a quarter of the table
-  hipLaunchKernelGGL(k_exact_binned, dim3(std::min<uint32_t>(g.cus * 4, grid_for(n, 1u << 20))),
-                     dim3(WG), 0, s, bytes, off, n, sc.exact_id, exact_args(ix), ix.wild_empty,
-                     sc.xord);
+  const ExactArgs X = exact_args(ix);
+  hipLaunchKernelGGL(k_xhash, dim3(grid_for(n, 1u << 20)), dim3(WG), 0, s, bytes, off, n,
+                     sc.exact_id, X, ix.wild_empty, sc.xh);
+  for (uint64_t lo = 0; lo < buckets; lo += rb) {
+    const uint64_t hi = std::min<uint64_t>(buckets, lo + rb);
+    hipLaunchKernelGGL(k_exact_range, dim3(grid_for(n, 1u << 20)), dim3(WG), 0, s, bytes, off, n,
+                       sc.exact_id, X, (const uint2*)sc.xh, (uint32_t)lo, (uint32_t)hi, sc.ctl);
+  }
   return hipGetLastError();
 }
 
@@ -404,7 +411,9 @@ hipError_t launch_verify(const uint8_t* bytes, const uint32_t* off, const DevInd
   a.rlist = sc.rlist;
   a.rcap = sc.r_cap;
   a.ctl = sc.ctl;
-  hipLaunchKernelGGL(k_verify, dim3(grid_for(sc.p_cap, g.cus * 8)), dim3(WG), 0, s, a);
+  // a block per staging chunk (up to 16 per CU): a sparse pass (a few pairs in each of many
+  // waves' chunks) is one dependent chain of loads per chunk, all chunks at once
+  hipLaunchKernelGGL(k_verify, dim3(std::min<uint32_t>(sc.p_cap / CH, g.cus * 16)), dim3(WG), 0, s, a);
   return hipGetLastError();
 }
 

@@ -224,6 +224,10 @@ def test_host_pipes_equal_match_batch(emqx):
         for pat in itertools.product((0, 1), repeat=k):
             lv = ["+" if x else words[i] for i, x in enumerate(pat)]
             eng.trie_insert(("/".join(lv + ["#"]) if k < 10 else "/".join(lv)).encode())
+    # plain route keys for some names of the first batch only: the other batches have no exact
+    # hit, so their exact ids come from the pipe's all-NONE buffer (no download, CTL_XHIT)
+    for i in range(0, 10000, 7):
+        eng.route_ref(w.topic(i))
     eng.commit()
     heavy = ["/".join(words).encode()] * 1000  # ~2M pairs: overflows a fresh pipe's staging
     batches = []

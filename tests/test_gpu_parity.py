@@ -244,19 +244,23 @@ def test_wildcard_topic_routes_exact_only(emqx):
                                                (b"a/b", "node")]
 
 
+@pytest.mark.parametrize("range_kb", [0, 1])
 @pytest.mark.parametrize("full_bits", [64, 2])
 @pytest.mark.parametrize("kinds", ["wild", "plain", "both"])
-def test_route_key_regions(emqx, kinds, full_bits):
+def test_route_key_regions(emqx, kinds, full_bits, range_kb):
     """Route keys live in two regions of the exact table (plain names, wildcard strings): a
     publish name only probes the region of its own kind.  Only-wildcard keys (the IoT-tree
     case: no probe for plain names at all), only-plain keys, both; 2-bit key hashes force every
-    key of a region onto one probe chain; a 40 kB wildcard name takes the global-memory path."""
+    key of a region onto one probe chain; a 40 kB wildcard name takes the global-memory path.
+    range_kb=1: the probe runs in passes over 16-bucket ranges (k_xhash + k_exact_range, the
+    path of tables beyond 3 GiB), chains running across range ends and the region boundary."""
     rng = random.Random(17)
     wild = [f"s/{i}/+/#".encode() for i in range(300)] + [b"+", b"#", b"a/+/b", b"+/+"]
     plain = [f"s/{i}/x/y".encode() for i in range(300)] + [b"", b"a", b"a//b", b"$SYS/x"]
     longw = b"/".join([b"w" * 50] * 800) + b"/+"
     keys = (wild + [longw] if kinds != "plain" else []) + (plain if kinds != "wild" else [])
     eng = emqx.Engine(full_hash_bits=full_bits)
+    eng.tune("exact_range_kb", range_kb)
     for k in keys:
         eng.route_ref(k)
     eng.commit()
@@ -475,6 +479,11 @@ def test_cfg4_exact_heavy_10m(emqx):
     eng, ref = _load_both(emqx, w)
     res = _assert_engine_equals_ref(eng, ref, None, w.tbytes, w.toff)
     assert (res.exact_id != emqx.NONE).mean() > 0.85
+    # the same batch probed in passes over 64-MiB bucket ranges (the > 3 GiB table path)
+    eng.tune("exact_range_kb", 64 << 10)
+    res2 = eng.match_packed(w.tbytes, w.toff)
+    assert np.array_equal(res2.exact_id, res.exact_id)
+    assert np.array_equal(res2.row_ptr, res.row_ptr) and np.array_equal(res2.filter_id, res.filter_id)
 
 
 def test_cfg4_full_size(emqx):

@@ -7,6 +7,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <stdint.h>
+#include <algorithm>
 
 #define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
@@ -48,6 +49,8 @@ __global__ __launch_bounds__(256) void k_gather(const uint4* __restrict__ tab, u
 
 int main(int argc, char** argv) {
   // usage: gather_bench [table_MiB=2048] [wg_per_cu=8] [width_16B_units=0 (all)] [depth=0 (all)]
+  //                     [alloc=0: hipMalloc, 1: hipExtMallocWithFlags(hipDeviceMallocContiguous),
+  //                      2: hipMemCreate/hipMemMap at 1 GiB granularity]
   const uint64_t mb = argc > 1 ? atoll(argv[1]) : 2048;
   const int wgpc = argc > 2 ? atoi(argv[2]) : 8;
   const int only_w = argc > 3 ? atoi(argv[3]) : 0;
@@ -57,7 +60,34 @@ int main(int argc, char** argv) {
   const uint64_t bytes = mb << 20;
   uint4* tab;
   uint64_t* out;
-  CHK(hipMalloc(&tab, bytes));
+  const int alloc = argc > 5 ? atoi(argv[5]) : 0;
+  if (alloc == 1) {
+    CHK(hipExtMallocWithFlags((void**)&tab, bytes, hipDeviceMallocContiguous));
+  } else if (alloc == 2) {
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = 0;
+    size_t gran = 0;
+    CHK(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended));
+    const size_t chunk = std::max<size_t>(gran, 1ull << 30);
+    const size_t total = (bytes + chunk - 1) / chunk * chunk;
+    void* va = nullptr;
+    CHK(hipMemAddressReserve(&va, total, chunk, nullptr, 0));
+    for (size_t o = 0; o < total; o += chunk) {
+      hipMemGenericAllocationHandle_t hnd;
+      CHK(hipMemCreate(&hnd, chunk, &prop, 0));
+      CHK(hipMemMap((char*)va + o, chunk, 0, hnd, 0));
+    }
+    hipMemAccessDesc acc = {};
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    CHK(hipMemSetAccess(va, total, &acc, 1));
+    tab = (uint4*)va;
+    printf("vmm granularity %zu, chunk %zu\n", gran, chunk);
+  } else {
+    CHK(hipMalloc(&tab, bytes));
+  }
   CHK(hipMalloc(&out, 64));
   CHK(hipMemset(tab, 1, bytes));
   hipEvent_t a, b;
@@ -65,7 +95,7 @@ int main(int argc, char** argv) {
   CHK(hipEventCreate(&b));
   const int blocks = p.multiProcessorCount * wgpc;
   const int rounds = 64;
-  printf("table %llu MiB, %d CUs x %d WG, %d rounds\n", (unsigned long long)mb, p.multiProcessorCount, wgpc, rounds);
+  printf("table %llu MiB, %d CUs x %d WG, %d rounds, alloc %d\n", (unsigned long long)mb, p.multiProcessorCount, wgpc, rounds, alloc);
   for (int W : {1, 2, 4}) {
     if (only_w && W != only_w) continue;
     for (int depth : {1, 2, 4}) {
