@@ -83,7 +83,8 @@ enum : int {
   CTL_FAN_R = 9,      // publish fan-out: aggre entries of the batch
   CTL_FAN_D = 10,     //   local deliveries of the batch
   CTL_CLAIM0 = 16,    // walk topic-claim counters, one per shard, CTL_CLAIM_STRIDE apart
-  CTL_N = 16 + 8 * 32
+  CTL_SHARDS_OUT = 16 + 8 * 32,  // walk: bit c = claim shard c ran out (a line of its own)
+  CTL_N = 16 + 9 * 32
 };
 
 // diagnostic walk counters: states, slot loads, lane iterations, wave iterations

@@ -210,8 +210,9 @@ int emqxgm_match_device_wait(emqxgm_t* h, uint64_t ticket, emqxgm_dev_out* out);
  * offsets stay untouched until the wait (pinned memory from emqxgm_host_alloc gives full-speed
  * copies).  The result (batch-local u32 row pointers, trie filter ids, exact ids) lives in
  * pinned buffers of the pipe and stays valid until ticket + EMQXGM_HOST_PIPES is submitted;
- * submitting that ticket before this one was waited for returns -EBUSY.  Results are identical
- * to emqxgm_match_batch's. */
+ * submitting that ticket before this one was waited for returns -EBUSY.  When no topic of the
+ * batch equals a route key, exact_id points at an all-EMQXGM_NONE buffer of the pipe (same
+ * lifetime) and no exact id crossed PCIe.  Results are identical to emqxgm_match_batch's. */
 #define EMQXGM_HOST_PIPES 3
 typedef struct emqxgm_batch_out {
   uint32_t n;
