@@ -1426,7 +1426,7 @@ int ensure_scratch(emqxgm* h, PassCtx& c, uint32_t n, uint64_t words, uint32_t p
       (rc = dev_alloc(h, c, (void**)&s.rej, (size_t)ncap * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.exact_id, (size_t)ncap * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.xh, (size_t)ncap * 8)) ||
-      (rc = dev_alloc(h, c, (void**)&s.stg, (size_t)pcap * 16)) ||
+      (rc = dev_alloc(h, c, (void**)&s.stg, (size_t)pcap * 12)) ||
       (rc = dev_alloc(h, c, (void**)&s.chk, (size_t)(pcap / STAGE_CHUNK + 1) * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.out, (size_t)pcap * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.out2, (size_t)pcap * 4)) ||

@@ -54,7 +54,7 @@ struct Scratch {
   uint32_t* exact_id = nullptr;  // [n]
   uint2* xh = nullptr;        // [n]   exact probe over a huge table: {home bucket, h32} per name
   uint32_t p_cap = 0;   // pair staging capacity
-  uint4* stg = nullptr;       // staged pairs {topic, filter, rank | REJ_BIT, 0}, CH-slot chunks
+  uint3* stg = nullptr;       // staged pairs {topic, filter, rank | REJ_BIT} (12 B), CH-slot chunks
   uint32_t* chk = nullptr;    // per staged chunk: pairs in it (written by the walk)
   uint32_t o_cap = 0;
   uint32_t* out = nullptr;    // [pairs] CSR filter ids
