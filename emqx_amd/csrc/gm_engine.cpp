@@ -180,7 +180,9 @@ struct Epoch {
   DevIndex ix;
   std::vector<OwnerP> owners;   // tables, fan-out tables, pool mirrors
   hipEvent_t ready = nullptr;   // this epoch's uploads / patches are complete (writer stream)
-  std::atomic<bool> walk_spill{false};  // its walks need the spilling variant (learnt by a pass)
+  // the walk variant its passes need (WalkLevel: shallow LDS stack, deep, deep + spill), learnt
+  // by passes whose lanes outgrew a stack; only ever raised
+  std::atomic<uint32_t> walk_level{WALK_SHALLOW};
   ~Epoch() {
     if (ready) (void)hipEventDestroy(ready);
   }
@@ -197,6 +199,7 @@ struct PassCtx {
   hipEvent_t done = nullptr;  // recorded after each pass enqueued here (guarded by emqxgm::emu)
   bool done_rec = false;
   EpochP epoch;               // epoch of the pass last enqueued here (kept until it completes)
+  uint32_t walk_level = 0;    // walk variant of that pass (WalkLevel)
 };
 
 constexpr uint64_t DEAD = ~0ull;  // TrieModel::slot of the root and of removed nodes
@@ -1296,7 +1299,7 @@ int publish_epoch(emqxgm* h, bool delta) {
   E->owners = {h->o_tab, h->o_fan, h->m_pool.o, h->m_foff.o, h->m_fver.o};
   HIPCHK(h, hipEventCreateWithFlags(&E->ready, hipEventDisableTiming));
   std::lock_guard<std::mutex> g(h->emu);
-  if (delta && h->cur) E->walk_spill.store(h->cur->walk_spill.load());
+  if (delta && h->cur) E->walk_level.store(h->cur->walk_level.load());
   if (!h->patches.ents.empty()) {
     int rc = 0;
     for_each_reader(h, [&](PassCtx& c) {
@@ -1504,8 +1507,8 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
   } else {
     // per-topic reject counts: only the verification passes write (and then read) them
     if (ix.needs_verify || legacy) HIPCHK(h, hipMemsetAsync(s.rej, 0, (size_t)n * 4, st));
-    HIPCHK(h, launch_walk(ix, s, n, h->geom, st, census ? s.census : nullptr,
-                          E.walk_spill.load(std::memory_order_relaxed)));
+    c.walk_level = E.walk_level.load(std::memory_order_relaxed);
+    HIPCHK(h, launch_walk(ix, s, n, h->geom, st, census ? s.census : nullptr, c.walk_level));
     if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[2], st));
     if (!legacy) {
       // pairs of filters made of short (exact) tokens need no byte check (gm_verify.inc)
@@ -1562,11 +1565,13 @@ int pass_check(emqxgm* h, PassCtx& c, uint32_t n, uint64_t bytes_len, int attemp
     int rc = ensure_scratch(h, c, n, words, (uint32_t)np);
     return rc ? rc : 1;
   }
-  if (s.ctl_host[CTL_ERR] && !E.walk_spill.load()) {
-    // a walk lane's item stack outgrew LDS: redo with the spilling variant (kept for this
-    // committed index)
+  if (s.ctl_host[CTL_ERR] && c.walk_level < WALK_SPILL) {
+    // a walk lane's item stack outgrew its LDS stack: redo with the next variant (deep stack,
+    // then deep + spill), kept for this committed index
     rerun();
-    E.walk_spill.store(true);
+    uint32_t cur = E.walk_level.load();
+    while (cur <= c.walk_level && !E.walk_level.compare_exchange_weak(cur, c.walk_level + 1)) {
+    }
     return 1;
   }
   if (s.ctl_host[CTL_ERR]) {

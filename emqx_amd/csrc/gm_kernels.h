@@ -103,7 +103,16 @@ constexpr uint32_t CTL_CLAIM_STRIDE = 32;
 constexpr uint32_t STAGE_CHUNK = 1024;  // staged-pair slots a walk wave reserves per atomic
 constexpr uint32_t REJ_BIT = 0x80000000u;
 constexpr uint32_t REJ_SCAN_MAX = 4096;  // rejects the deferred scatter handles in-line
-constexpr uint32_t WALK_LDS_STACK = 6;   // walk probe items per lane kept in LDS (rest spill)
+// Walk probe items per lane kept in LDS.  Passes start with the shallow stack (34 KB of LDS per
+// walk block: four blocks per CU leave room for the other pipe's tokenizer tile beside them);
+// an index whose walks outgrow it moves to the deep one (39 KB: four blocks still fit, the
+// tokenizer no longer does), then to the deep stack continued in global memory (spill).
+// Measured (profiles/r02/session2/ab_walk_stack.txt): cfg2 outgrows 6 items, and its walk on the
+// 8-deep stack takes 1.18 ms against 1.35 ms spilling; cfg3 never spills and loses ~1.5% of its
+// pipelined step with the deep stack.
+constexpr uint32_t WALK_STK_SHALLOW = 6;
+constexpr uint32_t WALK_STK_DEEP = 8;
+enum WalkLevel : uint32_t { WALK_SHALLOW = 0, WALK_DEEP = 1, WALK_SPILL = 2 };
 constexpr uint32_t WALK_SPILL_MIN = 32;  // initial spill items per lane (grown on overflow)
 // spill items per lane that no walk can exceed: a resolved probe pushes <= 4 items spanning
 // 3 levels, and the LIFO holds <= 3 unexplored siblings per level of the current path
@@ -177,10 +186,11 @@ hipError_t launch_patch(const PatchEnt* ents, uint32_t n, const uint32_t* src, h
 hipError_t launch_fanout(const DevIndex& ix, const Scratch& sc, FanScratch& fs, uint32_t n,
                          bool fill, hipStream_t s);
 
-// census != nullptr selects the diagnostic walk (adds to census[0..CENSUS_N)); spill selects
-// the variant whose probe-item stack continues in global memory (after an LDS overflow)
+// census != nullptr selects the diagnostic walk (adds to census[0..CENSUS_N)); level (WalkLevel)
+// the probe-item stack: shallow or deep in LDS, or deep continued in global memory (spill)
 hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGeom& g,
-                       hipStream_t s, unsigned long long* census = nullptr, bool spill = false);
+                       hipStream_t s, unsigned long long* census = nullptr,
+                       uint32_t level = WALK_SHALLOW);
 // production: verify (flags + counts) -> [scan] -> deferred scatter
 hipError_t launch_verify(const uint8_t* bytes, const uint32_t* off, const DevIndex& ix,
                          Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_t s);

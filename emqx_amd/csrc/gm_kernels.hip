@@ -353,7 +353,7 @@ hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, c
 }
 
 hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGeom& g,
-                       hipStream_t s, unsigned long long* census, bool spill) {
+                       hipStream_t s, unsigned long long* census, uint32_t level) {
   WalkArgs a;
   a.rec = sc.rec;
   a.wh = sc.wh;
@@ -382,14 +382,22 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   a.census = census;
   a.leafp_mask = ix.leafp_mask;
   a.root_sig = ix.root_sig;
-  if (census && spill)
-    hipLaunchKernelGGL((k_walk<true, true>), dim3(g.blocks), dim3(WG), 0, s, a);
-  else if (census)
-    hipLaunchKernelGGL((k_walk<true, false>), dim3(g.blocks), dim3(WG), 0, s, a);
-  else if (spill)
-    hipLaunchKernelGGL((k_walk<false, true>), dim3(g.blocks), dim3(WG), 0, s, a);
-  else
-    hipLaunchKernelGGL((k_walk<false, false>), dim3(g.blocks), dim3(WG), 0, s, a);
+  constexpr uint32_t SH = WALK_STK_SHALLOW, DP = WALK_STK_DEEP;
+  if (census) {
+    if (level >= WALK_SPILL)
+      hipLaunchKernelGGL((k_walk<true, true, DP>), dim3(g.blocks), dim3(WG), 0, s, a);
+    else if (level == WALK_DEEP)
+      hipLaunchKernelGGL((k_walk<true, false, DP>), dim3(g.blocks), dim3(WG), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_walk<true, false, SH>), dim3(g.blocks), dim3(WG), 0, s, a);
+  } else {
+    if (level >= WALK_SPILL)
+      hipLaunchKernelGGL((k_walk<false, true, DP>), dim3(g.blocks), dim3(WG), 0, s, a);
+    else if (level == WALK_DEEP)
+      hipLaunchKernelGGL((k_walk<false, false, DP>), dim3(g.blocks), dim3(WG), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_walk<false, false, SH>), dim3(g.blocks), dim3(WG), 0, s, a);
+  }
   return hipGetLastError();
 }
 
