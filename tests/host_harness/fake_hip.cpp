@@ -102,7 +102,7 @@ hipError_t launch_patch(const PatchEnt* ents, uint32_t n, const uint32_t* src, h
 hipError_t launch_scan(const uint32_t*, uint32_t*, uint32_t, uint32_t*, uint32_t*, hipStream_t) { NOT_HERE; }
 hipError_t launch_tok(const uint8_t*, const uint32_t*, uint32_t, const DevIndex&, Scratch&, hipStream_t) { NOT_HERE; }
 hipError_t launch_exact(const uint8_t*, const uint32_t*, uint32_t, const DevIndex&, Scratch&, const WalkGeom&, hipStream_t) { NOT_HERE; }
-hipError_t launch_walk(const DevIndex&, Scratch&, uint32_t, const WalkGeom&, hipStream_t, unsigned long long*, bool) { NOT_HERE; }
+hipError_t launch_walk(const DevIndex&, Scratch&, uint32_t, const WalkGeom&, hipStream_t, unsigned long long*, uint32_t) { NOT_HERE; }
 hipError_t launch_verify(const uint8_t*, const uint32_t*, const DevIndex&, Scratch&, uint32_t, const WalkGeom&, hipStream_t) { NOT_HERE; }
 hipError_t launch_scatter(Scratch&, uint32_t, const WalkGeom&, hipStream_t) { NOT_HERE; }
 hipError_t launch_verify_scatter(const uint8_t*, const uint32_t*, const DevIndex&, Scratch&, uint32_t, hipStream_t) { NOT_HERE; }

@@ -26,6 +26,9 @@ enum hipMemcpyKind {
 struct uint2 {
   uint32_t x, y;
 };
+struct uint3 {
+  uint32_t x, y, z;
+};
 struct uint4 {
   uint32_t x, y, z, w;
 };
