@@ -183,6 +183,8 @@ struct Epoch {
   // the walk variant its passes need (WalkLevel: shallow LDS stack, deep, deep + spill), learnt
   // by passes whose lanes outgrew a stack; only ever raised
   std::atomic<uint32_t> walk_level{WALK_SHALLOW};
+  std::atomic<uint32_t> census_level{WALK_SHALLOW};  // the same for diagnostic census passes
+                                                      // (their unpruned walks stack deeper)
   ~Epoch() {
     if (ready) (void)hipEventDestroy(ready);
   }
@@ -200,6 +202,7 @@ struct PassCtx {
   bool done_rec = false;
   EpochP epoch;               // epoch of the pass last enqueued here (kept until it completes)
   uint32_t walk_level = 0;    // walk variant of that pass (WalkLevel)
+  bool census = false;        // that pass was a census pass
 };
 
 constexpr uint64_t DEAD = ~0ull;  // TrieModel::slot of the root and of removed nodes
@@ -1299,7 +1302,10 @@ int publish_epoch(emqxgm* h, bool delta) {
   E->owners = {h->o_tab, h->o_fan, h->m_pool.o, h->m_foff.o, h->m_fver.o};
   HIPCHK(h, hipEventCreateWithFlags(&E->ready, hipEventDisableTiming));
   std::lock_guard<std::mutex> g(h->emu);
-  if (delta && h->cur) E->walk_level.store(h->cur->walk_level.load());
+  if (delta && h->cur) {
+    E->walk_level.store(h->cur->walk_level.load());
+    E->census_level.store(h->cur->census_level.load());
+  }
   if (!h->patches.ents.empty()) {
     int rc = 0;
     for_each_reader(h, [&](PassCtx& c) {
@@ -1507,7 +1513,8 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
   } else {
     // per-topic reject counts: only the verification passes write (and then read) them
     if (ix.needs_verify || legacy) HIPCHK(h, hipMemsetAsync(s.rej, 0, (size_t)n * 4, st));
-    c.walk_level = E.walk_level.load(std::memory_order_relaxed);
+    c.census = census;
+    c.walk_level = (census ? E.census_level : E.walk_level).load(std::memory_order_relaxed);
     HIPCHK(h, launch_walk(ix, s, n, h->geom, st, census ? s.census : nullptr, c.walk_level));
     if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[2], st));
     if (!legacy) {
@@ -1569,8 +1576,9 @@ int pass_check(emqxgm* h, PassCtx& c, uint32_t n, uint64_t bytes_len, int attemp
     // a walk lane's item stack outgrew its LDS stack: redo with the next variant (deep stack,
     // then deep + spill), kept for this committed index
     rerun();
-    uint32_t cur = E.walk_level.load();
-    while (cur <= c.walk_level && !E.walk_level.compare_exchange_weak(cur, c.walk_level + 1)) {
+    std::atomic<uint32_t>& lvl = c.census ? E.census_level : E.walk_level;
+    uint32_t cur = lvl.load();
+    while (cur <= c.walk_level && !lvl.compare_exchange_weak(cur, c.walk_level + 1)) {
     }
     return 1;
   }

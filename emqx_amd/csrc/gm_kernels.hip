@@ -419,9 +419,9 @@ hipError_t launch_verify(const uint8_t* bytes, const uint32_t* off, const DevInd
   a.rlist = sc.rlist;
   a.rcap = sc.r_cap;
   a.ctl = sc.ctl;
-  // a block per staging chunk (up to 16 per CU): a sparse pass (a few pairs in each of many
-  // waves' chunks) is one dependent chain of loads per chunk, all chunks at once
-  hipLaunchKernelGGL(k_verify, dim3(std::min<uint32_t>(sc.p_cap / CH, g.cus * 16)), dim3(WG), 0, s, a);
+  // a wave per staging chunk, every block resident at once (k_verify: 4 blocks per CU by LDS)
+  hipLaunchKernelGGL(k_verify, dim3(std::min<uint32_t>((sc.p_cap / CH + 3) / 4, g.cus * 4)), dim3(WG),
+                     0, s, a);
   return hipGetLastError();
 }
 

@@ -17,7 +17,8 @@ for f in glob.glob(root + "/**/*counter_collection.csv", recursive=True):
 out = {}
 for k, d in acc.items():
     out[k] = {c: sum(v) / len(v) for c, v in d.items()}
+    out[k]["n"] = max(len(v) for v in d.values())
     print(k)
-    for c in sorted(out[k]):
+    for c in sorted(d):
         print(f"   {c:24s} {out[k][c]:16.1f}  (n={len(d[c])})")
 json.dump(out, open(root + "/summary.json", "w"), indent=1)

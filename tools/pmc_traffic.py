@@ -26,6 +26,8 @@ kern = {}
 for name, k in s.items():
     if "FETCH_SIZE" not in k:
         continue
+    if "n" not in k:  # summaries written before launch counts were recorded
+        k["n"] = 1
     short = name.split("<")[0]
     corr = 2.0 if short.startswith(STREAMING) else 1.0
     fetch = k["FETCH_SIZE"] * 1024.0 * corr
@@ -33,8 +35,14 @@ for name, k in s.items():
     ent = {"kernel": name, "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
            "hbm_bytes_per_launch": fetch + write, "fetch_correction": corr,
            "tcc_hit": k.get("TCC_HIT_sum"), "tcc_miss": k.get("TCC_MISS_sum")}
-    # the production variant of a kernel wins over its census / spill variants
-    if short not in kern or name in ("k_walk<false, false>", "k_tok<true>", "k_tok<false>"):
+    # the production variant of a kernel (not a census walk; the one with the most launches)
+    # wins over the others
+    census = name.startswith("k_walk<true")
+    ent["n"] = k.get("n", 0)
+    prev = kern.get(short)
+    if prev is None or (prev["census"] and not census) or (
+            prev["census"] == census and ent["n"] > prev["n"]):
+        ent["census"] = census
         kern[short] = ent
 out = {"topics": a.topics, "cfg": a.cfg, "source": a.root, "kernels": kern}
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
