@@ -201,6 +201,7 @@ struct PassCtx {
   hipEvent_t done = nullptr;  // recorded after each pass enqueued here (guarded by emqxgm::emu)
   bool done_rec = false;
   EpochP epoch;               // epoch of the pass last enqueued here (kept until it completes)
+  bool own_stream = false;    // false: the stream is one of the handle's shared pipe streams
   uint32_t walk_level = 0;    // walk variant of that pass (WalkLevel)
   bool census = false;        // that pass was a census pass
 };
@@ -448,6 +449,7 @@ struct emqxgm {
     uint64_t bytes_len = 0;
   } hpipes[EMQXGM_HOST_PIPES];
   uint64_t next_hticket = 1;
+  hipStream_t pipe_streams[EMQXGM_HOST_PIPES] = {};  // pipe_stream(): shared by both pipe kinds
   // results to the host: 0 = hipMemcpyAsync (SDMA; default), 1 = copy kernel writing host
   // memory over PCIe.  Measured on cfg3 (profiles/r02/pcie_e2e.json): 1.24 vs 1.02 G topics/s
   // host-in/host-out -- the kernel's PCIe writes contend with the uploads
@@ -1385,9 +1387,27 @@ int dev_alloc(emqxgm* h, PassCtx& c, void** p, size_t bytes) {
 }
 
 // A reader context's stream and events (created on first use).
-int ctx_init(emqxgm* h, PassCtx& c) {
+// Stream k of the pipelined passes, shared by device pipe k and host pipe k.  HIP maps streams
+// onto GPU_MAX_HW_QUEUES (4) hardware queues: the synchronous context's stream plus these three
+// keep one queue each, where separate streams for the two device pipes and the three host pipes
+// (six in all) doubled pipes up on queues and serialised them (cfg1 host-in/host-out 46 M
+// topics/s in a process that had used both kinds, 366 M with host pipes alone).
+static_assert(EMQXGM_PIPES <= EMQXGM_HOST_PIPES, "device pipe k borrows host pipe k's stream");
+hipStream_t pipe_stream(emqxgm* h, uint32_t k) {
+  if (!h->pipe_streams[k] &&
+      hipStreamCreateWithFlags(&h->pipe_streams[k], hipStreamNonBlocking) != hipSuccess)
+    h->pipe_streams[k] = nullptr;
+  return h->pipe_streams[k];
+}
+
+int ctx_init(emqxgm* h, PassCtx& c, hipStream_t shared = nullptr) {
   if (c.stream) return 0;
-  HIPCHK(h, hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+  if (shared) {
+    c.stream = shared;
+  } else {
+    HIPCHK(h, hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    c.own_stream = true;
+  }
   for (auto& e : c.ev) HIPCHK(h, hipEventCreate(&e));
   HIPCHK(h, hipEventCreateWithFlags(&c.done, hipEventDisableTiming));
   return 0;
@@ -1396,7 +1416,7 @@ int ctx_init(emqxgm* h, PassCtx& c) {
 void ctx_free(PassCtx& c) {
   if (c.stream) {
     (void)hipStreamSynchronize(c.stream);
-    (void)hipStreamDestroy(c.stream);
+    if (c.own_stream) (void)hipStreamDestroy(c.stream);
   }
   for (auto& e : c.ev)
     if (e) (void)hipEventDestroy(e);
@@ -1900,7 +1920,8 @@ int host_pipe_complete(emqxgm* h, emqxgm::HostPipe& p) {
   const Scratch& s = p.c.sc;
   const bool mode1 = h->host_out_mode == 1;
   const bool fids_copied = rows_copied && mode1 && p.pairs <= p.fid_cap;
-  if (p.pairs > p.fid_cap && (rc = host_pipe_reserve(h, p, p.n, 0, p.pairs))) {
+  if (p.pairs > p.fid_cap &&
+      (rc = host_pipe_reserve(h, p, p.n, 0, (uint64_t)p.pairs + p.pairs / 4))) {
     p.state = 0;
     return rc;
   }
@@ -1989,6 +2010,8 @@ void emqxgm_destroy(emqxgm_t* h) {
   (void)hipSetDevice(h->cfg.device);
   for (auto& p : h->pipes) ctx_free(p.c);
   for (auto& p : h->hpipes) host_pipe_free(p);
+  for (auto& st : h->pipe_streams)
+    if (st) (void)hipStreamDestroy(st);
   ctx_free(h->sync);
   for (auto* b : {&h->hp_row, &h->hp_fid, &h->hp_exact})
     if (b->p) (void)hipHostFree(b->p);
@@ -2521,7 +2544,12 @@ int emqxgm_match_device_submit(emqxgm_t* h, const uint8_t* d_bytes, const uint32
     set_err(h, "pipe busy: wait for the ticket submitted EMQXGM_PIPES submissions ago");
     return -EBUSY;
   }
-  int rc = ctx_init(h, p.c);
+  hipStream_t ps = pipe_stream(h, (uint32_t)(tk % EMQXGM_PIPES));
+  if (!ps) {
+    set_err(h, "hipStreamCreateWithFlags failed");
+    return -EIO;
+  }
+  int rc = ctx_init(h, p.c, ps);
   if (rc) return rc;
   rc = pass_prepare(h, p.c, n, bytes_len);
   if (rc < 0) return rc;
@@ -2576,11 +2604,21 @@ int emqxgm_match_batch_submit(emqxgm_t* h, const uint8_t* bytes, const uint32_t*
     return -EBUSY;
   }
   const uint64_t nb = offsets[n];
-  int rc = ctx_init(h, p.c);
+  hipStream_t ps = pipe_stream(h, (uint32_t)(tk % EMQXGM_HOST_PIPES));
+  if (!ps) {
+    set_err(h, "hipStreamCreateWithFlags failed");
+    return -EIO;
+  }
+  int rc = ctx_init(h, p.c, ps);
   if (rc) return rc;
   rc = pass_prepare(h, p.c, n, nb);
   if (rc < 0) return rc;
-  if ((rc = host_pipe_reserve(h, p, n, std::max<uint64_t>(nb, 1), p.c.sc.p_cap))) return rc;
+  // the filter-id buffer: the copy kernel (host_out 1) writes up to its capacity behind the pass;
+  // the default path copies the ids in _wait, sized then by the pair count (a pinned allocation
+  // here would follow every staging growth and stall the stream)
+  if ((rc = host_pipe_reserve(h, p, n, std::max<uint64_t>(nb, 1),
+                              h->host_out_mode == 1 ? p.c.sc.p_cap : 1)))
+    return rc;
   p.n = n;
   p.bytes_len = nb;
   p.pairs = 0;
