@@ -227,35 +227,35 @@ def main():
             t1 = time.perf_counter()
             eng.match_packed(hb, ho, copy=False)
             best = min(best, time.perf_counter() - t1)
-        # the NIF batcher's call: emqxgm_match_batch_submit/_wait with two batches in flight (one
-        # batch's upload and pass overlap the other's download; a third in flight measured no
-        # better on 2M-topic batches and worse on small ones: tools/host_pipe_probe.py,
-        # profiles/r02/session2/host_pipe_probe_*.json)
+        # the NIF batcher's call: emqxgm_match_batch_submit/_wait with 2 and with 3 (all host
+        # pipes) batches in flight: one batch's upload and pass overlap another's download.  Which
+        # is faster depends on the batch (tools/host_pipe_probe.py,
+        # profiles/r02/session2/host_pipe_probe_*.json: 2 for small batches); both are reported
         k = max(20, args.steps)
-        inflight = 2
         pend = []
         for _ in range(2 * eng.HOST_PIPES):  # every pipe's scratch and buffers at their size
             pend.append(eng.match_batch_submit(hb, ho))
-            if len(pend) == inflight:
+            if len(pend) == eng.HOST_PIPES:
                 eng.match_batch_wait(pend.pop(0), copy=False)
         while pend:
             eng.match_batch_wait(pend.pop(0), copy=False)
-        r0 = eng.stats()["reruns"]
-        waits = []
-        t1 = time.perf_counter()
-        for _ in range(k):
-            pend.append(eng.match_batch_submit(hb, ho))
-            if len(pend) == inflight:
-                t2 = time.perf_counter()
+        by_inflight = {}
+        for inflight in (2, eng.HOST_PIPES):
+            r0 = eng.stats()["reruns"]
+            t1 = time.perf_counter()
+            for _ in range(k):
+                pend.append(eng.match_batch_submit(hb, ho))
+                if len(pend) == inflight:
+                    eng.match_batch_wait(pend.pop(0), copy=False)
+            while pend:
                 eng.match_batch_wait(pend.pop(0), copy=False)
-                waits.append(time.perf_counter() - t2)
-        while pend:
-            eng.match_batch_wait(pend.pop(0), copy=False)
-        pipe_s = (time.perf_counter() - t1) / k
-        reruns = eng.stats()["reruns"] - r0
+            s_ = (time.perf_counter() - t1) / k
+            by_inflight[inflight] = (s_, eng.stats()["reruns"] - r0)
+        inflight = min(by_inflight, key=lambda x: by_inflight[x][0])
+        pipe_s, reruns = by_inflight[inflight]
         e2e = {"value": round(w.nt / pipe_s, 1), "unit": "topics/s",
                "ms_per_batch": round(pipe_s * 1e3, 3), "batches_in_flight": inflight,
-               "wait_ms_median": round(float(np.median(waits)) * 1e3, 3) if waits else None,
+               "ms_per_batch_by_inflight": {str(i): round(v[0] * 1e3, 3) for i, v in by_inflight.items()},
                "reruns": int(reruns),
                "includes": "H2D topic bytes + offsets from pinned host memory, the device pass, "
                            "row pointers (u32) + filter ids + exact ids written into pinned host "
