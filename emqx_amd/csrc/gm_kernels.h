@@ -105,13 +105,16 @@ constexpr uint32_t REJ_BIT = 0x80000000u;
 constexpr uint32_t REJ_SCAN_MAX = 4096;  // rejects the deferred scatter handles in-line
 // Walk probe items per lane kept in LDS.  Passes start with the shallow stack (34 KB of LDS per
 // walk block: four blocks per CU leave room for the other pipe's tokenizer tile beside them);
-// an index whose walks outgrow it moves to the deep one (39 KB: four blocks still fit, the
-// tokenizer no longer does), then to the deep stack continued in global memory (spill).
-// Measured (profiles/r02/session2/ab_walk_stack.txt): cfg2 outgrows 6 items, and its walk on the
-// 8-deep stack takes 1.18 ms against 1.35 ms spilling; cfg3 never spills and loses ~1.5% of its
-// pipelined step with the deep stack.
+// an index whose walks outgrow it moves to the deep one (47 KB: three blocks per CU), then to the
+// deep stack continued in global memory (spill).  Measured on cfg2, whose walks outgrow 6 items
+// (profiles/r02/session2/ab_walk_stack.txt, ab_walk_stack_deep.txt): pipelined step 1.59 ms
+// spilling past 6, 1.38 ms past 8, 1.21 ms with 12 or 14 (3 blocks per CU), 1.45 ms with 16
+// (2 blocks per CU); cfg3 never leaves the shallow stack (an 8-deep one cost it ~1.5%).
 constexpr uint32_t WALK_STK_SHALLOW = 6;
-constexpr uint32_t WALK_STK_DEEP = 8;
+#ifndef GM_WALK_STK_DEEP  // A/B builds may override it
+#define GM_WALK_STK_DEEP 12
+#endif
+constexpr uint32_t WALK_STK_DEEP = GM_WALK_STK_DEEP;
 enum WalkLevel : uint32_t { WALK_SHALLOW = 0, WALK_DEEP = 1, WALK_SPILL = 2 };
 constexpr uint32_t WALK_SPILL_MIN = 32;  // initial spill items per lane (grown on overflow)
 // spill items per lane that no walk can exceed: a resolved probe pushes <= 4 items spanning

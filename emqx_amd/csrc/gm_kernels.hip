@@ -383,18 +383,23 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   a.leafp_mask = ix.leafp_mask;
   a.root_sig = ix.root_sig;
   constexpr uint32_t SH = WALK_STK_SHALLOW, DP = WALK_STK_DEEP;
+  // the deep-stack variants fit fewer blocks per CU (LDS): launch only as many as are resident
+  // at once, so that no block of the persistent grid starts after the others have drained
+  constexpr uint32_t LDS_CU = 160u * 1024u;
+  constexpr uint32_t DEEP_PER_CU = LDS_CU / walk_lds_bytes(DP);
+  const dim3 grid(level >= WALK_DEEP ? std::min<uint32_t>(g.blocks, g.cus * DEEP_PER_CU) : g.blocks);
   if (census) {
     if (level >= WALK_SPILL)
-      hipLaunchKernelGGL((k_walk<true, true, DP>), dim3(g.blocks), dim3(WG), 0, s, a);
+      hipLaunchKernelGGL((k_walk<true, true, DP>), grid, dim3(WG), 0, s, a);
     else if (level == WALK_DEEP)
-      hipLaunchKernelGGL((k_walk<true, false, DP>), dim3(g.blocks), dim3(WG), 0, s, a);
+      hipLaunchKernelGGL((k_walk<true, false, DP>), grid, dim3(WG), 0, s, a);
     else
       hipLaunchKernelGGL((k_walk<true, false, SH>), dim3(g.blocks), dim3(WG), 0, s, a);
   } else {
     if (level >= WALK_SPILL)
-      hipLaunchKernelGGL((k_walk<false, true, DP>), dim3(g.blocks), dim3(WG), 0, s, a);
+      hipLaunchKernelGGL((k_walk<false, true, DP>), grid, dim3(WG), 0, s, a);
     else if (level == WALK_DEEP)
-      hipLaunchKernelGGL((k_walk<false, false, DP>), dim3(g.blocks), dim3(WG), 0, s, a);
+      hipLaunchKernelGGL((k_walk<false, false, DP>), grid, dim3(WG), 0, s, a);
     else
       hipLaunchKernelGGL((k_walk<false, false, SH>), dim3(g.blocks), dim3(WG), 0, s, a);
   }
