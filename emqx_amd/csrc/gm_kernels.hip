@@ -20,7 +20,10 @@ namespace {
 
 constexpr uint32_t WG = 256;
 constexpr uint32_t CH = STAGE_CHUNK;  // staged-pair slots reserved per wave per atomic
-constexpr uint32_t TBLK = 128;    // topics claimed per wave per atomic
+#ifndef GM_TBLK  // A/B builds may override it
+#define GM_TBLK 128
+#endif
+constexpr uint32_t TBLK = GM_TBLK;  // topics claimed per wave per atomic
 constexpr uint32_t SCAN_ITEMS = 16;
 constexpr uint32_t SCAN_TILE = WG * SCAN_ITEMS;
 constexpr uint32_t TILE_BYTES = 16384;  // tokenizer LDS tile (256 topics)
