@@ -44,8 +44,8 @@ def log(*a):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--cfg", type=int, default=3)
     ap.add_argument("--filters", type=int, default=None)
     ap.add_argument("--topics", type=int, default=None, help="topics per GPU batch")
