@@ -11,5 +11,5 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout
 timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > $O/smoke.log 2>&1 || exit 1
 timeout -k 10 300 python -u bench.py > $O/cfg3.json 2> $O/cfg3.log || exit 1
 for c in ${CFGS:-1 2 4}; do
-  timeout -k 10 400 python -u bench.py --cfg $c --steps 10 > $O/cfg$c.json 2> $O/cfg$c.log || exit 1
+  timeout -k 10 400 python -u bench.py --cfg $c > $O/cfg$c.json 2> $O/cfg$c.log || exit 1
 done
