@@ -110,7 +110,10 @@ constexpr uint32_t REJ_SCAN_MAX = 4096;  // rejects the deferred scatter handles
 // (profiles/r02/session2/ab_walk_stack.txt, ab_walk_stack_deep.txt): pipelined step 1.59 ms
 // spilling past 6, 1.38 ms past 8, 1.21 ms with 12 or 14 (3 blocks per CU), 1.45 ms with 16
 // (2 blocks per CU); cfg3 never leaves the shallow stack (an 8-deep one cost it ~1.5%).
-constexpr uint32_t WALK_STK_SHALLOW = 6;
+#ifndef GM_WALK_STK_SHALLOW  // A/B builds may override it
+#define GM_WALK_STK_SHALLOW 6
+#endif
+constexpr uint32_t WALK_STK_SHALLOW = GM_WALK_STK_SHALLOW;
 #ifndef GM_WALK_STK_DEEP  // A/B builds may override it
 #define GM_WALK_STK_DEEP 12
 #endif
