@@ -3,7 +3,11 @@
 Workload (BASELINE.json configs[2]): 10M wildcard filters of the IoT tree
 ``site/+/device/+/#`` family, every GPU matching batches of ``site/{s}/device/{d}/{m}/{k}``
 topics.  One step = one full match pass over one batch already resident in HBM: tokenise +
-hash, exact route-key probe, trie walk, CSR build, byte verification of every pair.
+hash, route-key probe (when the index has plain route keys), trie walk, byte re-check of the
+pairs whose filters hold a hashed (> 7-byte) word (cfg3 has none: its words are all <= 7 bytes,
+whose level tokens are injective, so no pair needs one and k_verify does not launch), CSR build.
+Steps rotate over --batches distinct batches (different topic seeds, default 3), so no pass
+re-matches the batch the previous pass just warmed the caches with.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--cfg 3] [--shard topics|filters]
 
@@ -49,6 +53,9 @@ def main():
     ap.add_argument("--cfg", type=int, default=3)
     ap.add_argument("--filters", type=int, default=None)
     ap.add_argument("--topics", type=int, default=None, help="topics per GPU batch")
+    ap.add_argument("--batches", type=int, default=3,
+                    help="distinct topic batches (topic seeds) rotated through warm-up and the "
+                         "timed region")
     ap.add_argument("--shard", choices=["topics", "filters"], default="topics")
     ap.add_argument("--wg-per-cu", type=int, default=0)
     ap.add_argument("--no-filter-shard", action="store_true",
@@ -92,7 +99,11 @@ def main():
     t0 = time.time()
     seed_t = st + (1000 * rank if args.shard == "topics" else 0)
     w = workloads.generate(args.cfg, nf, nt, sf, seed_t)
-    log(f"[rank {rank}] generated {w.nf} filters, {w.nt} topics in {time.time() - t0:.1f}s")
+    # further batches: the same distribution under other topic seeds (no filters drawn again)
+    nb = max(1, args.batches)
+    extra = [workloads.generate(args.cfg, nf, nt, sf, seed_t + 7919 * b, topics_only=True)
+             for b in range(1, nb)]
+    log(f"[rank {rank}] generated {w.nf} filters, {nb} x {w.nt} topics in {time.time() - t0:.1f}s")
 
     # the CPU baseline's index (reference-style ordered set) builds in the background while the
     # GPU is measured; ctypes releases the GIL, so the two do not interleave on the host
@@ -110,19 +121,23 @@ def main():
 
     if args.topic_order != "as-is":
         w = _reorder_topics(w, args.topic_order)
-    tb = torch.from_numpy(w.tbytes).to(dev)
-    to = torch.from_numpy(w.toff.view(np.int32)).to(dev)
-    nbytes = int(w.toff[-1])
+        extra = [_reorder_topics(x, args.topic_order) for x in extra]
+    hosts = [w] + extra
+    dbat = [(torch.from_numpy(x.tbytes).to(dev), torch.from_numpy(x.toff.view(np.int32)).to(dev),
+             int(x.toff[-1])) for x in hosts]
+    tb, to, nbytes = dbat[0]
+    nbytes_mean = sum(b[2] for b in dbat) / nb
     torch.cuda.synchronize()
 
-    # ---- one diagnostic census pass (outside the timed region): S(t), slot loads, pairs ----
+    # ---- diagnostic census passes (outside the timed region): S(t), slot loads, pairs, as the
+    # mean over the batches ----
     # S(t) as SURVEY 8d defines it (every matched prefix state) comes from a census of the
     # unpruned walk; the production walk skips leaf-only children a deeper topic cannot match
     # (CF_LEAFP), so its own loads and iterations come from a second census
     eng.tune("leaf_prune", 0)
-    census_full = eng.walk_census(tb.data_ptr(), to.data_ptr(), w.nt, nbytes)
+    census_full = _census_mean(eng, dbat, w.nt)
     eng.tune("leaf_prune", 1)
-    census = eng.walk_census(tb.data_ptr(), to.data_ptr(), w.nt, nbytes)
+    census = _census_mean(eng, dbat, w.nt)
     census["states_visited"] = census["states"]
     census["states"] = census_full["states"]
 
@@ -132,12 +147,20 @@ def main():
     # last one inside the timed region.  Every batch is matched in full either way.
     pipelined = not args.no_pipeline
     pending = []
+    turn = [0]
+
+    def next_batch():
+        b = dbat[turn[0] % nb]
+        turn[0] += 1
+        return b
 
     def step_sync():
-        return eng.match_device(tb.data_ptr(), to.data_ptr(), w.nt, nbytes)
+        b_, o_, n_ = next_batch()
+        return eng.match_device(b_.data_ptr(), o_.data_ptr(), w.nt, n_)
 
     def step_pipe():
-        pending.append(eng.match_device_submit(tb.data_ptr(), to.data_ptr(), w.nt, nbytes))
+        b_, o_, n_ = next_batch()
+        pending.append(eng.match_device_submit(b_.data_ptr(), o_.data_ptr(), w.nt, n_))
         if len(pending) == eng.PIPES:
             eng.match_device_wait(pending.pop(0))
 
@@ -180,7 +203,7 @@ def main():
     # rank 0's batch broadcast, results gathered and merged on rank 0 every step)
     fsh = None
     if world > 1 and (args.shard == "filters" or not args.no_filter_shard):
-        fsh = _filter_sharded_run(Engine, D, args, w, tb, to, rank, world, dev, local)
+        fsh = _filter_sharded_run(Engine, D, args, w, dbat, rank, world, dev, local)
     # kernel timing with HIP events on the engine's stream, in extra passes after the timed
     # region (the events themselves add gaps between launches), one pass at a time so that a
     # launch's duration is its own (not stretched by the other pipe's overlapping work)
@@ -199,14 +222,14 @@ def main():
     walk_ms = (s1["walk_ms"] - s0["walk_ms"]) / max(1, walks)
     pipe_ms = (s1["total_ms"] - s0["total_ms"]) / max(1, launches)
     topics_total = w.nt * world
-    compulsory = int(w.toff[-1]) + 4 * w.nt + 8 * census["pairs"]
+    compulsory = nbytes_mean + 4 * w.nt + 8 * census["pairs"]
     value = topics_total / (elapsed / args.steps)
     if args.shard == "filters" and fsh is not None:
         # the north-star layout as the headline: one batch per step over all GPUs
         topics_total, elapsed = w.nt, fsh["ms_per_step"] * 1e-3 * args.steps
         value = fsh["value"]
-    pmc = _pmc(args.cfg, w.nt)
-    roofline = _roofline(w, census, pmc, tok_ms, exact_ms, walk_ms, pipe_ms,
+    pmc = _pmc(args.cfg, w.nt, nb)
+    roofline = _roofline(w.nt, nbytes_mean, census, pmc, tok_ms, exact_ms, walk_ms, pipe_ms,
                          exact_table_bytes=32 * int(est.get("exact_slots", 0)))
     roofline["compulsory_bytes_per_batch"] = int(compulsory)
     roofline["compulsory_frac"] = round(compulsory / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4)
@@ -217,13 +240,23 @@ def main():
         # host-resident batch in, host CSR out (PCIe both ways): reported beside `value`.  The
         # topics sit in pinned host memory, as a NIF batcher packs its window
         # (emqxgm_host_alloc); results are read in the handle's pinned buffers (no copy).
-        hb = eng.pinned(len(w.tbytes))
-        hb[:] = w.tbytes
-        ho = eng.pinned(w.nt + 1, np.uint32)
-        ho[:] = w.toff
-        eng.match_packed(hb, ho, copy=False)
+        hbat = []
+        for x in hosts:
+            hb = eng.pinned(len(x.tbytes))
+            hb[:] = x.tbytes
+            ho = eng.pinned(x.nt + 1, np.uint32)
+            ho[:] = x.toff
+            hbat.append((hb, ho))
+        hturn = [0]
+
+        def next_host():
+            b = hbat[hturn[0] % nb]
+            hturn[0] += 1
+            return b
+        eng.match_packed(*next_host(), copy=False)
         best = 1e9
         for _ in range(5):
+            hb, ho = next_host()
             t1 = time.perf_counter()
             eng.match_packed(hb, ho, copy=False)
             best = min(best, time.perf_counter() - t1)
@@ -234,7 +267,7 @@ def main():
         k = max(20, args.steps)
         pend = []
         for _ in range(2 * eng.HOST_PIPES):  # every pipe's scratch and buffers at their size
-            pend.append(eng.match_batch_submit(hb, ho))
+            pend.append(eng.match_batch_submit(*next_host()))
             if len(pend) == eng.HOST_PIPES:
                 eng.match_batch_wait(pend.pop(0), copy=False)
         while pend:
@@ -244,7 +277,7 @@ def main():
             r0 = eng.stats()["reruns"]
             t1 = time.perf_counter()
             for _ in range(k):
-                pend.append(eng.match_batch_submit(hb, ho))
+                pend.append(eng.match_batch_submit(*next_host()))
                 if len(pend) == inflight:
                     eng.match_batch_wait(pend.pop(0), copy=False)
             while pend:
@@ -283,6 +316,8 @@ def main():
                 "workload": f"cfg{args.cfg}: {w.nf} filters "
                             + ("(IoT site/+/device/+/# tree)" if args.cfg == 3 else ""),
                 "filters": int(w.nf), "topics_per_gpu_batch": int(w.nt),
+                "distinct_batches": nb,
+                "topic_seeds": [int(seed_t + 7919 * b) for b in range(nb)],
                 "global_batch": int(topics_total), "parallelism":
                     (f"topic-replica x{world}" if args.shard == "topics" or world == 1
                      else f"filter-shard x{world}"),
@@ -336,7 +371,26 @@ def _build_engine(Engine, w, idx, args, local):
     return eng, gid
 
 
-def _filter_sharded_run(Engine, D, args, w, tb, to, rank, world, dev, local):
+def _census_mean(eng, dbat, nt):
+    """walk_census over every batch, as the mean per batch."""
+    acc = None
+    for b_, o_, n_ in dbat:
+        c = eng.walk_census(b_.data_ptr(), o_.data_ptr(), nt, n_)
+        if acc is None:
+            acc = c
+            continue
+        for k, v in c.items():
+            if isinstance(v, dict):
+                for kk, vv in v.items():
+                    acc[k][kk] = [a + b for a, b in zip(acc[k][kk], vv)]
+            else:
+                acc[k] += v
+    k = len(dbat)
+    return {key: ({kk: [x / k for x in vv] for kk, vv in v.items()} if isinstance(v, dict) else v / k)
+            for key, v in acc.items()}
+
+
+def _filter_sharded_run(Engine, D, args, w, dbat, rank, world, dev, local):
     """The north-star layout on these ranks: this rank's filter shard in an engine of its own,
     rank 0's batch broadcast, matched on every shard, gathered and merged on rank 0 (dist.py
     ShardedMatcher).  Same steps / warmup as the replica measurement; max over ranks."""
@@ -345,16 +399,21 @@ def _filter_sharded_run(Engine, D, args, w, tb, to, rank, world, dev, local):
     seng, gid = _build_engine(Engine, w, mine, args, local)
     log(f"[rank {rank}] filter shard: {len(mine)} filters in {time.time() - t0:.1f}s")
     sm = D.ShardedMatcher(seng, torch.from_numpy(gid.view(np.int32)).to(dev), dev)
-    mb, mo = (tb, to) if rank == 0 else (None, None)
+    turn = [0]
+
+    def nxt():
+        b = dbat[turn[0] % len(dbat)]
+        turn[0] += 1
+        return (b[0], b[1]) if rank == 0 else (None, None)
     for _ in range(args.warmup):
-        sm.step(mb, mo)
+        sm.step(*nxt())
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     pairs = 0
     for _ in range(args.steps):
-        m = sm.step(mb, mo)
+        m = sm.step(*nxt())
         if m is not None:
             pairs = int(m.filter_id.numel())
     torch.cuda.synchronize()
@@ -433,54 +492,58 @@ def _random_lines_ceiling(table_bytes):
     return pts[-1][1]
 
 
-def _pmc(cfg, nt):
-    """Per-kernel PMC summary of this config from profiles/ (HBM bytes and L2 hits/misses per
-    launch, tools/pmc_traffic.py), if one was committed for this batch size."""
-    for name in (f"pmc_cfg{cfg}.json", f"pmc_walk_cfg{cfg}.json"):
+def _pmc(cfg, nt, nb):
+    """Per-kernel PMC summary of this config from profiles/ (HBM bytes, L2 hits/misses and
+    TCP->TCC read requests per launch, tools/pmc_traffic.py), if one was committed for this
+    batch size and number of distinct batches."""
+    for name in (f"pmc_cfg{cfg}.json",):
         p = os.path.join(ROOT, "profiles", name)
         try:
             with open(p) as f:
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        if int(d.get("topics", -1)) != nt:
+        if int(d.get("topics", -1)) != nt or int(d.get("batches", 1)) != nb:
             continue
-        if "kernels" in d:
-            return {k: dict(v, source=f"profiles/{name}") for k, v in d["kernels"].items()}
-        return {"k_walk": {"hbm_bytes_per_launch": d.get("hbm_bytes_per_launch"),
-                           "tcc_hit": d.get("tcc_hit"), "tcc_miss": d.get("tcc_miss"),
-                           "source": f"profiles/{name}"}}
+        return {k: dict(v, source=f"profiles/{name}") for k, v in d.get("kernels", {}).items()}
     return {}
 
 
-def _roofline(w, census, pmc, tok_ms, exact_ms, walk_ms, pipe_ms, exact_table_bytes=0):
+def _roofline(nt, nbytes, census, pmc, tok_ms, exact_ms, walk_ms, pipe_ms, exact_table_bytes=0):
     """Roofline of the step's dominant kernel (by HIP-event time, one pass at a time).
 
     k_walk and k_exact are dependent random gathers: the binding resource is the rate of random
-    64-B line accesses (RANDOM_LINES_PEAK), not HBM bandwidth.  `achieved` is the kernel's
-    random line accesses (k_walk: edge-bucket loads counted by the census pass; k_exact: one
-    bucket line per name) per second; beside it the SURVEY 8d algorithmic bytes and the PMC
-    counter bytes as fractions of the 8 TB/s HBM peak, and the PMC L2-miss lines per second
-    against RANDOM_LINES_PEAK.  k_tok streams: bound HBM."""
+    64-B line requests the memory system serves beyond the L1 (RANDOM_LINES_PEAK from beyond the
+    L2, RANDOM_LINES_L2 from it: tools/gather_bench.hip, whose every load misses the L1), not HBM
+    bandwidth.  `achieved` counts the requests that reach the L2: for k_walk the PMC
+    TCP_TCC_READ_REQ per launch of the committed HEAD profile (profiles/pmc_cfg<N>.json, same
+    batch size and batches), for k_exact one bucket line per name; the census edge-bucket loads
+    (L1 hits included) are `edge_loads_per_s`.  Beside it the SURVEY 8d algorithmic bytes and the
+    PMC counter bytes as fractions of the 8 TB/s HBM peak.  k_tok streams: bound HBM."""
     kernels = {"k_tok": tok_ms, "k_exact": exact_ms, "k_walk": walk_ms}
     dom = max(kernels, key=lambda k: kernels[k])
     post = max(0.0, pipe_ms - tok_ms - exact_ms - walk_ms)
     ms = kernels[dom]
     sec = ms * 1e-3 if ms > 0 else float("inf")
-    nt = w.nt
     p = pmc.get(dom, {})
     traffic = p.get("hbm_bytes_per_launch")
     out = {"kernel": dom}
     if dom == "k_tok":
         # topic bytes + offsets in; 64-B record, level count and exact id out per topic
-        alg = int(w.toff[-1]) + 4 * (nt + 1) + (64 + 4 + 4) * nt
+        alg = nbytes + 4 * (nt + 1) + (64 + 4 + 4) * nt
         ach = alg / sec / 1e9
         out.update({"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "algorithmic_bytes_per_launch": alg})
+                    "algorithmic_bytes_per_launch": int(alg)})
     else:
+        edge_loads = None
         if dom == "k_walk":
-            lines = census["slot_loads"]
+            edge_loads = census["slot_loads"]
+            req = p.get("tcp_tcc_read_req")
+            lines = req if req else edge_loads
+            src = ("PMC TCP_TCC_READ_REQ per launch (" + str(p.get("source")) + ")" if req else
+                   "census edge-bucket loads (no PMC request count committed for this batch: "
+                   "L1 hits included, an over-count)")
             # SURVEY 8d: per topic its 64-B record + 4-B count, 3 x 16-B edge probes per matched
             # trie state, a 16-B staged pair per match; the pruned walk never loads the states
             # the depth codes rule out (shown apart)
@@ -488,10 +551,11 @@ def _roofline(w, census, pmc, tok_ms, exact_ms, walk_ms, pipe_ms, exact_table_by
             pruned = 48 * (census["states"] - census.get("states_visited", census["states"]))
         else:
             lines = nt
-            alg = int(w.toff[-1]) + 8 * nt + 64 * nt + 4 * nt
+            src = "one route-key bucket line per name"
+            alg = nbytes + 8 * nt + 64 * nt + 4 * nt
             pruned = 0
         ach = lines / sec
-        # the ceiling of this access mix: a line that misses the L2 costs 1 / RANDOM_LINES_PEAK,
+        # the ceiling of this access mix: a request that misses the L2 costs 1 / RANDOM_LINES_PEAK,
         # one that hits 1 / RANDOM_LINES_L2 (the measured gather rates); the miss share comes
         # from the committed PMC run of this config (per-launch hit / miss counters).  The
         # route-key probe's bucket lines are all misses; over a table beyond the TLB's reach
@@ -507,7 +571,7 @@ def _roofline(w, census, pmc, tok_ms, exact_ms, walk_ms, pipe_ms, exact_table_by
             "bound": "random-access", "achieved": round(ach / 1e9, 2),
             "peak": round(peak / 1e9, 2), "unit": "G lines/s",
             "frac": round(ach / peak, 4), "traffic": traffic,
-            "random_lines_per_launch": int(lines),
+            "l2_requests_per_launch": int(lines), "achieved_source": src,
             "exact_table_bytes": int(exact_table_bytes) if dom == "k_exact" else None,
             "l2_miss_share": None if mr is None else round(mr, 4),
             "peak_source": ("measured dependent random 64-B gather rate over a table of the route-"
@@ -520,6 +584,9 @@ def _roofline(w, census, pmc, tok_ms, exact_ms, walk_ms, pipe_ms, exact_table_by
                                 "achieved_GBs": round(alg / sec / 1e9, 1),
                                 "frac": round(alg / sec / 1e9 / HBM_PEAK_GBS, 4)},
         })
+        if edge_loads is not None:
+            out["edge_loads_per_launch"] = int(edge_loads)
+            out["edge_loads_per_s"] = round(edge_loads / sec / 1e9, 2)
         if traffic:
             out["hbm_counter"] = {"bytes_per_launch": traffic,
                                   "achieved_GBs": round(traffic / sec / 1e9, 1),
@@ -535,6 +602,8 @@ def _roofline(w, census, pmc, tok_ms, exact_ms, walk_ms, pipe_ms, exact_table_by
                                # ceilings, over the kernel's time
                                "frac_mixed_ceiling": round(model / sec, 4),
                                "source": p.get("source")}
+        if p.get("duration_us") is not None:
+            out["rocprof_avg_us"] = p.get("duration_us")
     out["kernels_ms"] = {"k_tok": round(tok_ms, 4), "k_exact": round(exact_ms, 4),
                          "k_walk": round(walk_ms, 4), "verify+scan+scatter": round(post, 4),
                          "pass": round(pipe_ms, 4)}
@@ -587,38 +656,56 @@ class _CpuIndexJob:
         return self.ref, self.build_s
 
 
-def _cpu_baseline(w, args, job):
-    """The reference algorithm (C++ restatement of emqx_trie match_compact with an ordered-set
-    index, oracle/ref_trie.cpp) on this host's cores, over a bounded sample of the topics."""
-    # the GPU box gives each GPU a 16-CPU share (nproc / os.cpu_count() show the whole host)
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-    ref, build_s = job.wait()
+def _cpu_leg(ref, w, threads, seconds):
+    """Topics/s of the reference restatement on `threads` threads over a bounded sample."""
     n = min(w.nt, 20000)
     dt, _ = ref.time_match(w.tbytes, w.toff[: n + 1], threads)
     rate = n / max(dt, 1e-9)
-    n2 = int(min(w.nt, max(n, rate * args.cpu_seconds)))
+    n2 = int(min(w.nt, max(n, rate * seconds)))
     if n2 > n:
         dt, _ = ref.time_match(w.tbytes, w.toff[: n2 + 1], threads)
         n = n2
     reps = 1
-    if dt < args.cpu_seconds / 2:
+    if dt < seconds / 2:
         # the whole batch takes less than the bounded sample's time: match it again and again
-        reps = max(1, int(args.cpu_seconds / max(dt, 1e-3)))
+        reps = max(1, int(seconds / max(dt, 1e-3)))
         t0 = time.perf_counter()
         for _ in range(reps):
             ref.time_match(w.tbytes, w.toff[: n + 1], threads)
         dt = (time.perf_counter() - t0) / reps
+    return n / dt, n, reps, dt
+
+
+def _cpu_baseline(w, args, job):
+    """The reference algorithm (C++ restatement of emqx_trie match_compact with an ordered-set
+    index, oracle/ref_trie.cpp) on this host's cores, over a bounded sample of the topics.
+    T = the CPUs this process may run on (os.sched_getaffinity, SURVEY 8d's nproc: one thread
+    per BEAM scheduler), and beside it the 16-CPU share the GPU box gives each GPU."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    threads = args.cpu_threads or aff
+    share = min(16, aff)
+    ref, build_s = job.wait()
+    rate, n, reps, dt = _cpu_leg(ref, w, threads, args.cpu_seconds)
     log(f"cpu baseline: index build {build_s:.1f}s, {n} topics in {dt:.2f}s on {threads} threads")
+    share_leg = None
+    if share != threads:
+        r2, n2, reps2, dt2 = _cpu_leg(ref, w, share, args.cpu_seconds / 2)
+        share_leg = {"value": round(r2, 1), "cores": share,
+                     "sample": f"first {n2} topics" + (f" (x{reps2}, mean)" if reps2 > 1 else "")}
     model = "?"
     try:
         with open("/proc/cpuinfo") as f:
             model = next(ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name"))
     except (OSError, StopIteration):
         pass
-    return {"value": round(n / dt, 1), "unit": "topics/s", "cores": threads, "kind": "port",
-            "cpu_model": model, "host_cpus": os.cpu_count(),
+    return {"value": round(rate, 1), "unit": "topics/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "host_cpus": os.cpu_count(), "affinity_cpus": aff,
+            "gpu_share_16": share_leg,
             "index_build_s": round(build_s, 1),
-            "sample": f"first {n} topics of the same batch" + (f" (x{reps}, mean)" if reps > 1 else "")
+            "sample": f"first {n} topics of batch 0" + (f" (x{reps}, mean)" if reps > 1 else "")
                   + f" against the same {w.nf} filters "
                       f"(emqx_trie match_compact restated in C++, std::map ordered set), "
                       f"{dt * reps:.1f}s wall" + job.note}

@@ -2314,6 +2314,82 @@ void snap_model(IO& io, M& m) {
   io.pod(m.n_route_w);
 }
 
+// Internal consistency of a loaded model against the registry it came with: every index
+// upload_model and the delta-commit code take from the file stays inside its array.  A
+// snapshot that fails this is rejected with -EINVAL instead of writing past host buffers.
+bool pow2(uint64_t x) { return x && !(x & (x - 1)); }
+
+bool model_consistent(const TrieModel& m, uint64_t n_filters, std::string& why) {
+  const uint64_t n = m.parent.size();
+  auto bad = [&](const char* w) {
+    why = w;
+    return false;
+  };
+  if (n == 0 || n > MAX_NODES) return bad("node count");
+  for (const auto* v : {&m.ref, &m.nlit, &m.pchild, &m.hf, &m.tw, &m.tn})
+    if (v->size() != n) return bad("per-node array size");
+  if (m.sig.size() != n || m.hcode.size() != n || m.tok.size() != n || m.slot.size() != n)
+    return bad("per-node array size");
+  if (!pow2(m.nbk) || m.ecap != m.nbk * EBUCKET || m.ecap > (1ull << 40)) return bad("edge capacity");
+  if (m.occ.size() < m.ecap / 64 + 1 || m.tomb.size() < m.ecap / 64 + 1) return bad("edge bitmaps");
+  if (m.tn_cap < n || m.tn_cap > (1ull << 32)) return bad("side array capacity");
+  if (m.fvbits.size() < (n_filters + 31) / 32 || m.fv_cap != m.fvbits.size()) return bad("verify bits");
+  if (!pow2(m.emap.ents.size()) || m.emap.mask + 1 != m.emap.ents.size() ||
+      m.emap.used > m.emap.ents.size())
+    return bad("edge map");
+  for (const auto& e : m.emap.ents)
+    if (e.parent != NONE && e.parent != TOMB && (e.parent >= n || e.child >= n)) return bad("edge map entry");
+  auto fid_ok = [&](uint32_t v) {
+    if (v == NONE) return true;
+    if (!(v & LIST_MULTI)) return v < n_filters;
+    const uint64_t i = v & ~LIST_MULTI;
+    if (i >= m.multi.size() || m.multi[i] + i + 1 > m.multi.size()) return false;
+    for (uint64_t k = 0; k < m.multi[i]; ++k)
+      if (m.multi[i + 1 + k] >= n_filters) return false;
+    return true;
+  };
+  if (m.slot[0] != DEAD) return bad("root slot");
+  for (uint64_t c = 0; c < n; ++c) {
+    if (c && m.slot[c] != DEAD && m.slot[c] >= m.ecap) return bad("slot position");
+    if (c && m.parent[c] != NONE && m.parent[c] >= c) return bad("parent id");
+    if (m.pchild[c] >= n) return bad("'+' child id");
+    if (!fid_ok(m.hf[c]) || !fid_ok(m.tw[c]) || !fid_ok(m.tn[c])) return bad("node filter id");
+  }
+  if (!pow2(m.xcap_p) || !pow2(m.xcap_w) || m.xcap_p + m.xcap_w > (1ull << 36)) return bad("key capacity");
+  const uint64_t xent_n = (m.xcap_p + m.xcap_w) * XBUCKET;
+  if (m.xocc.size() < xent_n / 64 + 1 || m.xtomb.size() < xent_n / 64 + 1 ||
+      m.xovf.size() < (m.xcap_p + m.xcap_w) / 64 + 1)
+    return bad("key bitmaps");
+  if (m.xpos.size() > n_filters) return bad("key positions");
+  for (uint32_t v : m.xpos)
+    if (v != NONE && v >= xent_n) return bad("key position");
+  if (m.max_depth > 65536) return bad("depth");
+  return true;
+}
+
+// A handle whose snapshot load failed half-way returns to the fresh state (empty registry,
+// no model): the next commit is a full build and another load may be tried.
+void reset_loaded(emqxgm* h) {
+  {
+    std::unique_lock<std::shared_mutex> pg(h->pmu);
+    h->pool.clear();
+    h->filters.clear();
+    h->slots.clear();
+    h->slot_mask = 0;
+  }
+  h->n_trie_pending = 0;
+  h->n_route_pending = 0;
+  h->local_node = NONE;
+  h->rdest.clear();
+  h->lsubs.clear();
+  h->foff_host.clear();
+  h->fver_host.clear();
+  h->tm = TrieModel();
+  h->changed.clear();
+  h->fan_changed.clear();
+  h->dirty = false;
+}
+
 template <class Map, class IO>
 void snap_map_out(IO& io, const Map& mp) {
   io.template pod<uint64_t>(mp.size());
@@ -2411,11 +2487,14 @@ int emqxgm_snapshot_load(emqxgm_t* h, const char* path) {
   snap_model(in, m);
   in.pod(magic2);
   fclose(f);
-  bool sane = in.ok && magic2 == SNAP_MAGIC && !m.parent.empty() && m.slot.size() == m.parent.size();
+  bool sane = in.ok && magic2 == SNAP_MAGIC && filters.size() < NONE;
   for (size_t i = 0; sane && i < filters.size(); ++i)
-    sane = filters[i].off + filters[i].len <= pool.size();
-  if (!sane) {
-    set_err(h, "snapshot truncated or corrupt");
+    sane = filters[i].len <= pool.size() && filters[i].off <= pool.size() - filters[i].len;
+  for (const auto& kv : rdest) sane = sane && kv.first < filters.size();
+  for (const auto& kv : lsubs) sane = sane && kv.first < filters.size();
+  std::string why = "truncated";
+  if (!sane || !model_consistent(m, filters.size(), why)) {
+    set_err(h, "snapshot corrupt: " + why);
     return -EINVAL;
   }
   {
@@ -2431,18 +2510,26 @@ int emqxgm_snapshot_load(emqxgm_t* h, const char* path) {
   h->local_node = local;
   h->rdest.swap(rdest);
   h->lsubs.swap(lsubs);
-  if (hipSetDevice(h->cfg.device) != hipSuccess) return fail(h, hipErrorInvalidDevice, "hipSetDevice");
+  if (hipSetDevice(h->cfg.device) != hipSuccess) {
+    reset_loaded(h);
+    return fail(h, hipErrorInvalidDevice, "hipSetDevice");
+  }
   int rc = 0;
   h->foff_host.clear();
   h->fver_host.clear();
   if ((rc = patch_wait(h)) || (rc = upload_pool(h, nullptr)) || (rc = fan_full(h)) ||
-      (rc = upload_model(h, m)))
+      (rc = upload_model(h, m))) {
+    reset_loaded(h);
     return rc;
+  }
   m.valid = true;
   h->tm = std::move(m);
   h->changed.clear();
   h->fan_changed.clear();
-  if ((rc = publish_epoch(h, false))) return rc;
+  if ((rc = publish_epoch(h, false))) {
+    reset_loaded(h);
+    return rc;
+  }
   h->dirty = false;
   commit_stats(h, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
                false);
@@ -2595,6 +2682,9 @@ int emqxgm_match_batch_submit(emqxgm_t* h, const uint8_t* bytes, const uint32_t*
                               uint32_t n, uint64_t* ticket) {
   if (!h || !ticket || !offsets || offsets[0] != 0 || (!bytes && offsets[n])) return -EINVAL;
   if (n > h->cfg.batch_max) return -E2BIG;
+  // a decreasing offset would make k_tok / k_exact read a topic of ~4 G bytes past the batch
+  for (uint32_t i = 0; i < n; ++i)
+    if (offsets[i + 1] < offsets[i]) return -EINVAL;
   std::lock_guard<std::mutex> g(h->mmu);
   if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
   const uint64_t tk = h->next_hticket;

@@ -206,7 +206,8 @@ int emqxgm_match_device_wait(emqxgm_t* h, uint64_t ticket, emqxgm_dev_out* out);
  * batch into HBM, the whole device pass and the copy of its result into pinned host memory, and
  * returns at once; _wait(ticket) completes it.  With several tickets in flight one batch's
  * upload, another's pass and a third's download overlap.  The batch: n <= cfg.batch_max topics,
- * topic i = bytes[offsets[i] .. offsets[i+1]), offsets[0] == 0 (-EINVAL otherwise); bytes and
+ * topic i = bytes[offsets[i] .. offsets[i+1]), offsets[0] == 0 and non-decreasing (-EINVAL
+ * otherwise, checked on the host before anything is enqueued); bytes and
  * offsets stay untouched until the wait (pinned memory from emqxgm_host_alloc gives full-speed
  * copies).  The result (batch-local u32 row pointers, trie filter ids, exact ids) lives in
  * pinned buffers of the pipe and stays valid until ticket + EMQXGM_HOST_PIPES is submitted;

@@ -272,6 +272,48 @@ int main(int argc, char** argv) {
       CHECK(emqxgm_trie_insert(other, (const uint8_t*)"a", 1, nullptr) == 0, "ins");
       CHECK(emqxgm_snapshot_load(other, snap.c_str()) == -EBUSY, "load into a used handle");
       emqxgm_destroy(other);
+      // corrupt copies (flipped bytes, random words, truncations): every load returns an error
+      // code or succeeds, never writes out of bounds (ASan), and a failed load leaves the handle
+      // fresh: the intact snapshot loads into it afterwards
+      {
+        FILE* f = fopen(snap.c_str(), "rb");
+        CHECK(f != nullptr, "open snap");
+        std::string img;
+        char buf[1 << 16];
+        size_t k;
+        while ((k = fread(buf, 1, sizeof buf, f)) > 0) img.append(buf, k);
+        fclose(f);
+        const std::string bad = snap + ".bad";
+        int rejected = 0;
+        for (int trial = 0; trial < 48; ++trial) {
+          std::string c = img;
+          const int kind = trial % 3;
+          if (kind == 0) {
+            for (int q = 0; q < 4; ++q) c[rnd(c.size())] ^= (char)(1 + rnd(255));
+          } else if (kind == 1) {
+            const size_t at = rnd(c.size() - 8);
+            const uint64_t v = rng() >> rnd(60);
+            memcpy(&c[at], &v, 8);
+          } else {
+            c.resize(rnd(c.size()));
+          }
+          FILE* g = fopen(bad.c_str(), "wb");
+          CHECK(g && fwrite(c.data(), 1, c.size(), g) == c.size(), "write bad snap");
+          fclose(g);
+          emqxgm_t* t = nullptr;
+          CHECK(emqxgm_create(&cfg, &t) == 0, "create");
+          const int rc = emqxgm_snapshot_load(t, bad.c_str());
+          CHECK(rc == 0 || rc < 0, "load rc");
+          if (rc < 0) {
+            ++rejected;
+            CHECK(emqxgm_snapshot_load(t, snap.c_str()) == 0, "reload after a failed load: %s",
+                  t->err.c_str());
+          }
+          emqxgm_destroy(t);
+        }
+        CHECK(rejected > 0, "no corrupt snapshot was rejected");
+        remove(bad.c_str());
+      }
       remove(snap.c_str());
     }
     const int mode = (int)rnd(10);
@@ -393,6 +435,15 @@ int main(int argc, char** argv) {
       }
     }
     ref_free(ids);
+  }
+  // emqxgm_match_batch_submit rejects malformed offsets on the host, before anything is enqueued
+  {
+    const uint8_t tb[8] = {'a', '/', 'b', 'c', 'd', 'e', 'f', 'g'};
+    uint64_t tk = 0;
+    const uint32_t dec[4] = {0, 5, 3, 8};
+    CHECK(emqxgm_match_batch_submit(hd, tb, dec, 3, &tk) == -EINVAL, "decreasing offsets");
+    const uint32_t nz[3] = {1, 3, 8};
+    CHECK(emqxgm_match_batch_submit(hd, tb, nz, 2, &tk) == -EINVAL, "offsets[0] != 0");
   }
   emqxgm_stats sd{}, sf{};
   emqxgm_get_stats(hd, &sd);

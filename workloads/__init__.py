@@ -48,7 +48,9 @@ class Workload:
 
 
 def generate(cfg: int, n_filters: int = None, n_topics: int = None, seed_f: int = None,
-             seed_t: int = None) -> Workload:
+             seed_t: int = None, topics_only: bool = False) -> Workload:
+    """The cfg's filters and a topic batch; topics_only=True draws the same topics without the
+    filters (empty filter arrays), for further batches against an index already built."""
     d = DEFAULTS[cfg]
     nf = d[0] if n_filters is None else n_filters
     nt = d[1] if n_topics is None else n_topics
@@ -58,9 +60,11 @@ def generate(cfg: int, n_filters: int = None, n_topics: int = None, seed_f: int 
     lib.wl_generate.restype = C.c_int
     lib.wl_generate.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
                                 C.POINTER(_Set)]
+    lib.wl_generate_topics.restype = C.c_int
+    lib.wl_generate_topics.argtypes = lib.wl_generate.argtypes
     lib.wl_free.argtypes = [C.POINTER(_Set)]
     s = _Set()
-    rc = lib.wl_generate(cfg, nf, nt, sf, st, C.byref(s))
+    rc = (lib.wl_generate_topics if topics_only else lib.wl_generate)(cfg, nf, nt, sf, st, C.byref(s))
     if rc != 0:
         raise RuntimeError(f"wl_generate({cfg}) failed: {rc}")
     try:

@@ -18,6 +18,8 @@
 
 namespace {
 
+bool g_topics_only = false;  // wl_generate_topics: skip the filter draws
+
 struct Rng {
   uint64_t s[4];
   explicit Rng(uint64_t seed) {
@@ -103,7 +105,7 @@ void gen_cfg1(uint64_t nf, uint64_t nt, uint64_t sf, uint64_t st, Packed& F, Pac
   Zipf zx(64, 1.1);
   Rng rf(sf);
   std::unordered_set<std::string> seen;
-  while (F.size() < nf) {
+  while (!g_topics_only && F.size() < nf) {
     std::string s;
     for (int k = 0; k < 4; ++k) {
       if (k) s += '/';
@@ -142,7 +144,7 @@ void gen_cfg2(uint64_t nf, uint64_t nt, uint64_t sf, uint64_t st, Packed& F, Pac
   Rng rf(sf);
   std::unordered_set<std::string> seen;
   seen.reserve(nf * 2);
-  while (F.size() < nf) {
+  while (!g_topics_only && F.size() < nf) {
     std::string s;
     for (int k = 0; k < 6; ++k) {
       if (k) s += '/';
@@ -183,7 +185,7 @@ void gen_cfg3(uint64_t nf, uint64_t nt, uint64_t sf, uint64_t st, Packed& F, Pac
   Rng rf(sf);
   std::unordered_set<std::string> seen;
   seen.reserve(nf * 2);
-  while (F.size() < nf) {
+  while (!g_topics_only && F.size() < nf) {
     const uint64_t s = zs.draw(rf);
     const uint64_t d = s * DEV + rf.below(DEV);
     const double u = rf.uni();
@@ -222,10 +224,10 @@ std::string id9(uint64_t id) {
 // fleet/+/dev/{id:09}/#, fleet/{f}/#; 1/3 each); topics 90% exact hits, 10% misses.
 void gen_cfg4(uint64_t nf, uint64_t nt, uint64_t sf, uint64_t st, Packed& F, Packed& T) {
   const uint64_t n_wild = nf / 101, n_exact = nf - n_wild;
-  for (uint64_t i = 0; i < n_exact; ++i) F.add("dev/" + id9(i) + "/state", false);
+  for (uint64_t i = 0; !g_topics_only && i < n_exact; ++i) F.add("dev/" + id9(i) + "/state", false);
   Rng rf(sf);
   std::unordered_set<std::string> seen;
-  while (F.size() < nf) {
+  while (!g_topics_only && F.size() < nf) {
     const double u = rf.uni();
     std::string f;
     if (u < 1.0 / 3)
@@ -288,6 +290,16 @@ int wl_generate(int cfg, uint64_t nf, uint64_t nt, uint64_t seed_f, uint64_t see
   memcpy(out->tbytes, T.bytes.data(), T.bytes.size());
   for (size_t i = 0; i < T.off.size(); ++i) out->toff[i] = (uint32_t)T.off[i];
   return 0;
+}
+
+// the topics of wl_generate(cfg, nf, nt, seed_f, seed_t) without the filters (bench.py draws
+// several distinct batches against one index)
+int wl_generate_topics(int cfg, uint64_t nf, uint64_t nt, uint64_t seed_f, uint64_t seed_t,
+                       wl_set* out) {
+  g_topics_only = true;
+  const int rc = wl_generate(cfg, nf, nt, seed_f, seed_t, out);
+  g_topics_only = false;
+  return rc;
 }
 
 void wl_free(wl_set* s) {
