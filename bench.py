@@ -58,6 +58,8 @@ def main():
                          "timed region")
     ap.add_argument("--shard", choices=["topics", "filters"], default="topics")
     ap.add_argument("--wg-per-cu", type=int, default=0)
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="emqxgm_tune before the index is built (A/B runs), e.g. fat_buckets=0")
     ap.add_argument("--no-filter-shard", action="store_true",
                     help="N>1: skip the filter-sharded measurement beside the replicas")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -332,6 +334,7 @@ def main():
                 "edge_loads_by_level": {k: [int(x) for x in v[:max(1, _last_nz(v) + 1)]]
                                         for k, v in census["loads_by_level"].items()},
                 "pipeline_ms_per_batch": round(pipe_ms, 4),
+                "tune": args.tune,
                 "passes_in_flight": eng.PIPES if pipelined else 1,
                 "one_pass_at_a_time": (None if sync_ms is None else {
                     "value": round(topics_total / (sync_ms * 1e-3), 1), "ms_per_step": round(sync_ms, 4)}),
@@ -352,6 +355,9 @@ def _build_engine(Engine, w, idx, args, local):
     wildcard ones in the trie (emqx_router_utils.erl:34-39).  Returns (engine, gid_map): the
     global filter index of each engine-local id, from the ids the engine returned."""
     eng = Engine(device=local, walk_wg_per_cu=args.wg_per_cu)
+    for kv in args.tune:
+        k, v = kv.split("=", 1)
+        eng.tune(k, int(v))
     fb, fo = _subset(w, idx)
     wild = w.fwild[idx].astype(bool)
     gid = np.full(max(1, len(idx)), 0xFFFFFFFF, np.uint32)

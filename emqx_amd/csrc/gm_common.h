@@ -97,7 +97,19 @@ constexpr uint32_t EBUCKET = 2;
 constexpr uint32_t EDGE_SLACK = 4;  // slots >= 4 x edges (load <= 1/4): fewer bucket overflows
 constexpr uint32_t CF_ID_BITS = 26;
 constexpr uint32_t CF_ID_MASK = (1u << CF_ID_BITS) - 1;
-constexpr uint32_t MAX_NODES = CF_ID_MASK - 1;  // ids stay below TOMB's and NONE's low 26 bits
+constexpr uint32_t MAX_NODES = CF_ID_MASK - 2;  // ids stay below FAT_ID and TOMB's / NONE's low 26 bits
+// Fat buckets (path compression of single-literal-child nodes).  A node C at depth 2, 4 or 6,
+// reached by a literal edge, whose only literal child is G, takes a whole bucket: C's slot in
+// the bucket's first half and G's slot in its second half, whose parent word is FAT_ID | G's
+// signature (FAT_ID is never a node id, so no key probe matches the half).  G has no slot at
+// its own hash position: a walk that resolves C finds G in the line it already loaded and, when
+// the topic's word equals G's token, creates G's state in the same round trip; otherwise C has
+// no matching literal child.  The root's only literal child, when it has one, is carried in
+// the kernel arguments the same way.  A delta commit that gives a fat node a second literal
+// child moves the half to its own hash position (the half's slot becomes TOMB), so a bucket
+// holds a half exactly when its first node's literal children are that half alone.
+constexpr uint32_t FAT_ID = CF_ID_MASK - 2;  // = MAX_NODES: no id; TOMB and NONE have low bits ..FE, ..FF
+constexpr uint32_t FAT_MAX_DEPTH = 6;  // C's word (level depth(C)) is a record token (< REC_TOKS)
 // Child signature: the top 6 bits of a slot's parent word (parent ids use 26) hold a 1-bit-per-
 // class summary of the child's literal children's level tokens (class = sig_bit(token)); the
 // walk does not probe a literal child whose token's class bit is clear.  Bits are only ever

@@ -207,6 +207,7 @@ struct PassCtx {
 };
 
 constexpr uint64_t DEAD = ~0ull;  // TrieModel::slot of the root and of removed nodes
+constexpr uint64_t ROOTH = ~1ull; // TrieModel::slot of the root's fat half (kernel arguments)
 
 // Device writes staged by one commit (k_patch): dword runs to device addresses, uploaded in
 // one copy and applied by one launch on the engine stream.
@@ -243,7 +244,13 @@ struct TrieModel {
   std::vector<uint8_t> hcode;  // depth code (gm_common.h CF_H0/CF_H1): exact at a full build,
                                // only reset to 0 (unbounded) by delta commits
   std::vector<uint64_t> tok;
-  std::vector<uint64_t> slot;       // edge slot of the node's incoming edge (DEAD: root/removed)
+  std::vector<uint64_t> slot;       // edge slot of the node's incoming edge (DEAD: root/removed,
+                                    // ROOTH: the root's fat half, carried in the arguments)
+  // fat buckets (gm_common.h FAT_ID): fchild = the node's only literal child when that child's
+  // slot is the second half of the node's bucket (the root's: the arguments), else 0; half = the
+  // node is such a child
+  std::vector<uint32_t> fchild;
+  std::vector<uint8_t> half;
   std::vector<uint64_t> occ, tomb;  // bitmaps over edge slots: used (live or TOMB), TOMB
   uint64_t nbk = 0, ecap = 0, n_occ = 0, n_edges = 0, tn_cap = 0, fv_cap = 0;
   std::vector<uint32_t> fvbits;
@@ -282,7 +289,7 @@ struct TrieModel {
   void node_slot(uint32_t c, uint4* sl) const {  // the 2 x uint4 of c's incoming edge
     const uint32_t p = pchild[c];
     sl[0] = make_uint4((uint32_t)tok[c], (uint32_t)(tok[c] >> 32),
-                       parent[c] | ((uint32_t)sig[c] << SIG_SHIFT), cf(c));
+                       (half[c] ? FAT_ID : parent[c]) | ((uint32_t)sig[c] << SIG_SHIFT), cf(c));
     sl[1] = make_uint4(hfd(c), tw[c], p ? pcf(p) : 0u, p ? phf(p) : NONE);
   }
   // the carried copy of '+' child p (gm_common.h CF_PTW): its '#' filter, or -- when it has
@@ -303,7 +310,16 @@ struct TrieModel {
     hcode.push_back(0);
     sig.push_back(0);
     slot.push_back(DEAD);
+    fchild.push_back(0);
+    half.push_back(0);
     return c;
+  }
+  // the root's fat half as the walk's arguments carry it (rh0.z = NONE: none)
+  void root_half(DevIndex& x) const {
+    uint4 sl[2] = {make_uint4(0u, 0u, NONE, 0u), make_uint4(0u, 0u, 0u, 0u)};
+    if (fchild[0]) node_slot(fchild[0], sl);
+    x.rh0 = sl[0];
+    x.rh1 = sl[1];
   }
   // a filter was added along path[0] = root .. path[m] (its end node; hash_last: a '#' filter
   // hanging off path[m]): a code its ancestors can no longer guarantee is reset to unbounded
@@ -471,6 +487,7 @@ struct emqxgm {
   uint64_t h_stage_bytes = 0;
   hipEvent_t patch_ev = nullptr;    // the last patch upload + launch
   uint32_t delta_mode = 1;        // 0: always rebuild, 1: delta when small, 2: delta if possible
+  uint32_t fat_mode = 1;          // 1: fat buckets at full builds (gm_common.h FAT_ID), 0: none
 };
 
 namespace {
@@ -840,7 +857,7 @@ int upload_model(emqxgm* h, TrieModel& m) {
   for (uint64_t i = 0; i < m.ecap; ++i)
     eslots[SLOT_U4 * i] = make_uint4(0u, 0u, bit(m.tomb, i) ? TOMB : NONE, 0u);
   for (uint32_t c = 1; c < n_nodes; ++c)
-    if (m.slot[c] != DEAD) m.node_slot(c, &eslots[SLOT_U4 * m.slot[c]]);
+    if (m.slot[c] != DEAD && m.slot[c] != ROOTH) m.node_slot(c, &eslots[SLOT_U4 * m.slot[c]]);
   std::vector<uint32_t> tn_of(m.tn_cap, NONE);
   for (size_t i = 0; i < n_nodes; ++i) tn_of[i] = m.tn[i];
   const uint64_t fmask =
@@ -881,6 +898,7 @@ int upload_model(emqxgm* h, TrieModel& m) {
   nx.root_hf = m.hfd(0);
   nx.root_pcf = root_p ? m.pcf(root_p) : 0u;
   nx.root_phf = root_p ? m.phf(root_p) : NONE;
+  m.root_half(nx);
   nx.test_mask = h->test_mask;
   nx.needs_verify = m.needs_verify;
   nx.full_mask = fmask;
@@ -989,11 +1007,53 @@ int commit_full(emqxgm* h) {
   m.nbk = m.ecap / EBUCKET;
   m.occ.assign(m.ecap / 64 + 1, 0ull);
   m.tomb.assign(m.ecap / 64 + 1, 0ull);
+  // fat buckets (gm_common.h FAT_ID): a node at depth 2, 4 or 6 reached by a literal edge whose
+  // only literal child is G takes a bucket of its own with G in the second half (halves are at
+  // odd depths, so a half is never fat itself); the root's only literal child rides in the
+  // kernel arguments.  Fat nodes are placed first, into the first bucket of their chain with
+  // both slots free; a bucket they pass that still has a free slot gets it TOMBed (a lookup
+  // must not stop there; later inserts may reuse it).
+  m.fchild.assign(n_nodes, 0u);
+  m.half.assign(n_nodes, 0u);
+  if (h->fat_mode) {
+    std::vector<uint8_t> depth(n_nodes, 0);
+    std::vector<uint32_t> lit(n_nodes, 0);
+    for (uint32_t c = 1; c < n_nodes; ++c) {
+      depth[c] = (uint8_t)std::min<uint32_t>(depth[m.parent[c]] + 1u, 255u);
+      if (m.tok[c] != PLUS_TOK) lit[m.parent[c]] = c;
+    }
+    for (uint32_t x = 0; x < n_nodes; ++x)
+      if (m.nlit[x] == 1 && (x == 0 || (depth[x] % 2 == 0 && depth[x] <= FAT_MAX_DEPTH &&
+                                        m.tok[x] != PLUS_TOK))) {
+        m.fchild[x] = lit[x];
+        m.half[lit[x]] = 1;
+      }
+  }
   for (uint32_t c = 1; c < n_nodes; ++c) {
+    if (!m.fchild[c]) continue;
+    uint64_t b = edge_slot(m.parent[c], m.tok[c], m.nbk - 1);
+    for (;;) {
+      const uint64_t q = b * EBUCKET;
+      if (!bit(m.occ, q) && !bit(m.occ, q + 1)) break;
+      for (uint32_t j = 0; j < EBUCKET; ++j)
+        if (!bit(m.occ, q + j)) {
+          bset(m.occ, q + j);
+          bset(m.tomb, q + j);
+        }
+      b = (b + 1) & (m.nbk - 1);
+    }
+    bset(m.occ, b * EBUCKET);
+    bset(m.occ, b * EBUCKET + 1);
+    m.slot[c] = b * EBUCKET;
+    m.slot[m.fchild[c]] = b * EBUCKET + 1;
+  }
+  if (m.fchild[0]) m.slot[m.fchild[0]] = ROOTH;
+  for (uint32_t c = 1; c < n_nodes; ++c) {
+    if (m.fchild[c] || m.half[c]) continue;
     uint64_t b = edge_slot(m.parent[c], m.tok[c], m.nbk - 1), i;
     for (;;) {
       uint32_t j = 0;
-      while (j < EBUCKET && bit(m.occ, b * EBUCKET + j)) ++j;
+      while (j < EBUCKET && bit(m.occ, b * EBUCKET + j) && !bit(m.tomb, b * EBUCKET + j)) ++j;
       if (j < EBUCKET) {
         i = b * EBUCKET + j;
         break;
@@ -1001,9 +1061,11 @@ int commit_full(emqxgm* h) {
       b = (b + 1) & (m.nbk - 1);
     }
     bset(m.occ, i);
+    bclr(m.tomb, i);
     m.slot[c] = i;
   }
-  m.n_occ = m.n_edges;
+  m.n_occ = 0;
+  for (uint64_t w : m.occ) m.n_occ += (uint64_t)__builtin_popcountll(w);
   // node side array with headroom for delta-commit growth
   m.tn_cap = n_nodes + std::max<uint64_t>(4096, n_nodes / 4);
   m.fv_cap = m.fvbits.size() + std::max<uint64_t>(1024, m.fvbits.size() / 4);
@@ -1120,8 +1182,14 @@ int commit_delta(emqxgm* h) {
         m.pchild[par] = 0;
       else
         m.nlit[par] -= 1;
-      bset(m.tomb, m.slot[n]);
-      epatch[m.slot[n]] = NONE;
+      if (m.half[n]) {  // its slot is the parent's second half (or the root's arguments)
+        m.fchild[par] = 0;
+        m.half[n] = 0;
+      }
+      if (m.slot[n] != ROOTH) {
+        bset(m.tomb, m.slot[n]);
+        epatch[m.slot[n]] = NONE;
+      }
       m.slot[n] = DEAD;
       m.n_edges -= 1;
       dirty.push_back(par);
@@ -1130,6 +1198,24 @@ int commit_delta(emqxgm* h) {
   }
 
   // ---- trie inserts: new nodes take the first free or TOMB slot of their bucket chain ----
+  auto alloc_slot = [&](uint32_t par, uint64_t tok) {
+    uint64_t b = edge_slot(par, tok, m.nbk - 1), i = DEAD;
+    while (i == DEAD) {
+      for (uint32_t j = 0; j < EBUCKET && i == DEAD; ++j) {
+        const uint64_t q = b * EBUCKET + j;
+        if (!bit(m.occ, q)) {
+          bset(m.occ, q);
+          m.n_occ += 1;
+          i = q;
+        } else if (bit(m.tomb, q)) {
+          bclr(m.tomb, q);
+          i = q;
+        }
+      }
+      b = (b + 1) & (m.nbk - 1);
+    }
+    return i;
+  };
   for (uint32_t id : tadd) {
     const Filter& f = h->filters[id];
     bool hashed;
@@ -1151,23 +1237,24 @@ int commit_delta(emqxgm* h) {
       if (ins) {
         if (m.parent.size() >= std::min<uint64_t>(MAX_NODES, m.tn_cap)) return 1;
         if ((m.n_occ + 1) * 2 > m.ecap) return 1;  // load bound of a delta-patched table
+        const uint32_t fc = m.fchild[cur];
+        if (fc && !is_plus[w]) {
+          // a second literal child: the fat half moves to its own hash position (its old slot
+          // becomes TOMB), so cur's literal children are probed by hash from now on
+          if ((m.n_occ + 2) * 2 > m.ecap) return 1;
+          if (m.slot[fc] != ROOTH) {
+            bset(m.tomb, m.slot[fc]);
+            epatch[m.slot[fc]] = NONE;
+          }
+          m.half[fc] = 0;
+          m.fchild[cur] = 0;
+          m.slot[fc] = alloc_slot(cur, m.tok[fc]);
+          epatch[m.slot[fc]] = fc;
+          dirty.push_back(fc);
+        }
         const uint32_t c = m.new_node(cur, tok);
         *v = c;
-        uint64_t b = edge_slot(cur, tok, m.nbk - 1), i = DEAD;
-        while (i == DEAD) {
-          for (uint32_t j = 0; j < EBUCKET && i == DEAD; ++j) {
-            const uint64_t q = b * EBUCKET + j;
-            if (!bit(m.occ, q)) {
-              bset(m.occ, q);
-              m.n_occ += 1;
-              i = q;
-            } else if (bit(m.tomb, q)) {
-              bclr(m.tomb, q);
-              i = q;
-            }
-          }
-          b = (b + 1) & (m.nbk - 1);
-        }
+        const uint64_t i = alloc_slot(cur, tok);
         m.slot[c] = i;
         epatch[i] = c;
         m.n_edges += 1;
@@ -1241,10 +1328,11 @@ int commit_delta(emqxgm* h) {
   std::vector<uint32_t> tn_nodes;
   for (uint32_t n : dirty) {
     if (n != 0 && m.slot[n] == DEAD) continue;  // removed
-    if (n != 0) epatch[m.slot[n]] = n;
+    if (n != 0 && m.slot[n] != ROOTH) epatch[m.slot[n]] = n;  // ROOTH: the arguments, below
     tn_nodes.push_back(n);
     const uint32_t par = n ? m.parent[n] : NONE;
-    if (par != NONE && par != 0 && m.pchild[par] == n) epatch[m.slot[par]] = par;
+    if (par != NONE && par != 0 && m.pchild[par] == n && m.slot[par] != ROOTH)
+      epatch[m.slot[par]] = par;
   }
   // ---- stage the patches, upload them in one copy, apply them in one launch ----
   if (hipSetDevice(h->cfg.device) != hipSuccess) return fail(h, hipErrorInvalidDevice, "hipSetDevice");
@@ -1275,6 +1363,7 @@ int commit_delta(emqxgm* h) {
   ix.root_hf = m.hfd(0);
   ix.root_pcf = root_p ? m.pcf(root_p) : 0u;
   ix.root_phf = root_p ? m.phf(root_p) : NONE;
+  m.root_half(ix);
   ix.needs_verify = m.needs_verify;
   ix.max_depth = m.max_depth;
   ix.trie_empty = (m.n_trie == 0);
@@ -2238,7 +2327,7 @@ int emqxgm_commit(emqxgm_t* h, uint64_t* epoch) {
 namespace {
 
 constexpr uint64_t SNAP_MAGIC = 0x31534d47584d45ull;  // "EMXGMS1"
-constexpr uint32_t SNAP_VERSION = 1;
+constexpr uint32_t SNAP_VERSION = 2;  // 2: fat buckets (TrieModel fchild / half)
 
 struct SnapOut {
   FILE* f;
@@ -2288,6 +2377,8 @@ void snap_model(IO& io, M& m) {
   io.vec(m.hcode);
   io.vec(m.tok);
   io.vec(m.slot);
+  io.vec(m.fchild);
+  io.vec(m.half);
   io.vec(m.occ);
   io.vec(m.tomb);
   io.pod(m.nbk);
@@ -2328,7 +2419,8 @@ bool model_consistent(const TrieModel& m, uint64_t n_filters, std::string& why) 
   if (n == 0 || n > MAX_NODES) return bad("node count");
   for (const auto* v : {&m.ref, &m.nlit, &m.pchild, &m.hf, &m.tw, &m.tn})
     if (v->size() != n) return bad("per-node array size");
-  if (m.sig.size() != n || m.hcode.size() != n || m.tok.size() != n || m.slot.size() != n)
+  if (m.sig.size() != n || m.hcode.size() != n || m.tok.size() != n || m.slot.size() != n ||
+      m.fchild.size() != n || m.half.size() != n)
     return bad("per-node array size");
   if (!pow2(m.nbk) || m.ecap != m.nbk * EBUCKET || m.ecap > (1ull << 40)) return bad("edge capacity");
   if (m.occ.size() < m.ecap / 64 + 1 || m.tomb.size() < m.ecap / 64 + 1) return bad("edge bitmaps");
@@ -2350,7 +2442,15 @@ bool model_consistent(const TrieModel& m, uint64_t n_filters, std::string& why) 
   };
   if (m.slot[0] != DEAD) return bad("root slot");
   for (uint64_t c = 0; c < n; ++c) {
-    if (c && m.slot[c] != DEAD && m.slot[c] >= m.ecap) return bad("slot position");
+    if (c && m.slot[c] != DEAD && m.slot[c] != ROOTH && m.slot[c] >= m.ecap) return bad("slot position");
+    if (m.slot[c] == ROOTH && (!m.half[c] || m.parent[c] != 0)) return bad("root half");
+    if (const uint32_t g = m.fchild[c]) {  // the half sits right after its fat parent's slot
+      if (g >= n || !m.half[g] || m.parent[g] != c) return bad("fat child");
+      if (c ? (m.slot[c] == DEAD || m.slot[c] % EBUCKET != 0 || m.slot[g] != m.slot[c] + 1)
+            : m.slot[g] != ROOTH)
+        return bad("fat bucket");
+    }
+    if (m.half[c] && (c == 0 || m.parent[c] >= n || m.fchild[m.parent[c]] != c)) return bad("half");
     if (c && m.parent[c] != NONE && m.parent[c] >= c) return bad("parent id");
     if (m.pchild[c] >= n) return bad("'+' child id");
     if (!fid_ok(m.hf[c]) || !fid_ok(m.tw[c]) || !fid_ok(m.tn[c])) return bad("node filter id");
@@ -3055,6 +3155,14 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
     if (value < 0 || value > 2) return -EINVAL;
     std::lock_guard<std::mutex> g(h->wmu);
     h->delta_mode = (uint32_t)value;
+    return 0;
+  }
+  if (strcmp(key, "fat_buckets") == 0) {  // 1 (default) / 0: from the next full build on
+    if (value < 0 || value > 1) return -EINVAL;
+    std::lock_guard<std::mutex> g(h->wmu);
+    h->fat_mode = (uint32_t)value;
+    h->tm.valid = false;  // the next commit is a full build
+    h->dirty = true;
     return 0;
   }
   return -EINVAL;

@@ -13,6 +13,9 @@ struct DevIndex {
   uint32_t root_cf = 0, root_hf = 0xFFFFFFFFu;
   uint32_t root_pcf = 0, root_phf = 0xFFFFFFFFu;  // root's '+' child (cf 0: none)
   uint32_t root_sig = 0x3Fu;                       // root's child signature (gm_common.h)
+  // the root's fat half (gm_common.h FAT_ID): its only literal child's slot, as a bucket's
+  // second half would hold it (rh0.z = NONE: the root's literal children are probed by hash)
+  uint4 rh0 = {0u, 0u, 0xFFFFFFFFu, 0u}, rh1 = {0u, 0u, 0u, 0u};
   const uint32_t* tn_of = nullptr;  // per node: non-wildcard trie keys ending there
   // publish fan-out tables (gm_fanout.inc), per filter id < fan_nf
   const uint4* fan = nullptr;        // [fan_nf] {rt off, rt count, dl off, dl count}

@@ -385,6 +385,8 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   a.census = census;
   a.leafp_mask = ix.leafp_mask;
   a.root_sig = ix.root_sig;
+  a.rh0 = ix.rh0;
+  a.rh1 = ix.rh1;
   constexpr uint32_t SH = WALK_STK_SHALLOW, DP = WALK_STK_DEEP;
   // the deep-stack variants fit fewer blocks per CU (LDS): launch only as many as are resident
   // at once, so that no block of the persistent grid starts after the others have drained

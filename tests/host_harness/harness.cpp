@@ -111,13 +111,18 @@ struct CpuWalk {
       stk.push_back({cf & CF_ID_MASK, d});
     }
   }
+  // fat: the state's only literal child comes with it in {h0, h1} (gm_common.h FAT_ID)
   void create(uint32_t cf, uint32_t hf, uint32_t tw, uint32_t sig, uint32_t pcf, uint32_t phf,
-              uint32_t d, bool plus_ok, bool lit) {
+              uint32_t d, bool plus_ok, bool lit, bool fat = false, const uint4* h = nullptr) {
     cf = strip(cf, d);
     const uint64_t wtok = d < REC_TOKS ? (d < n ? toks[d] : 0ull) : 0ull;
-    if (d < REC_TOKS && !(sig & sig_bit(wtok))) cf &= ~CF_LIT;
+    const bool fat_go = fat && (cf & CF_LIT) && d < n && d < REC_TOKS &&
+                        (uint32_t)wtok == h[0].x && (uint32_t)(wtok >> 32) == h[0].y;
+    if (fat || (d < REC_TOKS && !(sig & sig_bit(wtok)))) cf &= ~CF_LIT;
     pcf = strip(pcf, d + 1);
     visit(cf, hf, tw, d, lit);
+    if (fat_go)
+      create(h[0].w, h[1].x, h[1].y, h[0].z >> SIG_SHIFT, h[1].z, h[1].w, d + 1, true, true);
     if (!plus_ok || d >= n || !(cf & CF_PLUS)) return;
     const bool ptw = (pcf & CF_PTW) != 0;  // the carried copy holds the child's tw, no hf
     if (d + 1 == n && (pcf & CF_TW) && !ptw) {
@@ -128,7 +133,8 @@ struct CpuWalk {
     if (d + 1 < n && (pcf & CF_PLUS)) stk.push_back({IT_PLUS | (pcf & CF_ID_MASK), d + 1});
   }
   // the edge slot of (node, key): probes buckets like k_walk (a bucket with an empty slot ends)
-  bool probe(uint32_t node, uint64_t key, uint4 s[2]) const {
+  // fat: the hit is a bucket's first slot and the second holds its fat half (copied to h)
+  bool probe(uint32_t node, uint64_t key, uint4 s[2], bool& fat, uint4 h[2]) const {
     for (uint64_t b = edge_slot(node, key, ix.emask);; b = (b + 1) & ix.emask) {
       bool empty = false;
       for (uint32_t j = 0; j < EBUCKET; ++j) {
@@ -137,6 +143,11 @@ struct CpuWalk {
             q[0].y == (uint32_t)(key >> 32)) {
           s[0] = q[0];
           s[1] = q[1];
+          fat = j == 0 && (q[SLOT_U4].z & CF_ID_MASK) == FAT_ID;
+          if (fat) {
+            h[0] = q[SLOT_U4];
+            h[1] = q[SLOT_U4 + 1];
+          }
           return true;
         }
         empty = empty || q[0].z == NONE;
@@ -155,8 +166,9 @@ struct CpuWalk {
       if (pl[i] || hs[i]) return out;  // wildcard topic name -> [] (emqx_trie.erl:157-166)
     if (ix.trie_empty) return out;
     dollar = !topic.empty() && topic[0] == '$';
+    const uint4 rh[2] = {ix.rh0, ix.rh1};
     create(ix.root_cf, dollar ? NONE : ix.root_hf, NONE, ix.root_sig, ix.root_pcf, ix.root_phf, 0,
-           !dollar, false);
+           !dollar, false, (ix.rh0.z & CF_ID_MASK) == FAT_ID, rh);
     while (!stk.empty()) {
       const auto it = stk.back();
       stk.pop_back();
@@ -166,10 +178,13 @@ struct CpuWalk {
       }
       const uint32_t node = it.first & CF_ID_MASK, k = it.second;
       const uint64_t key = (it.first & IT_PLUS) ? PLUS_TOK : toks[k];
-      uint4 s[2];
-      if (probe(node, key, s))
+      uint4 s[2], hh[2];
+      bool fat = false;
+      const bool hit = probe(node, key, s, fat, hh);
+      if (getenv("HH_TRACE")) fprintf(stderr, "probe node %u k %u plus %d -> %d fat %d\n", node, k, (it.first & IT_PLUS) ? 1 : 0, hit ? 1 : 0, fat ? 1 : 0);
+      if (hit)
         create(s[0].w, s[1].x, s[1].y, s[0].z >> SIG_SHIFT, s[1].z, s[1].w, k + 1, true,
-               !(it.first & IT_PLUS));
+               !(it.first & IT_PLUS), fat, hh);
     }
     return out;
   }
@@ -256,7 +271,7 @@ int main(int argc, char** argv) {
   Oracle orc;
   std::set<std::string> in_trie, keyed;
   std::map<std::string, std::vector<std::pair<uint32_t, uint32_t>>> dests;
-  uint64_t checks = 0;
+  uint64_t checks = 0, fat_seen = 0;
   const std::string snap = std::string(argc > 4 ? argv[4] : "/tmp") + "/emqxgm_harness_" +
                            std::to_string(seed) + ".snap";
   for (int round = 0; round < rounds; ++round) {
@@ -399,6 +414,7 @@ int main(int argc, char** argv) {
                     &ids, &nids, rex.data());
     for (emqxgm_t* h : {hd, hf}) {
       const DevIndex& ix = h->cur->ix;
+      for (uint32_t c : h->tm.fchild) fat_seen += c != 0;
       for (size_t i = 0; i < topics.size(); ++i) {
         const std::string& t = topics[i];
         CpuWalk w(ix);
@@ -412,6 +428,38 @@ int main(int argc, char** argv) {
         for (uint64_t j = row[i]; j < row[i + 1]; ++j) ws.push_back(orc.names[ids[j]]);
         std::sort(gs.begin(), gs.end());
         std::sort(ws.begin(), ws.end());
+        if (gs != ws && getenv("HH_DEBUG")) {
+          setenv("HH_TRACE", "1", 1);
+          CpuWalk w2(ix);
+          w2.run(t, h->test_mask);
+          unsetenv("HH_TRACE");
+          for (auto& x : gs) fprintf(stderr, "got  %s\n", x.c_str());
+          for (auto& x : ws) fprintf(stderr, "want %s\n", x.c_str());
+          for (auto& x : ws) {
+            if (std::count(gs.begin(), gs.end(), x)) continue;
+            std::vector<uint64_t> tk;
+            std::vector<uint8_t> pl, hs;
+            bool hashed;
+            tokenize((const uint8_t*)x.data(), (uint32_t)x.size(), h->test_mask, tk, pl, hs, hashed);
+            uint32_t cur = 0;
+            TrieModel& m = h->tm;
+            fprintf(stderr, "root fchild %u rh0.z %08x\n", m.fchild[0], ix.rh0.z);
+            for (size_t w = 0; w + (hs.back() ? 1 : 0) < tk.size(); ++w) {
+              const uint32_t* v = m.emap.find(cur, pl[w] ? PLUS_TOK : tk[w]);
+              if (!v) { fprintf(stderr, "  no edge at %zu\n", w); break; }
+              cur = *v;
+              const uint64_t sl = m.slot[cur];
+              fprintf(stderr, "  w%zu node %u slot %lld half %u fchild %u nlit %u pchild %u cf %08x", w, cur,
+                      (long long)sl, m.half[cur], m.fchild[cur], m.nlit[cur], m.pchild[cur], m.cf(cur));
+              if (sl < m.ecap) {
+                const uint4* q = ix.edges + SLOT_U4 * sl;
+                fprintf(stderr, " dev{%08x %08x %08x %08x}{%08x %08x %08x %08x} next{%08x %08x %08x %08x}", q[0].x, q[0].y, q[0].z, q[0].w,
+                        q[1].x, q[1].y, q[1].z, q[1].w, q[2].x, q[2].y, q[2].z, q[2].w);
+              }
+              fprintf(stderr, "\n");
+            }
+          }
+        }
         CHECK(gs == ws, "round %d (%s) topic '%s': %zu vs %zu filters", round,
               h == hd ? "delta" : "full", t.c_str(), gs.size(), ws.size());
         const uint32_t ex = cpu_exact(ix, t, is_wild_s(t));
@@ -449,6 +497,7 @@ int main(int argc, char** argv) {
   emqxgm_get_stats(hd, &sd);
   emqxgm_get_stats(hf, &sf);
   CHECK(sf.delta_commits == 0, "the rebuilding engine never patches");
+  CHECK(fat_seen > 0, "no fat bucket was ever built");
   printf("OK %d %llu %llu %llu\n", rounds, (unsigned long long)sd.delta_commits,
          (unsigned long long)sd.full_commits, (unsigned long long)checks);
   emqxgm_destroy(hd);
