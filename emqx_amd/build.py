@@ -21,7 +21,7 @@ ENGINE_SO = os.path.join(ROOT, "emqx_amd", "libemqx_gpumatch.so")
 ORACLE_SO = os.path.join(ROOT, "oracle", "build", "libemqx_ref.so")
 WORKLOAD_SO = os.path.join(ROOT, "workloads", "libemqx_workload.so")
 
-ENGINE_SRCS = ["gm_kernels.hip", "gm_engine.cpp", "gm_retain.cpp"]
+ENGINE_SRCS = ["gm_kernels.hip", "gm_engine.cpp", "gm_retain.cpp", "gm_batcher.cpp"]
 ENGINE_DEPS = sorted(set(ENGINE_SRCS) | {f for f in os.listdir(CSRC) if f.endswith((".h", ".inc"))})
 
 

@@ -1010,9 +1010,9 @@ int commit_full(emqxgm* h) {
   // fat buckets (gm_common.h FAT_ID): a node at depth 2, 4 or 6 reached by a literal edge whose
   // only literal child is G takes a bucket of its own with G in the second half (halves are at
   // odd depths, so a half is never fat itself); the root's only literal child rides in the
-  // kernel arguments.  Fat nodes are placed first, into the first bucket of their chain with
-  // both slots free; a bucket they pass that still has a free slot gets it TOMBed (a lookup
-  // must not stop there; later inserts may reuse it).
+  // kernel arguments.  Fat nodes are placed first, each only into its home bucket when both
+  // of its slots are free (else the node stays thin): no lookup chain grows past a bucket
+  // that still has a free slot (r03 A/B: TOMBing passed buckets lengthened cfg2's miss chains).
   m.fchild.assign(n_nodes, 0u);
   m.half.assign(n_nodes, 0u);
   if (h->fat_mode) {
@@ -1031,21 +1031,16 @@ int commit_full(emqxgm* h) {
   }
   for (uint32_t c = 1; c < n_nodes; ++c) {
     if (!m.fchild[c]) continue;
-    uint64_t b = edge_slot(m.parent[c], m.tok[c], m.nbk - 1);
-    for (;;) {
-      const uint64_t q = b * EBUCKET;
-      if (!bit(m.occ, q) && !bit(m.occ, q + 1)) break;
-      for (uint32_t j = 0; j < EBUCKET; ++j)
-        if (!bit(m.occ, q + j)) {
-          bset(m.occ, q + j);
-          bset(m.tomb, q + j);
-        }
-      b = (b + 1) & (m.nbk - 1);
+    const uint64_t q = edge_slot(m.parent[c], m.tok[c], m.nbk - 1) * EBUCKET;
+    if (bit(m.occ, q) || bit(m.occ, q + 1)) {  // home bucket taken: thin
+      m.half[m.fchild[c]] = 0;
+      m.fchild[c] = 0;
+      continue;
     }
-    bset(m.occ, b * EBUCKET);
-    bset(m.occ, b * EBUCKET + 1);
-    m.slot[c] = b * EBUCKET;
-    m.slot[m.fchild[c]] = b * EBUCKET + 1;
+    bset(m.occ, q);
+    bset(m.occ, q + 1);
+    m.slot[c] = q;
+    m.slot[m.fchild[c]] = q + 1;
   }
   if (m.fchild[0]) m.slot[m.fchild[0]] = ROOTH;
   for (uint32_t c = 1; c < n_nodes; ++c) {

@@ -175,7 +175,7 @@ struct RetainDev {
 // count (fill = false: cnt = runs + cnt_in) or fill (at rbase + rshift) the runs of each
 // filter in one store; delta tags its runs
 hipError_t launch_retain_walk(const RetainDev& st, const uint8_t* fb, const uint32_t* fo, uint32_t n,
-                              uint4* frames, uint32_t max_plus, uint32_t* cnt,
+                              const uint8_t* tail, uint4* frames, uint32_t max_plus, uint32_t* cnt,
                               const uint32_t* cnt_in, const uint32_t* rbase,
                               const uint32_t* rshift, bool delta, uint2* runs, bool fill,
                               hipStream_t s);

@@ -578,12 +578,12 @@ hipError_t launch_rules(const uint8_t* nb, const uint32_t* no, uint32_t n, const
 }
 
 hipError_t launch_retain_walk(const RetainDev& st, const uint8_t* fb, const uint32_t* fo, uint32_t n,
-                              uint4* frames, uint32_t max_plus, uint32_t* cnt,
+                              const uint8_t* tail, uint4* frames, uint32_t max_plus, uint32_t* cnt,
                               const uint32_t* cnt_in, const uint32_t* rbase,
                               const uint32_t* rshift, bool delta, uint2* runs, bool fill,
                               hipStream_t s) {
   if (n == 0) return hipSuccess;
-  RetainArgs a{fb, fo, n, st.rn, st.redge, st.rmask, st.rch, st.rw, st.pool, frames, max_plus,
+  RetainArgs a{fb, fo, n, st.rn, st.redge, st.rmask, st.rch, st.rw, st.pool, tail, frames, max_plus,
                cnt, cnt_in, rbase, rshift, delta ? RUN_DELTA : 0u, runs};
   const dim3 grid((n + WG - 1) / WG);
   if (fill)

@@ -5,7 +5,8 @@
 // Reference: apps/emqx_retainer/src/emqx_retainer_mnesia.erl (store_retained/2 :138-152,
 // delete_message/2 :166-180, read_message/2 :182-183 + read_messages/1 :372-382,
 // match_messages/3 :185-195 -> search_table/3 :300-330, clean/1, size/1) and the match-spec
-// pattern of emqx_retainer_index:condition/1 (emqx_retainer_index.erl:97-112).
+// patterns of emqx_retainer_index:condition/1 (emqx_retainer_index.erl:97-112, the full scan)
+// and condition/2 (:174-200, the index path of the configured index specs).
 #include <errno.h>
 #include <hip/hip_runtime.h>
 #include <string.h>
@@ -68,6 +69,11 @@ struct emqxgm_retain {
   std::vector<uint64_t> exp_committed;   // per id
   uint64_t n_committed = 0;
   int64_t delta_max = -1;  // delta topics before a full rebuild (-1: max(4096, base / 16))
+  // index specs (config_indices/0: sorted); empty = search_table's full scan only.  Default:
+  // ?DEFAULT_INDICES of emqx_retainer_schema.erl:24-29
+  std::vector<std::vector<uint32_t>> indices{{1, 2, 3}, {1, 3}, {2, 3}, {3}};
+  std::vector<uint8_t> h_fb, h_tail;  // planned filters (gm_retain.inc: cut, open tail)
+  std::vector<uint32_t> h_fo;
   uint64_t full_builds = 0, delta_builds = 0;
   // batch scratch and host outputs
   std::vector<Buf> sc;
@@ -78,7 +84,76 @@ struct emqxgm_retain {
 namespace {
 
 enum { S_FB, S_FO, S_FRAMES, S_CNT, S_RBASE, S_RUNS, S_ACNT, S_ABASE, S_OUT, S_PTR, S_TMP, S_CTL,
-       S_CNT2, S_PATCH };
+       S_CNT2, S_PATCH, S_TAIL };
+
+// emqx_retainer_index:index_score/2 (emqx_retainer_index.erl:141-152): index positions with a
+// literal word, in order, up to the first index position holding '+' or '#'.
+uint32_t index_score(const std::vector<uint32_t>& ix, const std::vector<std::pair<uint32_t, uint32_t>>& w,
+                     const uint8_t* f) {
+  uint32_t score = 0, i = 0;
+  for (uint32_t n = 1; n <= w.size() && i < ix.size(); ++n) {
+    if (ix[i] != n) continue;
+    const uint32_t b = w[n - 1].first, l = w[n - 1].second;
+    if (l == 1 && (f[b] == '+' || f[b] == '#')) return score;
+    ++score;
+    ++i;
+  }
+  return score;
+}
+
+// search_table/3 (emqx_retainer_mnesia.erl:300-330) for one filter, in the walk's terms
+// (gm_retain.inc): select_index/2 (:83-91, 154-165: the first index with the best score > 0,
+// none -> the full scan of condition/1, the filter as it is).  On the index path condition/2
+// (:174-200) walks the words with the index positions left; matched against a stored topic's
+// index key its pattern selects:
+//  * at a '#' reached while index positions remain or right as they run out (:174-177): both
+//    pattern parts open -- the words before it as a prefix with any tail, i.e. the filter cut
+//    after that '#';
+//  * once the positions are used up at a word that is not '#' (:178-179): the rest goes through
+//    condition/1, together the full scan's pattern -- the filter as it is;
+//  * when the filter ends while positions remain (:180-181): the index part open, the other
+//    closed -- the topic has the filter's words (with '+') and may go on only through index
+//    positions, i.e. up to `tail` more words, tail = the run of positions right after the
+//    filter's last word.
+// Checked against the restated index search by tests/test_oracle_golden.py (the predicate
+// form, R.retained_match_indexed).  Writes the (possibly cut) filter to fb, returns its tail.
+uint32_t plan_filter(const std::vector<std::vector<uint32_t>>& indices, const uint8_t* f,
+                     uint32_t len, std::vector<uint8_t>& fb) {
+  std::vector<std::pair<uint32_t, uint32_t>> w;
+  for (uint32_t b = 0, q = 0; q <= len; ++q)
+    if (q == len || f[q] == '/') {
+      w.emplace_back(b, q - b);
+      b = q + 1;
+    }
+  const std::vector<uint32_t>* sel = nullptr;
+  uint32_t best = 0;
+  for (const auto& ix : indices) {
+    const uint32_t sc = index_score(ix, w, f);
+    if (sc > best) {
+      best = sc;
+      sel = &ix;
+    }
+  }
+  if (!sel) {
+    fb.insert(fb.end(), f, f + len);
+    return 0;
+  }
+  size_t i = 0;  // index positions used so far
+  for (uint32_t n = 1; n <= w.size(); ++n) {
+    if (w[n - 1].second == 1 && f[w[n - 1].first] == '#') {
+      fb.insert(fb.end(), f, f + w[n - 1].first + 1);  // ".../#": the words before it + '#'
+      return 0;
+    }
+    if (i == sel->size()) break;  // the full scan's pattern
+    if ((*sel)[i] == n) ++i;
+  }
+  const uint32_t k = (uint32_t)w.size();
+  uint32_t tail = 0;
+  for (; i < sel->size(); ++i)
+    if ((*sel)[i] == k + 1 + tail) ++tail;
+  fb.insert(fb.end(), f, f + len);
+  return tail;
+}
 
 int grow(emqxgm_retain* r, size_t slot, uint64_t bytes);
 
@@ -467,6 +542,25 @@ int emqxgm_retain_tune(emqxgm_retain_t* r, const char* key, int64_t value) {
   return -EINVAL;
 }
 
+int emqxgm_retain_set_indices(emqxgm_retain_t* r, const uint32_t* pos, const uint32_t* offsets,
+                              uint32_t n) {
+  if (!r || (n && (!pos || !offsets)) || n > 64) return -EINVAL;
+  std::vector<std::vector<uint32_t>> ix(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (offsets[i + 1] <= offsets[i] || offsets[i + 1] - offsets[i] > 255) return -EINVAL;
+    for (uint32_t q = offsets[i]; q < offsets[i + 1]; ++q) {
+      // positions >= 1, strictly ascending (emqx_retainer_schema: an index is a sorted set)
+      if (pos[q] == 0 || pos[q] > 65535 || (q > offsets[i] && pos[q] <= pos[q - 1])) return -EINVAL;
+      ix[i].push_back(pos[q]);
+    }
+  }
+  std::sort(ix.begin(), ix.end());  // config_indices/0 (emqx_retainer_mnesia.erl) sorts them
+  ix.erase(std::unique(ix.begin(), ix.end()), ix.end());
+  std::lock_guard<std::mutex> g(r->mu);
+  r->indices = std::move(ix);
+  return 0;
+}
+
 int emqxgm_retain_stats(emqxgm_retain_t* r, uint64_t out[4]) {
   if (!r || !out) return -EINVAL;
   std::lock_guard<std::mutex> g(r->mu);
@@ -512,6 +606,7 @@ int emqxgm_retain_match(emqxgm_retain_t* r, const uint8_t* bytes, const uint32_t
   if (!r || !out || !offsets || (offsets[n] && !bytes)) return -EINVAL;
   // '+' words per filter bound the DFS frames of a lane
   uint32_t max_plus = 0;
+  std::vector<uint32_t> plus_of(n);
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t b = offsets[i], e = offsets[i + 1];
     if (e < b || e - b > 65535) return -EINVAL;
@@ -521,9 +616,24 @@ int emqxgm_retain_match(emqxgm_retain_t* r, const uint8_t* bytes, const uint32_t
         plus += (q - s == 1 && bytes[s] == '+');
         s = q + 1;
       }
-    max_plus = std::max(max_plus, plus);
+    plus_of[i] = plus;
   }
   std::lock_guard<std::mutex> g(r->mu);
+  // the index path's filter plan (cut after a '#', open tails): the walk's frames per filter
+  // are its '+' words plus its tail
+  r->h_fb.clear();
+  r->h_fo.assign(1, 0u);
+  r->h_tail.resize(n);
+  bool any_tail = false;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t tl = plan_filter(r->indices, bytes + offsets[i], offsets[i + 1] - offsets[i], r->h_fb);
+    r->h_tail[i] = (uint8_t)tl;
+    any_tail = any_tail || tl;
+    r->h_fo.push_back((uint32_t)r->h_fb.size());
+    max_plus = std::max<uint32_t>(max_plus, plus_of[i] + tl);
+  }
+  bytes = r->h_fb.data();
+  offsets = r->h_fo.data();
   out->n = n;
   r->h_ptr.assign((size_t)n + 1, 0);
   r->h_id.clear();
@@ -539,9 +649,11 @@ int emqxgm_retain_match(emqxgm_retain_t* r, const uint8_t* bytes, const uint32_t
       (rc = grow(r, S_FRAMES, (uint64_t)n * std::max<uint32_t>(max_plus, 1) * 16)) ||
       (rc = grow(r, S_CNT, (uint64_t)n * 4)) || (rc = grow(r, S_RBASE, ((uint64_t)n + 1) * 4)) ||
       (rc = grow(r, S_PTR, ((uint64_t)n + 1) * 4)) || (rc = grow(r, S_CTL, 64)) ||
-      (rc = grow(r, S_TMP, (uint64_t)scan_tmp_words(n) * 4)))
+      (rc = grow(r, S_TMP, (uint64_t)scan_tmp_words(n) * 4)) || (rc = grow(r, S_TAIL, (uint64_t)n + 16)))
     return rc;
   auto B = [&](int k) { return r->sc[k].p; };
+  if (any_tail) RCHK(r, hipMemcpyAsync(B(S_TAIL), r->h_tail.data(), n, hipMemcpyHostToDevice, s));
+  const uint8_t* tail = any_tail ? (const uint8_t*)B(S_TAIL) : nullptr;
   if (fbytes) RCHK(r, hipMemcpyAsync(B(S_FB), bytes, fbytes, hipMemcpyHostToDevice, s));
   RCHK(r, hipMemcpyAsync(B(S_FO), offsets, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s));
   const uint8_t* fb = (const uint8_t*)B(S_FB);
@@ -557,10 +669,10 @@ int emqxgm_retain_match(emqxgm_retain_t* r, const uint8_t* bytes, const uint32_t
     cnt2 = (uint32_t*)B(S_CNT2);
   }
   uint4* frames = (uint4*)B(S_FRAMES);
-  RCHK(r, launch_retain_walk(r->base.d, fb, fo, n, frames, max_plus, cnt, nullptr, nullptr, nullptr,
+  RCHK(r, launch_retain_walk(r->base.d, fb, fo, n, tail, frames, max_plus, cnt, nullptr, nullptr, nullptr,
                              false, nullptr, false, s));
   if (has_delta)
-    RCHK(r, launch_retain_walk(r->delta.d, fb, fo, n, frames, max_plus, cnt2, cnt, nullptr, nullptr,
+    RCHK(r, launch_retain_walk(r->delta.d, fb, fo, n, tail, frames, max_plus, cnt2, cnt, nullptr, nullptr,
                                true, nullptr, false, s));
   RCHK(r, launch_scan(has_delta ? cnt2 : cnt, rbase, n, (uint32_t*)B(S_TMP), ctl, s));
   uint32_t nr = 0;
@@ -573,10 +685,10 @@ int emqxgm_retain_match(emqxgm_retain_t* r, const uint8_t* bytes, const uint32_t
   uint2* runs = (uint2*)B(S_RUNS);
   uint32_t* acnt = (uint32_t*)B(S_ACNT);
   uint32_t* abase = (uint32_t*)B(S_ABASE);
-  RCHK(r, launch_retain_walk(r->base.d, fb, fo, n, frames, max_plus, nullptr, nullptr, rbase,
+  RCHK(r, launch_retain_walk(r->base.d, fb, fo, n, tail, frames, max_plus, nullptr, nullptr, rbase,
                              nullptr, false, runs, true, s));
   if (has_delta)
-    RCHK(r, launch_retain_walk(r->delta.d, fb, fo, n, frames, max_plus, nullptr, nullptr, rbase, cnt,
+    RCHK(r, launch_retain_walk(r->delta.d, fb, fo, n, tail, frames, max_plus, nullptr, nullptr, rbase, cnt,
                                true, runs, true, s));
   // live ids per run -> scan -> ids
   unsigned long long* total = (unsigned long long*)(ctl + 4);

@@ -55,6 +55,19 @@ class _BatchOut(C.Structure):
                 ("filter_id", C.POINTER(C.c_uint32)), ("exact_id", C.POINTER(C.c_uint32))]
 
 
+class _BatcherCfg(C.Structure):
+    _fields_ = [("window_topics", C.c_uint32), ("window_bytes", C.c_uint32),
+                ("window_us", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class _WindowOut(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("n_pairs", C.c_uint32), ("tag", C.POINTER(C.c_uint64)),
+                ("row", C.POINTER(C.c_uint32)), ("filter_id", C.POINTER(C.c_uint32)),
+                ("foff", C.POINTER(C.c_uint64)), ("fbytes", C.POINTER(C.c_uint8)),
+                ("exact_id", C.POINTER(C.c_uint32)), ("flush_ns", C.c_uint64),
+                ("done_ns", C.c_uint64)]
+
+
 class _RetOut(C.Structure):
     _fields_ = [("n", C.c_uint32), ("n_ids", C.c_uint64), ("ptr", C.POINTER(C.c_uint64)),
                 ("id", C.POINTER(C.c_uint32))]
@@ -126,9 +139,16 @@ SYMBOLS = {
     "emqxgm_retain_size": (C.c_int, [_P, _U64P]),
     "emqxgm_retain_tune": (C.c_int, [_P, C.c_char_p, C.c_int64]),
     "emqxgm_retain_stats": (C.c_int, [_P, _U64P]),
+    "emqxgm_retain_set_indices": (C.c_int, [_P, _P, _P, C.c_uint32]),
     "emqxgm_retain_read": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint64, _U32P]),
     "emqxgm_retain_topic": (C.c_int, [_P, C.c_uint32, C.POINTER(_U8P), _U32P]),
     "emqxgm_retain_match": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, C.POINTER(_RetOut)]),
+    "emqxgm_batcher_create": (C.c_int, [_P, C.POINTER(_BatcherCfg), C.POINTER(_P)]),
+    "emqxgm_batcher_destroy": (None, [_P]),
+    "emqxgm_batcher_add": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint64, _U32P]),
+    "emqxgm_batcher_due": (C.c_int, [_P, C.c_uint64]),
+    "emqxgm_batcher_flush": (C.c_int, [_P, _U64P]),
+    "emqxgm_batcher_collect": (C.c_int, [_P, C.c_uint64, C.POINTER(_WindowOut)]),
     "emqxgm_set_profiling": (C.c_int, [_P, C.c_int]),
     "emqxgm_tune": (C.c_int, [_P, C.c_char_p, C.c_int64]),
     "emqxgm_get_stats": (C.c_int, [_P, C.POINTER(_Stats)]),
@@ -521,3 +541,74 @@ class Engine:
         s = _Stats()
         self._check(self._lib.emqxgm_get_stats(self._h, C.byref(s)), "stats")
         return {k: getattr(s, k) for k, _ in _Stats._fields_}
+
+
+@dataclass
+class Window:
+    """A collected batcher window: per topic (in add order) its tag, its trie filters' bytes
+    and its exact route key id (NONE: none); flush -> completion latency in ns."""
+    tag: np.ndarray        # uint64 [n]
+    row: np.ndarray        # uint32 [n+1]
+    filter_id: np.ndarray  # uint32 [n_pairs]
+    foff: np.ndarray       # uint64 [n_pairs+1]
+    fbytes: bytes
+    exact_id: np.ndarray   # uint32 [n]
+    latency_ns: int
+
+    def filters(self, i: int) -> List[bytes]:
+        a, b = int(self.row[i]), int(self.row[i + 1])
+        return [self.fbytes[int(self.foff[j]):int(self.foff[j + 1])] for j in range(a, b)]
+
+
+class Batcher:
+    """emqxgm_batcher_*: the NIF batcher core (include/emqx_gpumatch.h) over an Engine."""
+
+    def __init__(self, engine: Engine, window_topics: int = 0, window_bytes: int = 0,
+                 window_us: int = 0):
+        self._lib = engine._lib
+        self._eng = engine  # the batcher's pinned windows belong to the engine's device
+        cfg = _BatcherCfg(window_topics, window_bytes, window_us, 0)
+        b = C.c_void_p()
+        engine._check(self._lib.emqxgm_batcher_create(engine._h, C.byref(cfg), C.byref(b)),
+                      "batcher_create")
+        self._b = b
+
+    def close(self):
+        if getattr(self, "_b", None):
+            self._lib.emqxgm_batcher_destroy(self._b)
+            self._b = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add(self, topic: bytes, tag: int) -> bool:
+        """Appends a topic to the open window; True when the window is now full."""
+        s = C.c_uint32()
+        return bool(self._eng._check(self._lib.emqxgm_batcher_add(self._b, topic, len(topic), tag,
+                                                                  C.byref(s)), "batcher_add"))
+
+    def due(self, now_ns: int) -> bool:
+        return bool(self._eng._check(self._lib.emqxgm_batcher_due(self._b, now_ns), "batcher_due"))
+
+    def flush(self) -> int:
+        """Submits the open window; its id (0: it was empty)."""
+        w = C.c_uint64()
+        self._eng._check(self._lib.emqxgm_batcher_flush(self._b, C.byref(w)), "batcher_flush")
+        return int(w.value)
+
+    def collect(self, window: int) -> Window:
+        o = _WindowOut()
+        self._eng._check(self._lib.emqxgm_batcher_collect(self._b, window, C.byref(o)),
+                         "batcher_collect")
+        n, m = o.n, o.n_pairs
+
+        def arr(p, k, dt):
+            return np.ctypeslib.as_array(p, shape=(k,)).copy() if k else np.zeros(0, dt)
+        nb = int(o.foff[m]) if m else 0
+        return Window(arr(o.tag, n, np.uint64), arr(o.row, n + 1, np.uint32),
+                      arr(o.filter_id, m, np.uint32), arr(o.foff, m + 1, np.uint64),
+                      C.string_at(o.fbytes, nb) if nb else b"", arr(o.exact_id, n, np.uint32),
+                      int(o.done_ns - o.flush_ns))

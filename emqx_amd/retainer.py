@@ -2,10 +2,12 @@
 SURVEY 8f rank 4: retained topics (messages stay with the caller) and the reverse match
 ``match_messages`` -- a subscription filter to the stored topics it selects -- in batches.
 
-The selected set is ``search_table/3``'s full-scan set (:300-330): the topics whose word list
-matches the ``emqx_retainer_index:condition/1`` pattern of the filter ('+' any one word, a last
-'#' any tail, no '$' rule) with expiry 0 or > now.  (With index specs configured the reference
-may also return some longer topics, an over-selection of its index path)
+The selected set is ``search_table/3``'s (:300-330) with expiry 0 or > now and no '$' rule:
+with index specs configured -- by default the reference's ``[[1,2,3],[1,3],[2,3],[3]]``
+(emqx_retainer_schema.erl:24-29) -- the index path of the best-scoring index
+(emqx_retainer_index.erl:83-91, 141-200: ``a/+`` also selects ``a/x/y`` under ``[1,2,3]``);
+with ``index_specs=[]``, or when no index scores, the full scan of ``condition/1`` (:97-112:
+'+' any one word, a last '#' any tail).  See DESIGN.md 6c.
 
     r = Retainer()
     r.store_retained(b"sensor/1/temp", expiry_ms=0)
@@ -26,8 +28,11 @@ def _now_ms() -> int:
     return int(time.time() * 1000)
 
 
+DEFAULT_INDEX_SPECS = ((1, 2, 3), (1, 3), (2, 3), (3,))  # emqx_retainer_schema.erl:24-29
+
+
 class Retainer:
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, index_specs: Sequence[Sequence[int]] = DEFAULT_INDEX_SPECS):
         self._lib = E.lib()
         h = C.c_void_p()
         rc = self._lib.emqxgm_retain_create(device, C.byref(h))
@@ -35,6 +40,15 @@ class Retainer:
             raise E.EngineError(f"emqxgm_retain_create failed: {rc}")
         self._h = h
         self._dirty = False
+        self.set_index_specs(index_specs)
+
+    def set_index_specs(self, specs: Sequence[Sequence[int]]) -> None:
+        """retainer.backend.index_specs (config_indices/0); [] = the full scan only."""
+        pos = np.array([p for s in specs for p in s], np.uint32)
+        off = np.zeros(len(specs) + 1, np.uint32)
+        np.cumsum([len(s) for s in specs], out=off[1:])
+        self._check(self._lib.emqxgm_retain_set_indices(self._h, E._ptr(pos), E._ptr(off),
+                                                        len(specs)), "retain_set_indices")
 
     def close(self):
         if self._h:

@@ -277,9 +277,13 @@ int emqxgm_match_rules(emqxgm_t* h, const uint8_t* name_bytes, const uint32_t* n
  * The retainer's mnesia backend (apps/emqx_retainer/src/emqx_retainer_mnesia.erl) on the
  * device: topics of retained messages (the messages stay with the caller) with their expiry
  * times, and match_messages/3 (:185-195) for batches of subscription filters.  The selected set
- * is search_table/3's full-scan set (:300-330, condition/1 of emqx_retainer_index.erl:97-112:
- * '+' any word, a last '#' any tail, no '$' rule, expiry 0 or > now).  Mutations are visible
- * after emqxgm_retain_commit. */
+ * is search_table/3's (:300-330): with index specs configured (emqxgm_retain_set_indices; the
+ * default is the reference's ?DEFAULT_INDICES [[1,2,3],[1,3],[2,3],[3]],
+ * emqx_retainer_schema.erl:24-29) the index path of the best-scoring index (select_index/2 and
+ * condition/2, emqx_retainer_index.erl:83-91, 141-200), including its open index tail (a/+
+ * also selects a/x/y under [1,2,3]); with none, or when no index scores, the full scan of
+ * condition/1 (:97-112: '+' any word, a last '#' any tail).  No '$' rule; expiry 0 or > now.
+ * Mutations are visible after emqxgm_retain_commit. */
 typedef struct emqxgm_retain emqxgm_retain_t;
 int emqxgm_retain_create(int32_t device, emqxgm_retain_t** out);
 void emqxgm_retain_destroy(emqxgm_retain_t* r);
@@ -294,6 +298,12 @@ int emqxgm_retain_commit(emqxgm_retain_t* r);
  * was built; re-storing or deleting a base topic patches it in place.  "delta_max": delta topics
  * before a commit rebuilds the base (-1 = max(4096, base / 16), 0 = rebuild at every commit). */
 int emqxgm_retain_tune(emqxgm_retain_t* r, const char* key, int64_t value);
+/* The retainer's index specs (retainer.backend.index_specs, config_indices/0 of
+ * emqx_retainer_mnesia.erl:424-425): spec i = positions pos[offsets[i] .. offsets[i+1]), each
+ * >= 1 and strictly ascending; n = 0 selects the full scan only (index_specs = []).  -EINVAL on a
+ * malformed spec (then the specs are unchanged).  Applies to the next emqxgm_retain_match. */
+int emqxgm_retain_set_indices(emqxgm_retain_t* r, const uint32_t* pos, const uint32_t* offsets,
+                              uint32_t n);
 /* out = {full rebuilds, delta commits, base topics (incl. deleted), delta topics} */
 int emqxgm_retain_stats(emqxgm_retain_t* r, uint64_t out[4]);
 /* size/1 (:246-247): committed topics */
@@ -313,6 +323,52 @@ typedef struct emqxgm_retain_out { /* host-resident, valid until the next call o
 /* match_messages/3 for a batch of filters (packed bytes + [n+1] offsets on the host) */
 int emqxgm_retain_match(emqxgm_retain_t* r, const uint8_t* bytes, const uint32_t* offsets,
                         uint32_t n, uint64_t now_ms, emqxgm_retain_out* out);
+
+/* ---- NIF batcher core: publish windows over the host pipes ----------------------------------
+ * What the emqx_trie_gpu NIF (c_src/emqx_trie_gpu_nif.c) calls per published topic.  The
+ * reference answers every publish in its own process (emqx_broker:publish/1 ->
+ * emqx_router:match_routes/1 -> emqx_trie:match/1, emqx_broker.erl:218-232,
+ * emqx_router.erl:141-157, emqx_trie.erl:147-169); the batcher packs the topics of concurrent
+ * publishers into a window in pinned host memory, submits a full window (or one that is due)
+ * with emqxgm_match_batch_submit, and on collection expands every topic's trie row into its
+ * filter bytes with one emqxgm_filters_copy per window, so the NIF builds each caller's filter
+ * list from one arena.  Up to EMQXGM_HOST_PIPES windows are in flight; a window's result stays
+ * valid until that many more windows are flushed.  One thread drives a batcher (the NIF's
+ * batcher process); the handle's other calls stay thread-safe around it. */
+typedef struct emqxgm_batcher emqxgm_batcher_t;
+typedef struct emqxgm_batcher_cfg {
+  uint32_t window_topics; /* topics per window (0 = 65,536; <= the engine's batch_max) */
+  uint32_t window_bytes;  /* topic bytes per window (0 = 64 x window_topics) */
+  uint32_t window_us;     /* a non-empty window is due this long after its first topic (0 = 50) */
+  uint32_t reserved;
+} emqxgm_batcher_cfg;
+typedef struct emqxgm_window_out {
+  uint32_t n;                 /* topics in the window, in the order they were added */
+  uint32_t n_pairs;
+  const uint64_t* tag;        /* [n] the caller's tag of each topic (e.g. its waiter) */
+  const uint32_t* row;        /* [n+1] topic i's trie filters are pairs row[i] .. row[i+1] */
+  const uint32_t* filter_id;  /* [n_pairs] */
+  const uint64_t* foff;       /* [n_pairs + 1] pair j's filter bytes: fbytes[foff[j] .. foff[j+1]) */
+  const uint8_t* fbytes;
+  const uint32_t* exact_id;   /* [n] route key equal to the topic, or EMQXGM_NONE */
+  uint64_t flush_ns, done_ns; /* CLOCK_MONOTONIC at the flush and when the result was complete */
+} emqxgm_window_out;
+int emqxgm_batcher_create(emqxgm_t* h, const emqxgm_batcher_cfg* cfg, emqxgm_batcher_t** out);
+void emqxgm_batcher_destroy(emqxgm_batcher_t* b);
+/* Appends a topic to the open window (*slot = its index there).  Returns 1 when the window is
+ * now full (flush it before the next add), 0 otherwise; -E2BIG for a topic longer than a window,
+ * -ENOSPC when the open window is full, -EINVAL. */
+int emqxgm_batcher_add(emqxgm_batcher_t* b, const uint8_t* topic, uint32_t len, uint64_t tag,
+                       uint32_t* slot);
+/* 1 when the open window holds topics and its first one was added window_us or more before
+ * now_ns (CLOCK_MONOTONIC), else 0. */
+int emqxgm_batcher_due(emqxgm_batcher_t* b, uint64_t now_ns);
+/* Submits the open window and opens an empty one; *window = the window's id (0: it was empty,
+ * nothing submitted).  -EBUSY when EMQXGM_HOST_PIPES windows are flushed and not collected. */
+int emqxgm_batcher_flush(emqxgm_batcher_t* b, uint64_t* window);
+/* Completes window `window` (flushed, not yet collected; the oldest first is cheapest) and
+ * returns its result. */
+int emqxgm_batcher_collect(emqxgm_batcher_t* b, uint64_t window, emqxgm_window_out* out);
 
 /* ---- filter-sharded layout over several GPUs (the subscription set partitioned by
  * filter, the topic batch broadcast, the per-GPU match lists gathered to one GPU) ----
@@ -347,7 +403,9 @@ int emqxgm_set_profiling(emqxgm_t* h, int on);
  * "exact_range_kb" (0 default: one route-key probe pass over the whole table; > 0: the probe
  * runs in passes over bucket ranges of that many KiB, so that the lines in flight share page
  * translations -- measured slower on a 100M-key table, kept as an option); "delta_commit": 0 = every commit rebuilds the index, 1 = small deltas are patched in place
- * (default), 2 = every delta that fits the tables' load bounds is patched in place. */
+ * (default), 2 = every delta that fits the tables' load bounds is patched in place;
+ * "fat_buckets": 1 (default) = single-literal-child nodes keep their child in their own bucket
+ * line, 0 = none (A/B runs), from the next full build on (the next commit). */
 int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value);
 int emqxgm_get_stats(emqxgm_t* h, emqxgm_stats* st);
 /* Last HIP error string seen by the handle (for diagnostics). */

@@ -670,6 +670,37 @@ class Retainer:
         self.index.clear()
 
 
+def retained_match_indexed(filt: bytes, topics: Iterable[bytes],
+                           index_specs: Sequence[Sequence[int]]) -> List[bytes]:
+    """The set ``Retainer(index_specs).match_messages`` selects (expiry aside), as a predicate
+    over the stored topics, derived from select_index/2 and condition/2
+    (emqx_retainer_index.erl:83-91, 141-200) and checked against ``Retainer.search_table`` by
+    tests/test_oracle_golden.py: with no index scoring > 0 the full scan; on the index path a
+    first '#' (any position) makes the words before it a prefix with any tail, and a filter that
+    ends while index positions remain selects topics up to the run of index positions right
+    after its last word longer (any words there)."""
+    toks = words(filt)
+    ix = retainer_select_index(toks, sorted(list(s) for s in index_specs))
+    if ix is None:
+        return retained_match(filt, topics)
+    rest = list(ix)
+    for n, w in enumerate(toks, 1):
+        if w == HASH:  # condition/5 :174-177, before the index is used up or right at it
+            pre = toks[:n - 1]
+            return [t for t in topics if len(words(t)) >= len(pre) and all(
+                f == PLUS or f == x for f, x in zip(pre, words(t)))]
+        if not rest:  # :178-179: the rest through condition/1, i.e. the full scan's pattern
+            return retained_match(filt, topics)
+        if rest[0] == n:
+            rest = rest[1:]
+    k, tail = len(toks), 0
+    for p in rest:
+        if p == k + 1 + tail:
+            tail += 1
+    return [t for t in topics if k <= len(words(t)) <= k + tail and all(
+        f == PLUS or f == w for f, w in zip(toks, words(t)))]
+
+
 def retained_match(filt: bytes, topics: Iterable[bytes]) -> List[bytes]:
     """The set match_messages selects, as a predicate: the topics whose word lists the
     condition/1 pattern of ``filt`` matches (``+`` any one word, a last ``#`` any tail, the

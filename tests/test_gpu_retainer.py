@@ -1,6 +1,7 @@
 """GPU parity of the retained-topic store (emqxgm_retain_*) against the
-oracle's emqx_retainer_mnesia restatement (oracle/emqx_ref.py Retainer, full-scan search_table,
-index_specs = []), itself pinned to the retainer suites (tests/test_oracle_golden.py)."""
+oracle's emqx_retainer_mnesia restatement (oracle/emqx_ref.py Retainer: search_table/3 with the
+reference's default index specs -- the index path -- and with index_specs = [], the full scan),
+itself pinned to the retainer suites (tests/test_oracle_golden.py)."""
 import random
 
 import pytest
@@ -26,9 +27,13 @@ def _wkey(t):
     return tuple(t.split(b"/"))
 
 
-def test_retainer_suite_cases_on_device(emqx, golden):
+DEFAULT = [[1, 2, 3], [1, 3], [2, 3], [3]]  # emqx_retainer_schema.erl:24-29
+
+
+@pytest.mark.parametrize("specs", [DEFAULT, []])
+def test_retainer_suite_cases_on_device(emqx, golden, specs):
     for case, steps in golden["retainer_cases"].items():
-        r = emqx.Retainer()
+        r = emqx.Retainer(index_specs=specs)
         for st in steps:
             if st[0] == "store":
                 r.store_retained(B(st[1]), st[2])
@@ -43,8 +48,27 @@ def test_retainer_suite_cases_on_device(emqx, golden):
         r.close()
 
 
+def test_retainer_index_path_quirk_on_device(emqx):
+    """The default index specs' open index tail (emqx_retainer_index.erl:180-181): 'a/+' also
+    selects 'a/x/y', 'a' selects 'a/x' and 'a/x/y'; a '#' not last cuts the filter there."""
+    r, q = emqx.Retainer(), R.Retainer(DEFAULT)
+    topics = [b"a", b"a/x", b"a/x/y", b"a/x/y/z", b"b/x", b"b/x/y", b"x/b/c"]
+    for t in topics:
+        r.store_retained(t)
+        q.store_retained(t)
+    cases = {b"a/+": [b"a/x", b"a/x/y"], b"a": [b"a", b"a/x", b"a/x/y"],
+             b"a/#/c": [b"a", b"a/x", b"a/x/y", b"a/x/y/z"], b"+/x": [b"a/x", b"b/x"],
+             b"+/b": [b"x/b/c"], b"#": sorted(topics, key=_wkey)}
+    got = r.match_messages_batch(list(cases), 1)
+    for (f, exp), g in zip(cases.items(), got):
+        assert sorted(q.match_messages(f, 1), key=_wkey) == exp, f  # hand list == oracle
+        assert sorted(g, key=_wkey) == exp, (f, g)
+    r.set_index_specs([])  # the full scan: exactly condition/1's set
+    assert r.match_messages(b"a/+", 1) == [b"a/x"] and r.match_messages(b"a/#/c", 1) == []
+
+
 def test_retainer_edges(emqx):
-    r = emqx.Retainer()
+    r = emqx.Retainer(index_specs=[])
     assert r.match_messages(b"#", 1) == []  # empty store
     topics = [b"a", b"a/b", b"a/b/c", b"a//c", b"/", b"", b"$SYS/x", b"$SYS", b"b/a",
               b"long-level-word/x", b"long-level-wordy/x", b"a/b/c/d/e/f/g/h/i/j/k/l/m/n/o/p/q"]
@@ -69,17 +93,28 @@ def test_retainer_edges(emqx):
     for (f, exp), g in zip(cases.items(), got):
         assert exp == sorted(R.retained_match(f, topics), key=_wkey), f  # hand list == oracle
         assert g == exp, (f, g)
+    # the same edges on the index path of the default specs
+    r.set_index_specs(DEFAULT)
+    q = R.Retainer(DEFAULT)
+    for t in topics:
+        q.store_retained(t)
+    got = r.match_messages_batch(list(cases), 1)
+    for f, g in zip(cases, got):
+        assert sorted(g, key=_wkey) == sorted(q.match_messages(f, 1), key=_wkey), (f, g)
     assert r.size() == len(topics)
     assert r.read_message(b"a/b", 1) == [b"a/b"] and r.read_message(b"a/x", 1) == []
 
 
-@pytest.mark.parametrize("seed,dmax", [(1, -1), (2, -1), (3, 0), (4, 10**9)])
-def test_retainer_random_vs_oracle(emqx, seed, dmax):
+@pytest.mark.parametrize("seed,dmax,specs", [(1, -1, DEFAULT), (2, -1, []), (3, 0, DEFAULT),
+                                             (4, 10**9, DEFAULT), (5, -1, [[2], [1, 3, 4]]),
+                                             (6, 10**9, [])])
+def test_retainer_random_vs_oracle(emqx, seed, dmax, specs):
     """dmax: delta topics before a base rebuild (0: rebuild at every commit; 10**9: the base
-    is only ever patched -- deletions and re-stores -- and new topics live in the delta)."""
+    is only ever patched -- deletions and re-stores -- and new topics live in the delta);
+    specs: the index specs (the wildcard delete selects by them too, :166-180)."""
     rng = random.Random(seed)
     vocab = [b"a", b"b", b"", b"$s", b"cc", b"long-word-%d" % seed, b"long-word-x"]
-    ref, dev = R.Retainer(), emqx.Retainer()
+    ref, dev = R.Retainer(specs), emqx.Retainer(index_specs=specs)
     dev.tune("delta_max", dmax)
     big = dmax == 10**9
     for step in range(6):
@@ -120,17 +155,19 @@ def test_retainer_random_vs_oracle(emqx, seed, dmax):
     dev.close()
 
 
-def test_retainer_cfg3_scale(emqx):
-    """200k cfg3 topics; a sample of subscription-shaped filters against the predicate form."""
+@pytest.mark.parametrize("specs", [DEFAULT, []])
+def test_retainer_cfg3_scale(emqx, specs):
+    """200k cfg3 topics; a sample of subscription-shaped filters against the predicate forms
+    (R.retained_match_indexed is checked against the restated search_table on the CPU)."""
     import workloads
     w = workloads.generate(3, 2000, 200_000)
     topics = [w.topic(i) for i in range(w.nt)]
-    r = emqx.Retainer()
+    r = emqx.Retainer(index_specs=specs)
     for t in topics:
         r.store_retained(t)
     uniq = sorted(set(topics), key=_wkey)
     filters = [w.filter(i) for i in range(0, w.nf, 100)] + [b"site/+/device/+/m1/#", b"#"]
     got = r.match_messages_batch(filters, 1)
     for f, g in zip(filters, got):
-        assert g == sorted(R.retained_match(f, uniq), key=_wkey), f
+        assert sorted(g, key=_wkey) == sorted(R.retained_match_indexed(f, uniq, specs), key=_wkey), f
     assert r.size() == len(uniq)

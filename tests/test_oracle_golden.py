@@ -301,7 +301,7 @@ def test_retainer_index_path_quirk():
     the index's last position (condition/2's `[_|_], []` clause leaves the index part open,
     emqx_retainer_index.erl:180-181): with the default specs (emqx_retainer_schema.erl:24-29)
     'a/+' also selects 'a/x/y'.  The scan path (index_specs = []) selects exactly condition/1's
-    set; the engine implements that set."""
+    set; the engine implements both, the index path by default."""
     default = [[1, 2, 3], [1, 3], [2, 3], [3]]
     q, plain = R.Retainer(default), R.Retainer()
     for t in (b"a/x", b"a/x/y", b"b/x"):
@@ -332,3 +332,23 @@ def test_retainer_index_path_covers_scan():
         assert set(a) <= set(indexed.match_messages(f, 100)), f
         live = [t for t in topics if plain.msgs[tuple(R.words(t))] in (0, 150)]
         assert a == sorted(R.retained_match(f, live)), f
+
+
+@pytest.mark.parametrize("specs", [[[1, 2, 3], [1, 3], [2, 3], [3]], [[1, 2], [2, 3], [1, 3, 4]],
+                                   [[2]], [[1, 2, 3, 4, 5]]])
+def test_retainer_indexed_predicate_equals_search_table(specs):
+    """The predicate form of the index path (R.retained_match_indexed, the set the engine's
+    filter plan reproduces: a cut after the first '#', an open index tail) equals the index
+    search of the restated emqx_retainer_mnesia (Retainer.search_table) -- including filters
+    with '#' not last and filters shorter than the index."""
+    rng = random.Random(len(specs))
+    vocab = [b"a", b"b", b"", b"$s", b"cc"]
+    topics = {b"/".join(rng.choice(vocab) for _ in range(rng.randint(1, 6))) for _ in range(500)}
+    r = R.Retainer(specs)
+    for t in topics:
+        r.store_retained(t, 0)
+    for _ in range(400):
+        d = rng.randint(1, 6)
+        ws = [rng.choice([b"+", b"+", b"a", b"b", b"", b"#"]) for _ in range(d)]
+        f = b"/".join(ws)
+        assert sorted(r.match_messages(f, 1)) == sorted(R.retained_match_indexed(f, topics, specs)), f
