@@ -64,6 +64,9 @@ def main():
                     help="N>1: skip the filter-sharded measurement beside the replicas")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-in/host-out timing")
+    ap.add_argument("--windows", default="16384,65536,262144,1048576",
+                    help="NIF batcher window sizes (topics) for the operating-point sweep "
+                         "('' = skip); rank 0, N=1, with the host-in/host-out timing")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-pipeline", action="store_true",
@@ -299,6 +302,11 @@ def main():
                                       "ms_per_batch": round(best * 1e3, 3),
                                       "api": "emqxgm_match_batch (u64 row pointers)"}}
 
+    windows = None
+    if rank == 0 and world == 1 and not args.no_e2e and args.windows:
+        from emqx_amd.engine import Batcher
+        windows = _window_sweep(Batcher, eng, w, [int(x) for x in args.windows.split(",")])
+
     if rank == 0:
         line = {
             "metric": ("published topics matched/sec at 10M filters" if args.cfg == 3
@@ -344,6 +352,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "end_to_end": e2e,
+            "nif_windows": windows,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -375,6 +384,60 @@ def _build_engine(Engine, w, idx, args, local):
     gid[tid] = idx[wsel]
     eng.commit()
     return eng, gid
+
+
+def _window_sweep(Batcher, eng, w, sizes):
+    """The NIF's operating point (a batcher in front of emqx_trie:match/1): batch 0's
+    topics streamed through an emqxgm_batcher of each window size -- packed into pinned windows
+    (emqxgm_batcher_add_many), flushed, the oldest window collected whenever EMQXGM_HOST_PIPES
+    are in flight (H2D, the device pass, results to pinned host memory, every pair's filter
+    bytes copied into the window's arena).  Host-in/host-out topics/s and the flush -> collected
+    latency per window (p50 / p99).  The driver loop is Python (one add_many / flush / collect
+    call per window, ~tens of us), as a NIF batcher process would make the same three calls."""
+    off = w.toff.astype(np.int64)
+    out = {}
+    for W in sizes:
+        W = min(W, w.nt)
+        b = Batcher(eng, window_topics=W, window_bytes=64 * W)
+        inflight, lat = [], []
+        state = {"pos": 0, "done": 0}
+
+        def collect():
+            r = b.collect(inflight.pop(0))
+            lat.append(r.latency_ns)
+            state["done"] += len(r.tag)
+
+        def run(total):
+            added = 0
+            while added < total:
+                i = state["pos"] % w.nt
+                j = min(i + W, w.nt)
+                sub = (off[i:j + 1] - off[i]).astype(np.uint32)
+                k = b.add_many(w.tbytes[off[i]:off[j]], sub, i)
+                state["pos"] += k
+                added += k
+                if len(inflight) == eng.HOST_PIPES:
+                    collect()
+                inflight.append(b.flush())
+            while inflight:
+                collect()
+        run(min(4 * W, 1 << 21))  # warm-up: pinned buffers and the engine's scratch at size
+        lat.clear()
+        state["done"] = 0
+        total = max(20 * W, 2_000_000)
+        t0 = time.perf_counter()
+        run(total)
+        el = time.perf_counter() - t0
+        b.close()
+        la = np.array(lat, np.float64) / 1e3
+        out[str(W)] = {"topics_per_s": round(state["done"] / el, 1), "windows": len(lat),
+                       "latency_us_p50": round(float(np.percentile(la, 50)), 1),
+                       "latency_us_p99": round(float(np.percentile(la, 99)), 1)}
+    out["includes"] = ("topics packed into pinned windows, H2D, the device pass, row pointers + "
+                       "filter ids + exact ids to pinned host memory, each pair's filter bytes "
+                       "copied into the window's arena (emqxgm_batcher_*), 3 windows in flight; "
+                       "latency = flush -> collected")
+    return out
 
 
 def _census_mean(eng, dbat, nt):

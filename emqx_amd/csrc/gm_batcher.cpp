@@ -116,6 +116,26 @@ int emqxgm_batcher_add(emqxgm_batcher_t* b, const uint8_t* topic, uint32_t len, 
   return (w.n == b->cfg.window_topics || w.off[w.n] == b->cfg.window_bytes) ? 1 : 0;
 }
 
+int emqxgm_batcher_add_many(emqxgm_batcher_t* b, const uint8_t* bytes, const uint32_t* offsets,
+                            uint32_t n, uint64_t tag0) {
+  if (!b || (n && (!offsets || (!bytes && offsets[n] != offsets[0])))) return -EINVAL;
+  std::lock_guard<std::mutex> g(b->mu);
+  Window& w = b->w[b->open];
+  uint32_t k = 0;
+  for (; k < n; ++k) {
+    if (offsets[k + 1] < offsets[k]) return k ? (int)k : -EINVAL;
+    const uint32_t len = offsets[k + 1] - offsets[k], used = w.off[w.n];
+    if (len > b->cfg.window_bytes) return k ? (int)k : -E2BIG;
+    if (w.n >= b->cfg.window_topics || len > b->cfg.window_bytes - used) break;
+    if (w.n == 0) w.first_ns = mono_ns();
+    if (len) memcpy(w.bytes + used, bytes + offsets[k], len);
+    w.off[w.n + 1] = used + len;
+    w.tag.push_back(tag0 + k);
+    w.n += 1;
+  }
+  return (int)k;
+}
+
 int emqxgm_batcher_due(emqxgm_batcher_t* b, uint64_t now_ns) {
   if (!b) return -EINVAL;
   std::lock_guard<std::mutex> g(b->mu);

@@ -147,6 +147,7 @@ SYMBOLS = {
     "emqxgm_batcher_destroy": (None, [_P]),
     "emqxgm_batcher_add": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint64, _U32P]),
     "emqxgm_batcher_due": (C.c_int, [_P, C.c_uint64]),
+    "emqxgm_batcher_add_many": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64]),
     "emqxgm_batcher_flush": (C.c_int, [_P, _U64P]),
     "emqxgm_batcher_collect": (C.c_int, [_P, C.c_uint64, C.POINTER(_WindowOut)]),
     "emqxgm_set_profiling": (C.c_int, [_P, C.c_int]),
@@ -589,6 +590,14 @@ class Batcher:
         s = C.c_uint32()
         return bool(self._eng._check(self._lib.emqxgm_batcher_add(self._b, topic, len(topic), tag,
                                                                   C.byref(s)), "batcher_add"))
+
+    def add_many(self, buf: np.ndarray, off: np.ndarray, tag0: int = 0) -> int:
+        """Appends packed topics (uint8 bytes, uint32 offsets[n+1]) until the window is full;
+        how many were added."""
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        return self._eng._check(self._lib.emqxgm_batcher_add_many(
+            self._b, _ptr(np.ascontiguousarray(buf, dtype=np.uint8)), _ptr(off), len(off) - 1,
+            tag0), "batcher_add_many")
 
     def due(self, now_ns: int) -> bool:
         return bool(self._eng._check(self._lib.emqxgm_batcher_due(self._b, now_ns), "batcher_due"))

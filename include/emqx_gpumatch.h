@@ -360,6 +360,11 @@ void emqxgm_batcher_destroy(emqxgm_batcher_t* b);
  * -ENOSPC when the open window is full, -EINVAL. */
 int emqxgm_batcher_add(emqxgm_batcher_t* b, const uint8_t* topic, uint32_t len, uint64_t tag,
                        uint32_t* slot);
+/* Appends topics bytes[offsets[i] .. offsets[i+1]) for i in [0, n) (tag tag0 + i) until the
+ * open window is full; returns how many were added (>= 0), or -EINVAL / -E2BIG as _add.  A
+ * batcher process that drains several callers at once packs them with one call. */
+int emqxgm_batcher_add_many(emqxgm_batcher_t* b, const uint8_t* bytes, const uint32_t* offsets,
+                            uint32_t n, uint64_t tag0);
 /* 1 when the open window holds topics and its first one was added window_us or more before
  * now_ns (CLOCK_MONOTONIC), else 0. */
 int emqxgm_batcher_due(emqxgm_batcher_t* b, uint64_t now_ns);
