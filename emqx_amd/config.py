@@ -1,0 +1,83 @@
+"""``broker.perf.gpu_match`` -- the configuration surface of the device match path, beside the
+reference's ``broker.perf.route_lock_type`` / ``trie_compaction`` (apps/emqx/src/emqx_schema.erl:
+1259-1273; SURVEY 5 "Config / flags"), and how each field reaches the engine.  The same table as
+``src/emqx_trie_gpu_schema.erl`` (the HOCON fields a maintainer adds to ``fields("broker_perf")``):
+
+============== ======================= ==========================================================
+field          default                 engine
+============== ======================= ==========================================================
+enable         false                   the device answers ``emqx_trie:match/1`` at all
+devices        [0]                     ``emqxgm_cfg.device`` (the first; one index per node)
+batch_max      65536                   ``emqxgm_cfg.batch_max`` = ``emqxgm_batcher_cfg.window_topics``
+                                       (``window_bytes`` = 64 x batch_max)
+batch_window_us 50                     ``emqxgm_batcher_cfg.window_us``
+max_levels     128                     deeper topics take the reference's ``emqx_trie:match/1``
+                                       (``mqtt.max_topic_levels``, emqx_schema.erl:405-412)
+delta_commit   small                   ``emqxgm_tune("delta_commit", never 0 / small 1 / always 2)``
+============== ======================= ==========================================================
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Mapping
+
+DELTA_COMMIT = {"never": 0, "small": 1, "always": 2}
+
+
+@dataclass(frozen=True)
+class GpuMatchConfig:
+    enable: bool = False
+    devices: List[int] = field(default_factory=lambda: [0])
+    batch_max: int = 65536
+    batch_window_us: int = 50
+    max_levels: int = 128
+    delta_commit: str = "small"
+
+    @classmethod
+    def from_map(cls, conf: Mapping) -> "GpuMatchConfig":
+        """A ``broker.perf.gpu_match`` map (HOCON keys) -> a checked config; ValueError on a
+        value the schema's ranges reject (emqx_trie_gpu_schema.erl)."""
+        known = {f for f in cls.__dataclass_fields__}
+        extra = set(conf) - known
+        if extra:
+            raise ValueError(f"unknown broker.perf.gpu_match fields: {sorted(extra)}")
+        c = cls(**{k: (list(v) if k == "devices" else v) for k, v in conf.items()})
+        c.check()
+        return c
+
+    def check(self) -> None:
+        def rng(name, v, lo, hi):
+            if not isinstance(v, int) or isinstance(v, bool) or not lo <= v <= hi:
+                raise ValueError(f"broker.perf.gpu_match.{name} = {v!r}: expected {lo}..{hi}")
+        if not isinstance(self.enable, bool):
+            raise ValueError("broker.perf.gpu_match.enable: expected a boolean")
+        if not self.devices:
+            raise ValueError("broker.perf.gpu_match.devices: at least one device")
+        for d in self.devices:
+            rng("devices[]", d, 0, 1023)
+        rng("batch_max", self.batch_max, 1, 4 << 20)
+        rng("batch_window_us", self.batch_window_us, 1, 1_000_000)
+        rng("max_levels", self.max_levels, 1, 65535)
+        if self.delta_commit not in DELTA_COMMIT:
+            raise ValueError(f"broker.perf.gpu_match.delta_commit: one of {sorted(DELTA_COMMIT)}")
+
+    def engine_kwargs(self) -> Dict[str, int]:
+        """``emqxgm_cfg`` fields (emqx_amd.Engine keywords)."""
+        return {"device": self.devices[0], "batch_max": self.batch_max}
+
+    def batcher_kwargs(self) -> Dict[str, int]:
+        """``emqxgm_batcher_cfg`` fields (emqx_amd.Batcher keywords)."""
+        return {"window_topics": self.batch_max, "window_bytes": 64 * self.batch_max,
+                "window_us": self.batch_window_us}
+
+    def tunes(self) -> Dict[str, int]:
+        """``emqxgm_tune`` knobs."""
+        return {"delta_commit": DELTA_COMMIT[self.delta_commit]}
+
+    def open(self):
+        """An Engine and its Batcher as the NIF's open/4 makes them (emqx_trie_gpu:start_link)."""
+        from .engine import Batcher, Engine
+        eng = Engine(**self.engine_kwargs())
+        for k, v in self.tunes().items():
+            eng.tune(k, v)
+        return eng, Batcher(eng, **self.batcher_kwargs())

@@ -29,6 +29,7 @@
 #include "../../include/emqx_gpumatch.h"
 #include "gm_common.h"
 #include "gm_kernels.h"
+#include "gm_roctx.h"
 
 using namespace gm;
 
@@ -488,6 +489,7 @@ struct emqxgm {
   hipEvent_t patch_ev = nullptr;    // the last patch upload + launch
   uint32_t delta_mode = 1;        // 0: always rebuild, 1: delta when small, 2: delta if possible
   uint32_t fat_mode = 1;          // 1: fat buckets at full builds (gm_common.h FAT_ID), 0: none
+  bool roctx = false;             // roctx ranges / launch markers (gm_roctx.h)
 };
 
 namespace {
@@ -1430,6 +1432,7 @@ void sweep_graveyard(emqxgm* h) {
 // Runs under wmu only: readers keep matching against the current epoch while a full build runs.
 int commit_locked(emqxgm* h) {
   const auto t0 = std::chrono::steady_clock::now();
+  RoctxRange rr(h->roctx, "emqxgm.commit");
   sweep_graveyard(h);
   h->patches.clear();
   int rc = patch_wait(h);  // the previous commit's patches are applied before buffers change
@@ -1603,13 +1606,16 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
   // the epoch's uploads / patches must have landed (a full build's have: its wait is skipped)
   if (hipEventQuery(E.ready) != hipSuccess) HIPCHK(h, hipStreamWaitEvent(st, E.ready, 0));
   if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[0], st));
+  RoctxRange rr(h->roctx, census ? "emqxgm.pass.census" : "emqxgm.pass");
   HIPCHK(h, hipMemsetAsync(s.ctl, 0, CTL_N * 4, st));
   if (census)
     HIPCHK(h, hipMemsetAsync(s.census, 0,
                              (CENSUS_HDR + 3 * (h->geom.lanes / 64)) * sizeof(unsigned long long),
                              st));
+  roctx_mark(h->roctx, "k_tok");
   HIPCHK(h, launch_tok(d_bytes, d_off, n, ix, s, st));
   if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[4], st));
+  roctx_mark(h->roctx, "k_exact");
   HIPCHK(h, launch_exact(d_bytes, d_off, n, ix, s, h->geom, st));
   if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[1], st));
   if (ix.trie_empty) {
@@ -1619,12 +1625,16 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
     if (ix.needs_verify || legacy) HIPCHK(h, hipMemsetAsync(s.rej, 0, (size_t)n * 4, st));
     c.census = census;
     c.walk_level = (census ? E.census_level : E.walk_level).load(std::memory_order_relaxed);
+    roctx_mark(h->roctx, "k_walk");
     HIPCHK(h, launch_walk(ix, s, n, h->geom, st, census ? s.census : nullptr, c.walk_level));
     if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[2], st));
     if (!legacy) {
       // pairs of filters made of short (exact) tokens need no byte check (gm_verify.inc)
+      roctx_mark(h->roctx && ix.needs_verify, "k_verify");
       if (ix.needs_verify) HIPCHK(h, launch_verify(d_bytes, d_off, ix, s, n, h->geom, st));
+      roctx_mark(h->roctx, "k_scan");
       HIPCHK(h, launch_scan(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, st));
+      roctx_mark(h->roctx, "k_scatter");
       HIPCHK(h, launch_scatter(s, n, h->geom, st));
     } else {
       HIPCHK(h, launch_scan(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, st));
@@ -2066,6 +2076,7 @@ int emqxgm_create(const emqxgm_cfg* cfg, emqxgm_t** out) {
   if (h->cfg.full_hash_bits == 0 || h->cfg.full_hash_bits > 64) h->cfg.full_hash_bits = 64;
   if (h->cfg.batch_max == 0) h->cfg.batch_max = 4u << 20;
   if (h->cfg.reject_cap) h->reject_cap = h->cfg.reject_cap;
+  if (const char* e = getenv("EMQXGM_ROCTX")) h->roctx = e[0] == '1';
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || h->cfg.device < 0 ||
       h->cfg.device >= ndev) {
@@ -2755,6 +2766,7 @@ int emqxgm_match_device_submit(emqxgm_t* h, const uint8_t* d_bytes, const uint32
 int emqxgm_match_device_wait(emqxgm_t* h, uint64_t ticket, emqxgm_dev_out* out) {
   if (!h || !out) return -EINVAL;
   std::lock_guard<std::mutex> g(h->mmu);
+  RoctxRange rr(h->roctx, "emqxgm.wait");
   if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
   emqxgm::Pipe& p = h->pipes[ticket % EMQXGM_PIPES];
   if (ticket == 0 || p.ticket != ticket || p.state == 0) {
@@ -2827,6 +2839,7 @@ int emqxgm_match_batch_submit(emqxgm_t* h, const uint8_t* bytes, const uint32_t*
 int emqxgm_match_batch_wait(emqxgm_t* h, uint64_t ticket, emqxgm_batch_out* out) {
   if (!h || !out) return -EINVAL;
   std::lock_guard<std::mutex> g(h->mmu);
+  RoctxRange rr(h->roctx, "emqxgm.host_wait");
   if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
   emqxgm::HostPipe& p = h->hpipes[ticket % EMQXGM_HOST_PIPES];
   if (ticket == 0 || p.ticket != ticket || p.state == 0) {
@@ -3150,6 +3163,11 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
     if (value < 0 || value > 2) return -EINVAL;
     std::lock_guard<std::mutex> g(h->wmu);
     h->delta_mode = (uint32_t)value;
+    return 0;
+  }
+  if (strcmp(key, "roctx") == 0) {  // 1: roctx ranges / launch markers (gm_roctx.h)
+    if (value < 0 || value > 1) return -EINVAL;
+    h->roctx = value != 0;
     return 0;
   }
   if (strcmp(key, "fat_buckets") == 0) {  // 1 (default) / 0: from the next full build on

@@ -410,7 +410,9 @@ int emqxgm_set_profiling(emqxgm_t* h, int on);
  * translations -- measured slower on a 100M-key table, kept as an option); "delta_commit": 0 = every commit rebuilds the index, 1 = small deltas are patched in place
  * (default), 2 = every delta that fits the tables' load bounds is patched in place;
  * "fat_buckets": 1 (default) = single-literal-child nodes keep their child in their own bucket
- * line, 0 = none (A/B runs), from the next full build on (the next commit). */
+ * line, 0 = none (A/B runs), from the next full build on (the next commit);
+ * "roctx": 1 = roctx ranges around passes, waits and commits and a marker at each kernel launch
+ * (rocprofv3 --marker-trace; also EMQXGM_ROCTX=1 at create), 0 (default) = none. */
 int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value);
 int emqxgm_get_stats(emqxgm_t* h, emqxgm_stats* st);
 /* Last HIP error string seen by the handle (for diagnostics). */
