@@ -57,7 +57,8 @@ def test_retainer_index_path_quirk_on_device(emqx):
         r.store_retained(t)
         q.store_retained(t)
     cases = {b"a/+": [b"a/x", b"a/x/y"], b"a": [b"a", b"a/x", b"a/x/y"],
-             b"a/#/c": [b"a", b"a/x", b"a/x/y", b"a/x/y/z"], b"+/x": [b"a/x", b"b/x"],
+             b"a/#/c": [b"a", b"a/x", b"a/x/y", b"a/x/y/z"],
+             b"+/x": [b"a/x", b"a/x/y", b"b/x", b"b/x/y"],  # [2,3]: a tail of one
              b"+/b": [b"x/b/c"], b"#": sorted(topics, key=_wkey)}
     got = r.match_messages_batch(list(cases), 1)
     for (f, exp), g in zip(cases.items(), got):
