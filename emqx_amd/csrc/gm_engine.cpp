@@ -464,6 +464,11 @@ struct emqxgm {
     uint64_t row_cap = 0, fid_cap = 0;  // entries
     uint32_t n = 0, pairs = 0;
     uint64_t bytes_len = 0;
+    // emqxgm_match_batch_wait_filters: the pairs' filter bytes gathered on the device
+    // ([len | off | scan | total] words, then bytes) and copied into pinned memory
+    DevBuf d_fb;
+    Pinned h_fboff, h_fb;
+    uint64_t fb_bytes = 0;
   } hpipes[EMQXGM_HOST_PIPES];
   uint64_t next_hticket = 1;
   hipStream_t pipe_streams[EMQXGM_HOST_PIPES] = {};  // pipe_stream(): shared by both pipe kinds
@@ -1992,7 +1997,44 @@ int host_pipe_copy_out(emqxgm* h, emqxgm::HostPipe& p) {
 
 // Completes an in-flight host pipe: checks the pass (redoing it synchronously when it has to be)
 // and makes sure every result array is in its pinned buffer.
-int host_pipe_complete(emqxgm* h, emqxgm::HostPipe& p) {
+int grow_dev(emqxgm* h, DevBuf& b, uint64_t bytes, hipStream_t s);
+
+// The pairs' filter bytes of a completed pass (its epoch still held: the device string pool
+// the gather reads is the epoch's), into the pipe's pinned buffers.
+int host_pipe_gather(emqxgm* h, emqxgm::HostPipe& p) {
+  const Scratch& s = p.c.sc;
+  const DevIndex& ix = p.c.epoch->ix;
+  const uint32_t m = p.pairs;
+  const uint64_t tw = scan_tmp_words(std::max<uint32_t>(m, 1));
+  const uint64_t words = 2ull * m + 1 + tw + 2;
+  int rc = grow_dev(h, p.d_fb, words * 4, p.c.stream);
+  if (rc) return rc;
+  uint32_t* len = (uint32_t*)p.d_fb.p;
+  uint32_t* ooff = len + m;
+  uint32_t* total = ooff + m + 1;
+  uint32_t* tmp = total + 2;
+  HIPCHK(h, launch_filter_len(s.out, m, ix.foff, len, ooff, tmp, total, p.c.stream));
+  uint32_t nb = 0;
+  HIPCHK(h, hipMemcpyAsync(&nb, total, 4, hipMemcpyDeviceToHost, p.c.stream));
+  HIPCHK(h, hipStreamSynchronize(p.c.stream));
+  if (m == 0) nb = 0;
+  const uint64_t at = ((words * 4 + 255) / 256) * 256;  // the bytes after the words
+  if ((rc = grow_dev(h, p.d_fb, at + nb + 1, p.c.stream)) ||
+      (rc = pinned_reserve(h, p.h_fboff, ((size_t)m + 1) * 4, false)) ||
+      (rc = pinned_reserve(h, p.h_fb, (size_t)nb + 1, false)))
+    return rc;
+  len = (uint32_t*)p.d_fb.p;  // (grown: re-derive; the scan results were kept by grow_dev)
+  ooff = len + m;
+  uint8_t* out = (uint8_t*)p.d_fb.p + at;
+  HIPCHK(h, launch_filter_gather(s.out, m, ix.foff, ix.fbytes, ooff, out, p.c.stream));
+  HIPCHK(h, hipMemcpyAsync(p.h_fboff.p, ooff, ((size_t)m + 1) * 4, hipMemcpyDeviceToHost, p.c.stream));
+  if (nb) HIPCHK(h, hipMemcpyAsync(p.h_fb.p, out, nb, hipMemcpyDeviceToHost, p.c.stream));
+  HIPCHK(h, hipStreamSynchronize(p.c.stream));
+  p.fb_bytes = nb;
+  return 0;
+}
+
+int host_pipe_complete(emqxgm* h, emqxgm::HostPipe& p, bool gather = false) {
   if (p.state != 1) return 0;
   HIPCHK(h, hipStreamSynchronize(p.c.stream));
   bool legacy = false;
@@ -2006,6 +2048,7 @@ int host_pipe_complete(emqxgm* h, emqxgm::HostPipe& p) {
     rc = run_device(h, p.c, p.d_bytes, p.d_off, p.n, p.bytes_len, &p.pairs);
     rows_copied = false;
   }
+  if (rc == 0 && gather) rc = host_pipe_gather(h, p);
   p.c.epoch.reset();
   if (rc < 0) {
     p.state = 0;
@@ -2040,8 +2083,27 @@ int host_pipe_complete(emqxgm* h, emqxgm::HostPipe& p) {
   return 0;
 }
 
+// A device buffer of at least `bytes`, its contents kept (stream-ordered on s).
+int grow_dev(emqxgm* h, DevBuf& b, uint64_t bytes, hipStream_t s) {
+  if (bytes <= b.bytes && b.p) return 0;
+  const uint64_t cap = std::max<uint64_t>(bytes + bytes / 4, 1 << 20);
+  void* p = nullptr;
+  HIPCHK(h, hipMalloc(&p, cap));
+  if (b.p) {
+    HIPCHK(h, hipMemcpyAsync(p, b.p, b.bytes, hipMemcpyDeviceToDevice, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    (void)hipFree(b.p);
+  }
+  b.p = p;
+  b.bytes = cap;
+  return 0;
+}
+
 void host_pipe_free(emqxgm::HostPipe& p) {
   ctx_free(p.c);
+  if (p.d_fb.p) (void)hipFree(p.d_fb.p);
+  for (void* q : {p.h_fboff.p, p.h_fb.p})
+    if (q) (void)hipHostFree(q);
   if (p.d_bytes) (void)hipFree(p.d_bytes);
   if (p.d_off) (void)hipFree(p.d_off);
   for (uint32_t* q : {p.h_row, p.h_exact, p.h_fid})
@@ -2857,6 +2919,33 @@ int emqxgm_match_batch_wait(emqxgm_t* h, uint64_t ticket, emqxgm_batch_out* out)
   return 0;
 }
 
+int emqxgm_match_batch_wait_filters(emqxgm_t* h, uint64_t ticket, emqxgm_batch_out* out,
+                                    const uint32_t** foff, const uint8_t** fbytes) {
+  if (!h || !out || !foff || !fbytes) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mmu);
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
+  RoctxRange rr(h->roctx, "emqxgm.host_wait_filters");
+  emqxgm::HostPipe& p = h->hpipes[ticket % EMQXGM_HOST_PIPES];
+  if (ticket == 0 || p.ticket != ticket || p.state == 0) {
+    set_err(h, "unknown ticket, or its result was already taken / overwritten");
+    return -ENOENT;
+  }
+  const bool empty = p.state == 2;  // an empty batch: no pass ran
+  int rc = host_pipe_complete(h, p, true);
+  if (rc || (rc = pinned_reserve(h, p.h_fboff, 4, true)) || (rc = pinned_reserve(h, p.h_fb, 1, true)))
+    return rc;
+  if (empty) ((uint32_t*)p.h_fboff.p)[0] = 0;
+  p.state = 0;
+  out->n = p.n;
+  out->n_pairs = p.pairs;
+  out->row_ptr = p.h_row;
+  out->filter_id = p.h_fid;
+  out->exact_id = p.exact_none ? p.h_none : p.h_exact;
+  *foff = (const uint32_t*)p.h_fboff.p;
+  *fbytes = (const uint8_t*)p.h_fb.p;
+  return 0;
+}
+
 int emqxgm_match_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets, uint32_t n,
                        emqxgm_out* out) {
   if (!h || !out || (!offsets && n)) return -EINVAL;
@@ -3041,6 +3130,62 @@ int emqxgm_merge(emqxgm_t* h, uint32_t parts, const uint32_t* const* rows,
   uint32_t* cnt = (uint32_t*)(d + (3ull * parts + 1) * 8);
   uint32_t* total = cnt + n;
   uint32_t* tmp = total + 2;
+  if (parts) HIPCHK(h, hipMemcpyAsync(d, pp.data(), pp.size() * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(h, launch_merge((const uint32_t* const*)d, parts, n, cnt, tmp, out_row, out_fid, out_exact,
+                         total, s));
+  uint32_t tot = 0;
+  if (n) HIPCHK(h, hipMemcpyAsync(&tot, total, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(h, hipStreamSynchronize(s));
+  if (n_pairs) *n_pairs = tot;
+  return 0;
+}
+
+int emqxgm_export_wire(emqxgm_t* h, const emqxgm_dev_out* r, const uint32_t* id_map, uint8_t* cnt8,
+                       uint32_t* fid, uint32_t* xs, uint32_t* ovf, uint32_t counts[2]) {
+  if (!h || !r || !counts || (r->n && (!cnt8 || !xs || !ovf)) || (r->n_pairs && !fid)) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mmu);
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
+  hipStream_t s = h->sync.stream;
+  if (int rc = grow_buf(h, h->d_merge, 16)) return rc;
+  uint32_t* ctr = (uint32_t*)h->d_merge.p;
+  HIPCHK(h, launch_wire_export(r->row_ptr, r->filter_id, r->exact_id, r->n, r->n_pairs, id_map,
+                               cnt8, fid, (uint2*)xs, (uint2*)ovf, ctr, s));
+  HIPCHK(h, hipMemcpyAsync(counts, ctr, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(h, hipStreamSynchronize(s));
+  return 0;
+}
+
+int emqxgm_merge_wire(emqxgm_t* h, uint32_t parts, const uint8_t* const* cnt8s,
+                      const uint32_t* const* fids, const uint32_t* const* xss, const uint32_t* n_xs,
+                      const uint32_t* const* ovfs, const uint32_t* n_ovf, uint32_t n,
+                      uint32_t* out_row, uint32_t* out_fid, uint32_t* out_exact, uint32_t* n_pairs) {
+  if (!h || !out_row || (parts && (!cnt8s || !fids || !xss || !n_xs || !ovfs || !n_ovf)) ||
+      (n && !out_exact))
+    return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mmu);
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
+  hipStream_t s = h->sync.stream;
+  // scratch: [pointer table 3 x parts | parts x (n+1) row words | n count words | total | scan]
+  const uint64_t tw = scan_tmp_words(std::max<uint32_t>(n, 1));
+  const uint64_t rows_off = (3ull * parts + 1) * 8;
+  const uint64_t need = rows_off + ((uint64_t)parts * (n + 1) + n + 2 + tw) * 4;
+  if (int rc = grow_buf(h, h->d_merge, need)) return rc;
+  uint8_t* d = (uint8_t*)h->d_merge.p;
+  uint32_t* prow = (uint32_t*)(d + rows_off);
+  uint32_t* cnt = prow + (uint64_t)parts * (n + 1);
+  uint32_t* total = cnt + n;
+  uint32_t* tmp = total + 2;
+  for (uint32_t r = 0; r < parts; ++r)
+    HIPCHK(h, launch_wire_rows(cnt8s[r], (const uint2*)ovfs[r], n_ovf[r], n, cnt, tmp,
+                               prow + (uint64_t)r * (n + 1), s));
+  HIPCHK(h, launch_wire_exact((const uint2* const*)xss, n_xs, parts, n, out_exact, s));
+  // then the merge of emqxgm_merge over {part rows, part ids, the merged exact ids}
+  std::vector<const uint32_t*> pp(3ull * parts);
+  for (uint32_t r = 0; r < parts; ++r) {
+    pp[3 * r] = prow + (uint64_t)r * (n + 1);
+    pp[3 * r + 1] = fids[r];
+    pp[3 * r + 2] = out_exact;
+  }
   if (parts) HIPCHK(h, hipMemcpyAsync(d, pp.data(), pp.size() * 8, hipMemcpyHostToDevice, s));
   HIPCHK(h, launch_merge((const uint32_t* const*)d, parts, n, cnt, tmp, out_row, out_fid, out_exact,
                          total, s));

@@ -228,6 +228,27 @@ hipError_t launch_export(const uint32_t* row, const uint32_t* fid, const uint32_
 hipError_t launch_merge(const uint32_t* const* parts, uint32_t np, uint32_t n, uint32_t* cnt,
                         uint32_t* tmp, uint32_t* orow, uint32_t* ofid, uint32_t* oexact,
                         uint32_t* total, hipStream_t s);
+// The compact wire form of a shard's result: u8 counts, mapped ids, sparse
+// (topic, exact id) xs and (topic, count) ovf lists; ctr[0] / ctr[1] = their lengths.
+hipError_t launch_wire_export(const uint32_t* row, const uint32_t* fid, const uint32_t* exact,
+                              uint32_t n, uint32_t pairs, const uint32_t* map, uint8_t* cnt8,
+                              uint32_t* ofid, uint2* xs, uint2* ovf, uint32_t* ctr, hipStream_t s);
+// a received part's row pointers [n+1] from its counts and overflow list (cnt/tmp scratch)
+hipError_t launch_wire_rows(const uint8_t* cnt8, const uint2* ovf, uint32_t novf, uint32_t n,
+                            uint32_t* cnt, uint32_t* tmp, uint32_t* row, hipStream_t s);
+// the merged exact ids [n]: NONE, then every part's (topic, id) entries (host arrays of device
+// pointers / lengths)
+hipError_t launch_wire_exact(const uint2* const* xs, const uint32_t* nx, uint32_t parts, uint32_t n,
+                             uint32_t* exact, hipStream_t s);
+// The bytes of the filters fid[0..pairs) from the device string pool (foff: pool offsets per
+// filter id): ooff = exclusive scan of their lengths (pairs + 1 entries; *total = bytes; len /
+// tmp scratch), then out[ooff[j] ..] = filter fid[j]'s bytes.
+hipError_t launch_filter_len(const uint32_t* fid, uint32_t pairs, const uint64_t* foff,
+                             uint32_t* len, uint32_t* ooff, uint32_t* tmp, uint32_t* total,
+                             hipStream_t s);
+hipError_t launch_filter_gather(const uint32_t* fid, uint32_t pairs, const uint64_t* foff,
+                                const uint8_t* pool, const uint32_t* ooff, uint8_t* out,
+                                hipStream_t s);
 // out[i] = base + row[i], i < m (u64 CSR row pointers of the host API, built on the device)
 hipError_t launch_row64(const uint32_t* row, uint64_t base, uint64_t* out, uint32_t m,
                         hipStream_t s);

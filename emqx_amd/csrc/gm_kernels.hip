@@ -258,6 +258,83 @@ __global__ __launch_bounds__(WG) void k_merge_fill(const uint32_t* const* parts,
   }
 }
 
+// ---- the compact wire form of a shard's result (filter-sharded layout over xGMI): per topic a
+// u8 pair count (255: the count is in the overflow list), the pairs' global ids in topic order,
+// and sparse lists of (topic, exact id) and (topic, count >= 255).  Sparse entries are appended
+// with one atomic per wave (their order is free: the root scatters them). ----
+__device__ __forceinline__ uint32_t wave_append(bool v, uint32_t* ctr) {
+  const uint64_t m = __ballot(v);
+  uint32_t base = 0;
+  if (lane_id() == 0 && m) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+  base = __shfl(base, 0, 64);
+  return base + mbcnt64(m);
+}
+
+__global__ __launch_bounds__(WG) void k_wire_export(const uint32_t* row, const uint32_t* fid,
+                                                    const uint32_t* exact, uint32_t n,
+                                                    uint32_t pairs, const uint32_t* map,
+                                                    uint8_t* cnt8, uint32_t* ofid, uint2* xs,
+                                                    uint2* ovf, uint32_t* ctr) {
+  const uint32_t m = max(n, pairs);
+  // every lane of a wave runs the same trip count (wave_append is a wave-wide ballot)
+  const uint32_t stride = gridDim.x * WG;
+  const uint32_t trips = (m + stride - 1) / stride;
+  for (uint32_t k = 0; k < trips; ++k) {
+    const uint32_t i = k * stride + blockIdx.x * WG + threadIdx.x;
+    const bool tv = i < n;
+    const uint32_t c = tv ? row[i + 1] - row[i] : 0u;
+    const uint32_t e = tv ? exact[i] : NONE;
+    if (tv) cnt8[i] = (uint8_t)min(c, 255u);
+    const bool big = tv && c >= 255u, hit = tv && e != NONE;
+    const uint32_t po = wave_append(big, &ctr[1]);
+    if (big) ovf[po] = make_uint2(i, c);
+    const uint32_t px = wave_append(hit, &ctr[0]);
+    if (hit) xs[px] = make_uint2(i, map ? map[e] : e);
+    if (i < pairs) ofid[i] = map ? map[fid[i]] : fid[i];
+  }
+}
+
+// one part's counts from its wire form (overflow entries patched in by k_wire_patch)
+__global__ __launch_bounds__(WG) void k_wire_counts(const uint8_t* cnt8, uint32_t n, uint32_t* cnt) {
+  for (uint32_t i = blockIdx.x * WG + threadIdx.x; i < n; i += gridDim.x * WG) cnt[i] = cnt8[i];
+}
+
+// dst[e.x] = e.y for the m sparse entries (overflow counts; exact ids)
+__global__ __launch_bounds__(WG) void k_wire_patch(const uint2* ent, uint32_t m, uint32_t* dst) {
+  for (uint32_t i = blockIdx.x * WG + threadIdx.x; i < m; i += gridDim.x * WG) {
+    const uint2 e = ent[i];
+    dst[e.x] = e.y;
+  }
+}
+
+__global__ __launch_bounds__(WG) void k_fill_u32(uint32_t* dst, uint32_t n, uint32_t v) {
+  for (uint32_t i = blockIdx.x * WG + threadIdx.x; i < n; i += gridDim.x * WG) dst[i] = v;
+}
+
+// ---- the matched filters' bytes for the host (the NIF's filter binaries): lengths from the
+// device copy of the string pool's offsets, a scan, then each pair's bytes gathered ----
+__global__ __launch_bounds__(WG) void k_filter_len(const uint32_t* fid, uint32_t pairs,
+                                                   const uint64_t* foff, uint32_t* len) {
+  for (uint32_t j = blockIdx.x * WG + threadIdx.x; j < pairs; j += gridDim.x * WG) {
+    const uint32_t f = fid[j];
+    len[j] = (uint32_t)(foff[f + 1] - foff[f]);
+  }
+}
+
+// one lane per pair; a filter's bytes are contiguous in the pool, so after its first line every
+// load of the lane hits the same line
+__global__ __launch_bounds__(WG) void k_filter_gather(const uint32_t* fid, uint32_t pairs,
+                                                      const uint64_t* foff, const uint8_t* pool,
+                                                      const uint32_t* ooff, uint8_t* out) {
+  for (uint32_t j = blockIdx.x * WG + threadIdx.x; j < pairs; j += gridDim.x * WG) {
+    const uint32_t f = fid[j];
+    const uint8_t* src = pool + foff[f];
+    uint8_t* dst = out + ooff[j];
+    const uint32_t n = ooff[j + 1] - ooff[j];
+    for (uint32_t i = 0; i < n; ++i) dst[i] = src[i];
+  }
+}
+
 uint32_t grid_for(uint64_t items, uint32_t cap_blocks) {
   uint64_t b = (items + WG - 1) / WG;
   if (b == 0) b = 1;
@@ -500,6 +577,56 @@ hipError_t launch_merge(const uint32_t* const* parts, uint32_t np, uint32_t n, u
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_merge_fill, dim3(grid_for(n, 8192)), dim3(WG), 0, s, parts, np, n, orow,
                      ofid);
+  return hipGetLastError();
+}
+
+hipError_t launch_wire_export(const uint32_t* row, const uint32_t* fid, const uint32_t* exact,
+                              uint32_t n, uint32_t pairs, const uint32_t* map, uint8_t* cnt8,
+                              uint32_t* ofid, uint2* xs, uint2* ovf, uint32_t* ctr, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(ctr, 0, 8, s);
+  if (e != hipSuccess) return e;
+  const uint64_t m = std::max<uint64_t>(n, pairs);
+  if (m == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_wire_export, dim3(grid_for(m, 8192)), dim3(WG), 0, s, row, fid, exact, n,
+                     pairs, map, cnt8, ofid, xs, ovf, ctr);
+  return hipGetLastError();
+}
+
+hipError_t launch_wire_rows(const uint8_t* cnt8, const uint2* ovf, uint32_t novf, uint32_t n,
+                            uint32_t* cnt, uint32_t* tmp, uint32_t* row, hipStream_t s) {
+  if (n) {
+    hipLaunchKernelGGL(k_wire_counts, dim3(grid_for(n, 8192)), dim3(WG), 0, s, cnt8, n, cnt);
+    if (novf)
+      hipLaunchKernelGGL(k_wire_patch, dim3(grid_for(novf, 8192)), dim3(WG), 0, s, ovf, novf, cnt);
+  }
+  return launch_scan(cnt, row, n, tmp, nullptr, s);
+}
+
+hipError_t launch_wire_exact(const uint2* const* xs, const uint32_t* nx, uint32_t parts, uint32_t n,
+                             uint32_t* exact, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_fill_u32, dim3(grid_for(n, 8192)), dim3(WG), 0, s, exact, n, NONE);
+  for (uint32_t r = 0; r < parts; ++r)
+    if (nx[r])
+      hipLaunchKernelGGL(k_wire_patch, dim3(grid_for(nx[r], 8192)), dim3(WG), 0, s, xs[r], nx[r],
+                         exact);
+  return hipGetLastError();
+}
+
+hipError_t launch_filter_len(const uint32_t* fid, uint32_t pairs, const uint64_t* foff,
+                             uint32_t* len, uint32_t* ooff, uint32_t* tmp, uint32_t* total,
+                             hipStream_t s) {
+  if (pairs)
+    hipLaunchKernelGGL(k_filter_len, dim3(grid_for(pairs, 8192)), dim3(WG), 0, s, fid, pairs, foff,
+                       len);
+  return launch_scan(len, ooff, pairs, tmp, total, s);
+}
+
+hipError_t launch_filter_gather(const uint32_t* fid, uint32_t pairs, const uint64_t* foff,
+                                const uint8_t* pool, const uint32_t* ooff, uint8_t* out,
+                                hipStream_t s) {
+  if (pairs)
+    hipLaunchKernelGGL(k_filter_gather, dim3(grid_for(pairs, 8192)), dim3(WG), 0, s, fid, pairs,
+                       foff, pool, ooff, out);
   return hipGetLastError();
 }
 

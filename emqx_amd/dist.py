@@ -6,21 +6,23 @@
 1. rank 0 broadcasts the packed topic batch (RCCL over xGMI);
 2. every rank matches it against its shard on its GPU and exports the CSR with its local filter
    ids mapped to global ids (``emqxgm_export``, one kernel);
-3. the ranks' pair counts are exchanged with one all_gather of G integers, and rank 0 receives
-   each rank's CSR with sized point-to-point receives (``batch_isend_irecv``: grouped
-   send/recv, each rank's list crosses xGMI once, only to rank 0);
-4. rank 0 merges the G CSRs topic by topic in a HIP kernel (``emqxgm_merge``: shards are
+3. every rank puts its result in the compact wire form (``emqxgm_export_wire``: u8 pair counts,
+   global ids, sparse exact hits); the lengths go round in one all_gather of 3 x G integers and
+   rank 0 receives each rank's part with sized point-to-point receives (``batch_isend_irecv``);
+4. rank 0 merges the G parts topic by topic in HIP kernels (``emqxgm_merge_wire``: shards are
    disjoint, nothing to dedupe; a topic's exact route key lives on exactly one shard).
 
-Host synchronisations per step: the batch size on the receiving ranks (step 1), the match pass
-itself, and the pair counts on rank 0 (step 3).
+Steps are pipelined (``ShardedMatcher.run``): batch k+1 is broadcast while the engine walks batch
+k.  Host synchronisations per step: the match pass (its pair count sizes the export), the
+export's entry counts, and the lengths on rank 0; the batch shape is known to every rank.
 
 ``shard="topics"`` (replicas): every rank holds the whole index (it fits: SURVEY 8e capacity
 note) and matches its own batch; no collective is on the data path.
 
-The collective code (broadcast_batch, gather_to_root) is device-agnostic: with the gloo backend
-it runs on CPU tensors, which is how tests/test_dist.py covers world_size 2 without a GPU (the
-per-rank matcher and the merge there are the test's own).  The merge (merge_parts) is HIP only.
+The collective code (broadcast_batch, gather_wire_to_root) is device-agnostic: with the gloo
+backend it runs on CPU tensors, which is how tests/test_dist.py covers world_size 2 without a GPU
+(the per-rank matcher, the wire export and the merge there are the test's torch restatements).
+The export and the merge (merge_wire) are HIP only.
 """
 from __future__ import annotations
 
@@ -88,49 +90,64 @@ def broadcast_batch(tbytes: Optional[torch.Tensor], toff: Optional[torch.Tensor]
     return tbytes.to(device), toff.to(device)
 
 
-Part = Tuple[torch.Tensor, torch.Tensor, torch.Tensor]  # (row [n+1], fid [pairs], exact [n])
+@dataclass
+class WirePart:
+    """One shard's result in the compact wire form (emqxgm_export_wire): u8 pair counts per
+    topic (255: see ovf), the pairs' global ids, (topic, exact id) and (topic, count) pairs."""
+    cnt8: torch.Tensor  # uint8 [n]
+    fid: torch.Tensor   # int32 [pairs]
+    xs: torch.Tensor    # int32 [2 * nx]
+    ovf: torch.Tensor   # int32 [2 * novf]
+
+    def nbytes(self) -> int:
+        return sum(int(t.numel()) * t.element_size() for t in (self.cnt8, self.fid, self.xs, self.ovf))
 
 
-def gather_to_root(row: torch.Tensor, fid: torch.Tensor, exact: torch.Tensor, n_pairs: int,
-                   root: int = 0, group=None) -> Optional[List[Part]]:
-    """Each rank's CSR (int32 row [n+1], fid [>= n_pairs], exact [n]) to `root`: the pair counts
-    with one all_gather of G integers, then sized point-to-point receives on the root only.
+def gather_wire_to_root(part: WirePart, root: int = 0, group=None) -> Optional[List[WirePart]]:
+    """Each rank's wire part to `root`: the (pairs, exact, overflow) lengths with one all_gather
+    of 3 x G integers (the root's one host synchronisation: it sizes the receives), then sized
+    point-to-point receives on the root only -- per non-root rank n + 4 pairs + 8 (exact hits +
+    overflows) bytes cross xGMI, against 8 n + 4 pairs for dense u32 row pointers and exact ids.
     Returns on the root the G parts in rank order (its own included), None elsewhere."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    dev = row.device
+    dev = part.cnt8.device
     cpu = _comm_on_cpu(group)
     cdev = "cpu" if cpu else dev
-    cnt = torch.tensor([n_pairs], dtype=torch.int64, device=cdev)
-    allc = [torch.zeros(1, dtype=torch.int64, device=cdev) for _ in range(world)]
-    dist.all_gather(allc, cnt, group=group)
-    fid = fid[:n_pairs]
+    lens = torch.tensor([part.fid.numel(), part.xs.numel() // 2, part.ovf.numel() // 2],
+                        dtype=torch.int64, device=cdev)
+    alll = [torch.zeros(3, dtype=torch.int64, device=cdev) for _ in range(world)]
+    dist.all_gather(alll, lens, group=group)
     if rank != root:
-        ops = [dist.P2POp(dist.isend, row.to(cdev), root, group),
-               dist.P2POp(dist.isend, exact.to(cdev), root, group)]
-        if n_pairs:
-            ops.append(dist.P2POp(dist.isend, fid.to(cdev), root, group))
+        ops = [dist.P2POp(dist.isend, part.cnt8.to(cdev), root, group)]
+        for t in (part.fid, part.xs, part.ovf):
+            if t.numel():
+                ops.append(dist.P2POp(dist.isend, t.to(cdev), root, group))
         for req in dist.batch_isend_irecv(ops):
             req.wait()
         return None
-    counts = [int(c) for c in torch.cat(allc).tolist()]
-    parts: List[Part] = []
+    ls = torch.stack(alll).tolist()
+    n = part.cnt8.numel()
+    parts: List[WirePart] = []
     ops = []
     for r in range(world):
         if r == root:
-            parts.append((row, fid, exact))
+            parts.append(part)
             continue
-        rr = torch.empty(row.numel(), dtype=row.dtype, device=cdev)
-        ee = torch.empty(exact.numel(), dtype=exact.dtype, device=cdev)
-        ff = torch.empty(counts[r], dtype=fid.dtype, device=cdev)
-        ops += [dist.P2POp(dist.irecv, rr, r, group), dist.P2POp(dist.irecv, ee, r, group)]
-        if counts[r]:
-            ops.append(dist.P2POp(dist.irecv, ff, r, group))
-        parts.append((rr, ff, ee))
+        p, nx, no = (int(x) for x in ls[r])
+        q = WirePart(torch.empty(n, dtype=torch.uint8, device=cdev),
+                     torch.empty(p, dtype=torch.int32, device=cdev),
+                     torch.empty(2 * nx, dtype=torch.int32, device=cdev),
+                     torch.empty(2 * no, dtype=torch.int32, device=cdev))
+        ops.append(dist.P2POp(dist.irecv, q.cnt8, r, group))
+        for t in (q.fid, q.xs, q.ovf):
+            if t.numel():
+                ops.append(dist.P2POp(dist.irecv, t, r, group))
+        parts.append(q)
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
-    return [(a.to(dev), b.to(dev), c.to(dev)) for a, b, c in parts]
+    return [WirePart(*(t.to(dev) for t in (q.cnt8, q.fid, q.xs, q.ovf))) for q in parts]
 
 
 @dataclass
@@ -140,8 +157,11 @@ class Merged:
     exact_id: torch.Tensor   # int32 [n] global id or NONE (u32 bits)
 
 
+Part = Tuple[torch.Tensor, torch.Tensor, torch.Tensor]  # (row [n+1], fid [pairs], exact [n])
+
+
 def merge_parts(eng, parts: Sequence[Part], n: int) -> Merged:
-    """Merge the shards' CSRs topic by topic on the device (emqxgm_merge, a HIP kernel)."""
+    """Merge dense per-shard CSRs (emqxgm_export's form) topic by topic (emqxgm_merge)."""
     dev = parts[0][0].device
     if dev.type != "cuda":
         raise RuntimeError("merge_parts runs on the GPU (emqxgm_merge); there is no CPU merge")
@@ -149,7 +169,7 @@ def merge_parts(eng, parts: Sequence[Part], n: int) -> Merged:
     row = torch.empty(n + 1, dtype=torch.int32, device=dev)
     fid = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
     ex = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
-    torch.cuda.current_stream(dev).synchronize()  # the parts came in on torch's streams
+    torch.cuda.current_stream(dev).synchronize()
     got = eng.merge([p[0].data_ptr() for p in parts],
                     [p[1].data_ptr() if p[1].numel() else 0 for p in parts],
                     [p[2].data_ptr() for p in parts], n, row.data_ptr(),
@@ -158,9 +178,33 @@ def merge_parts(eng, parts: Sequence[Part], n: int) -> Merged:
     return Merged(row, fid[:total], ex[:n])
 
 
+def merge_wire(eng, parts: Sequence[WirePart], n: int) -> Merged:
+    """Merge the shards' wire parts topic by topic on the device (emqxgm_merge_wire)."""
+    dev = parts[0].cnt8.device
+    if dev.type != "cuda":
+        raise RuntimeError("merge_wire runs on the GPU (emqxgm_merge_wire); there is no CPU merge")
+    total = sum(int(p.fid.numel()) for p in parts)
+    row = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    fid = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
+    ex = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    torch.cuda.current_stream(dev).synchronize()  # the parts came in on torch's streams
+    ptr = lambda t: t.data_ptr() if t.numel() else 0  # noqa: E731
+    got = eng.merge_wire([ptr(p.cnt8) for p in parts], [ptr(p.fid) for p in parts],
+                         [ptr(p.xs) for p in parts], [p.xs.numel() // 2 for p in parts],
+                         [ptr(p.ovf) for p in parts], [p.ovf.numel() // 2 for p in parts], n,
+                         row.data_ptr(), fid.data_ptr() if total else 0, ex.data_ptr())
+    assert got == total, (got, total)
+    return Merged(row, fid[:total], ex[:n])
+
+
 class ShardedMatcher:
     """The filter-sharded match step of one rank: `eng` holds this rank's filter
-    shard, `gid_map` (int32 device tensor) maps its local filter ids to global ids."""
+    shard, `gid_map` (int32 device tensor) maps its local filter ids to global ids.
+
+    ``run(batches)`` pipelines steps: while the engine walks batch k (emqxgm_match_device_submit
+    on its own stream), rank 0 already broadcasts batch k+1 into the other of two receive buffers;
+    then batch k's result goes to rank 0 in the wire form and is merged there.  The batch shape
+    (bytes, topics) is given to every rank, so no size message precedes a broadcast."""
 
     def __init__(self, eng, gid_map: torch.Tensor, device, group=None, root: int = 0):
         self.eng = eng
@@ -168,28 +212,65 @@ class ShardedMatcher:
         self.device = device
         self.group = group
         self.root = root
-        self._bufs = None
+        self._wire = None
+        self.bytes_to_root = 0   # per step, summed over the ranks that send (set on the root)
+        self.bytes_broadcast = 0
 
-    def _out(self, n: int, pairs: int):
-        cap_n, cap_p = (0, 0) if self._bufs is None else (self._bufs[2].numel(), self._bufs[1].numel())
-        if n + 1 > cap_n or pairs > cap_p:
-            self._bufs = (torch.empty(max(n + 1, cap_n), dtype=torch.int32, device=self.device),
-                          torch.empty(max(pairs, cap_p, 1), dtype=torch.int32, device=self.device),
-                          torch.empty(max(n + 1, cap_n), dtype=torch.int32, device=self.device))
-        row, fid, ex = self._bufs
-        return row[: n + 1], fid, ex[:n]
+    def _wire_bufs(self, n: int, pairs: int):
+        cap_n, cap_p = (0, 0) if self._wire is None else (self._wire[0].numel(), self._wire[1].numel())
+        if n > cap_n or pairs > cap_p:
+            n2, p2 = max(n, cap_n, 1), max(pairs, cap_p, 1)
+            self._wire = (torch.empty(n2, dtype=torch.uint8, device=self.device),
+                          torch.empty(p2, dtype=torch.int32, device=self.device),
+                          torch.empty(2 * n2, dtype=torch.int32, device=self.device),
+                          torch.empty(2 * n2, dtype=torch.int32, device=self.device))
+        return self._wire
 
-    def step(self, tbytes: Optional[torch.Tensor] = None,
-             toff: Optional[torch.Tensor] = None) -> Optional[Merged]:
-        """One batch (given on the root): broadcast, match this shard, gather, merge on root."""
-        b, o = broadcast_batch(tbytes, toff, self.device, self.root, self.group)
-        n = o.numel() - 1
-        torch.cuda.current_stream(self.device).synchronize()  # the engine's stream reads them
-        r = self.eng.match_device(b.data_ptr(), o.data_ptr(), n, b.numel())
-        row, fid, ex = self._out(n, r.n_pairs)
-        self.eng.export(r, self.gid_map.data_ptr(), row.data_ptr(),
-                        fid.data_ptr() if r.n_pairs else 0, ex.data_ptr() if n else 0)
-        parts = gather_to_root(row, fid, ex, r.n_pairs, self.root, self.group)
+    def _bcast(self, tb, to, shape):
+        nb, nt = shape
+        cpu = _comm_on_cpu(self.group)
+        cdev = "cpu" if cpu else self.device
+        if dist.get_rank(self.group) == self.root:
+            b, o = tb.to(cdev), to.to(cdev)
+        else:
+            b = torch.empty(nb, dtype=torch.uint8, device=cdev)
+            o = torch.empty(nt + 1, dtype=torch.int32, device=cdev)
+        if nb:
+            dist.broadcast(b, self.root, group=self.group)
+        dist.broadcast(o, self.root, group=self.group)
+        self.bytes_broadcast = (nb + 4 * (nt + 1)) * (dist.get_world_size(self.group) - 1)
+        return b.to(self.device), o.to(self.device)
+
+    def _finish(self, ticket, n: int) -> Optional[Merged]:
+        r = self.eng.match_device_wait(ticket)
+        cnt8, fid, xs, ovf = self._wire_bufs(n, r.n_pairs)
+        nx, no = self.eng.export_wire(r, self.gid_map.data_ptr(), cnt8.data_ptr() if n else 0,
+                                      fid.data_ptr() if r.n_pairs else 0, xs.data_ptr(),
+                                      ovf.data_ptr())
+        part = WirePart(cnt8[:n], fid[:r.n_pairs], xs[:2 * nx], ovf[:2 * no])
+        parts = gather_wire_to_root(part, self.root, self.group)
         if parts is None:
             return None
-        return merge_parts(self.eng, parts, n)
+        self.bytes_to_root = sum(p.nbytes() for i, p in enumerate(parts) if i != self.root)
+        return merge_wire(self.eng, parts, n)
+
+    def run(self, batches, shapes):
+        """Yields the merged result of every batch on the root (None elsewhere).  `batches`:
+        (bytes, offsets) tensors per step on the root (ignored elsewhere); `shapes`: (bytes,
+        topics) per step on every rank."""
+        it = iter(batches)
+        shapes = list(shapes)
+        b, o = self._bcast(*next(it), shapes[0])
+        for k, (nb, nt) in enumerate(shapes):
+            torch.cuda.current_stream(self.device).synchronize()  # batch k is in HBM
+            ticket = self.eng.match_device_submit(b.data_ptr(), o.data_ptr(), nt, nb)
+            nxt = None
+            if k + 1 < len(shapes):  # batch k+1 crosses xGMI while the engine walks batch k
+                nxt = self._bcast(*next(it), shapes[k + 1])
+            yield self._finish(ticket, nt)
+            if nxt is not None:
+                b, o = nxt
+
+    def step(self, tbytes: Optional[torch.Tensor], toff: Optional[torch.Tensor], shape) -> Optional[Merged]:
+        """One batch: broadcast, match this shard, wire to root, merge there."""
+        return next(self.run([(tbytes, toff)], [shape]))

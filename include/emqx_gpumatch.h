@@ -225,6 +225,12 @@ typedef struct emqxgm_batch_out {
 int emqxgm_match_batch_submit(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets,
                               uint32_t n, uint64_t* ticket);
 int emqxgm_match_batch_wait(emqxgm_t* h, uint64_t ticket, emqxgm_batch_out* out);
+/* _wait, plus the bytes of every matched pair's filter, gathered on the device from its copy of
+ * the string pool and copied into pinned buffers of the pipe (same lifetime as the result): pair
+ * j's filter is fbytes[foff[j] .. foff[j+1]), foff has n_pairs + 1 entries.  What a NIF needs to
+ * build each caller's filter binaries without touching the host registry per pair. */
+int emqxgm_match_batch_wait_filters(emqxgm_t* h, uint64_t ticket, emqxgm_batch_out* out,
+                                    const uint32_t** foff, const uint8_t** fbytes);
 
 /* ---- publish fan-out (emqx_broker.erl:218-355) -------------------------------------------
  * Routes with dest identity: a plain route {Filter, Node} passes group = EMQXGM_NONE; a shared-
@@ -389,6 +395,20 @@ int emqxgm_export(emqxgm_t* h, const emqxgm_dev_out* r, const uint32_t* id_map, 
 int emqxgm_merge(emqxgm_t* h, uint32_t parts, const uint32_t* const* rows,
                  const uint32_t* const* fids, const uint32_t* const* exacts, uint32_t n,
                  uint32_t* out_row, uint32_t* out_fid, uint32_t* out_exact, uint32_t* n_pairs);
+
+/* The compact wire form of a shard's result for the exchange to the root:
+ * cnt8[n] = per-topic pair count (255: the count is in ovf), fid[n_pairs] = the pairs' ids mapped
+ * through id_map (NULL = identity), xs = (topic, exact id) pairs of the topics that equal a route
+ * key, ovf = (topic, count) pairs of the topics with >= 255 pairs; xs and ovf are device arrays
+ * of 2 x n u32, counts[0] / counts[1] = their entries.  emqxgm_merge_wire merges `parts` such
+ * results (host arrays of device pointers / lengths) into one CSR exactly as emqxgm_merge does.
+ * Both return when the device work is complete. */
+int emqxgm_export_wire(emqxgm_t* h, const emqxgm_dev_out* r, const uint32_t* id_map, uint8_t* cnt8,
+                       uint32_t* fid, uint32_t* xs, uint32_t* ovf, uint32_t counts[2]);
+int emqxgm_merge_wire(emqxgm_t* h, uint32_t parts, const uint8_t* const* cnt8s,
+                      const uint32_t* const* fids, const uint32_t* const* xss, const uint32_t* n_xs,
+                      const uint32_t* const* ovfs, const uint32_t* n_ovf, uint32_t n,
+                      uint32_t* out_row, uint32_t* out_fid, uint32_t* out_exact, uint32_t* n_pairs);
 
 /* Diagnostic pass (instrumented walk kernel, not the production launch): runs the device
  * match and returns out[0] = trie states matched (SURVEY 8d S(t) summed over the batch),

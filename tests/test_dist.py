@@ -2,11 +2,13 @@
 on CPU.
 
 Each rank holds one filter shard; rank 0 broadcasts the topic batch, every rank matches it
-against its shard, the pair counts are all-gathered and every rank's CSR reaches rank 0 through
-sized point-to-point receives; merged there, it must equal the unsharded answer.  The per-rank
-matcher is the oracle and the merge a torch restatement of emqxgm_merge (no GPU in this
-container); on the GPU box bench.py runs the same collective code with the HIP engine (match,
-export, merge) and RCCL, and tests/test_gpu_dist.py checks emqxgm_merge against _ref_merge."""
+against its shard and puts the result in the compact wire form (u8 counts, global ids, sparse
+exact hits and overflow counts), the lengths are all-gathered and every rank's part reaches
+rank 0 through sized point-to-point receives; merged there, it must equal the unsharded answer.
+The per-rank matcher is the oracle, the wire export and the merge numpy restatements of
+emqxgm_export_wire / emqxgm_merge_wire (no GPU in this container); on the GPU box bench.py runs
+the same collective code with the HIP engine and RCCL, and tests/test_gpu_dist.py checks the
+HIP export / merge against these restatements."""
 import os
 import socket
 
@@ -58,6 +60,57 @@ def parts_len(p):
     return int(p[0][-1])
 
 
+def _ref_export_wire(row, gid, exg):
+    """numpy restatement of emqxgm_export_wire (gm_kernels.hip k_wire_export): u8 counts (255:
+    see ovf), ids, (topic, exact id) and (topic, count >= 255) pairs (any order)."""
+    cnt = np.diff(row.astype(np.int64))
+    t = np.arange(len(cnt), dtype=np.int64)
+    hit, big = exg != 0xFFFFFFFF, cnt >= 255
+    xs = np.stack([t[hit], exg[hit].astype(np.int64)], 1).reshape(-1)
+    ovf = np.stack([t[big], cnt[big]], 1).reshape(-1)
+    return (np.minimum(cnt, 255).astype(np.uint8), gid.astype(np.uint32), xs.astype(np.uint32),
+            ovf.astype(np.uint32))
+
+
+def _ref_merge_wire(parts, n):
+    """numpy restatement of emqxgm_merge_wire: each part's rows from its counts and overflow
+    list, the exact ids from the sparse pairs, then _ref_merge."""
+    dense = []
+    ex = np.full(n, 0xFFFFFFFF, np.uint32)
+    for cnt8, fid, xs, ovf in parts:
+        cnt = cnt8.astype(np.int64)
+        o = ovf.reshape(-1, 2).astype(np.int64)
+        cnt[o[:, 0]] = o[:, 1]
+        row = np.zeros(n + 1, np.int64)
+        np.cumsum(cnt, out=row[1:])
+        x = xs.reshape(-1, 2).astype(np.int64)
+        ex[x[:, 0]] = x[:, 1]
+        dense.append((row, fid))
+    i32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint32).view(np.int32))  # noqa: E731
+    return _ref_merge([(i32(r), i32(f), i32(ex)) for r, f in dense], n)
+
+
+def test_wire_restatement_round_trip():
+    """Counts of 255 and more go through the overflow list; exact ids through the sparse pairs."""
+    rng = np.random.default_rng(5)
+    n = 3000
+    parts_dense, parts_wire = [], []
+    owner = rng.integers(-1, 3, n)
+    for r in range(3):
+        cnt = rng.integers(0, 4, n)
+        cnt[rng.integers(0, n, 20)] = rng.integers(250, 700, 20)
+        row = np.zeros(n + 1, np.uint32)
+        np.cumsum(cnt, out=row[1:])
+        gid = rng.integers(0, 10 ** 6, int(row[-1])).astype(np.uint32)
+        exg = np.where(owner == r, rng.integers(0, 10 ** 6, n), 0xFFFFFFFF).astype(np.uint32)
+        i32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint32).view(np.int32))  # noqa: E731
+        parts_dense.append((i32(row), i32(gid), i32(exg)))
+        parts_wire.append(_ref_export_wire(row, gid, exg))
+    a, b = _ref_merge(parts_dense, n), _ref_merge_wire(parts_wire, n)
+    assert all(np.array_equal(x, y) for x, y in zip(a, b))
+    assert sum(len(w[3]) for w in parts_wire) > 0  # overflow entries were exercised
+
+
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -79,15 +132,19 @@ def _worker(rank, world, port, q):
         gid = mine[ids.astype(np.int64)].astype(np.uint32)
         exg = np.where(ex == D.NONE, D.NONE, mine[np.minimum(ex, len(mine) - 1).astype(np.int64)])
         i32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint32).view(np.int32))  # noqa: E731
-        # rank 1 sends a padded fid buffer: only its first n_pairs entries may travel
-        pad = np.concatenate([gid, np.full(7, 12345, np.uint32)])
-        parts = D.gather_to_root(i32(row), i32(pad if rank else gid), i32(exg), len(gid))
+        cnt8, fid, xs, ovf = _ref_export_wire(row, gid, exg.astype(np.uint32))
+        part = D.WirePart(torch.from_numpy(cnt8), i32(fid), i32(xs), i32(ovf))
+        parts = D.gather_wire_to_root(part)
         if rank != 0:
             assert parts is None
         else:
-            merged = _ref_merge(parts, w.nt)
-        if rank == 0:
-            assert [p[1].numel() for p in parts][1] == parts_len(parts[1])
+            u = lambda t: t.numpy().view(np.uint32) if t.dtype == torch.int32 else t.numpy()  # noqa: E731
+            merged = _ref_merge_wire([tuple(u(t) for t in (p.cnt8, p.fid, p.xs, p.ovf))
+                                      for p in parts], w.nt)
+            p1 = parts[1]
+            sent = p1.nbytes()
+            assert sent == w.nt + 4 * p1.fid.numel() + 4 * (p1.xs.numel() + p1.ovf.numel())
+            assert sent < 4 * (w.nt + 1) + 4 * w.nt + 4 * p1.fid.numel()  # the dense CSR + exact
             full = RefIndex(True)
             full.add_many(w.fbytes, w.foff, 2 + w.fwild)
             frow, fids, fex = full.match(w.tbytes, w.toff)

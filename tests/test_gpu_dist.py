@@ -1,8 +1,9 @@
-"""The filter-sharded layout's device side (emqx_amd/dist.py): emqxgm_export (a
-shard's CSR with global ids) and emqxgm_merge (G shards merged topic by topic on the device),
-checked against tests/test_dist.py's restatement _ref_merge, and the whole ShardedMatcher step
-rehearsed with two ranks sharing this box's GPU (gloo: RCCL refuses two ranks on one device)
-against the unsharded oracle."""
+"""The filter-sharded layout's device side (emqx_amd/dist.py): emqxgm_export /
+emqxgm_export_wire (a shard's result with global ids, dense or in the compact wire form) and
+emqxgm_merge / emqxgm_merge_wire (G shards merged topic by topic on the device), checked against
+tests/test_dist.py's restatements, and the pipelined ShardedMatcher rehearsed with two ranks
+sharing this box's GPU (gloo: RCCL refuses two ranks on one device) against the unsharded
+oracle."""
 import os
 import socket
 
@@ -10,7 +11,7 @@ import numpy as np
 import pytest
 import torch
 
-from tests.test_dist import _ref_merge, _subset
+from tests.test_dist import _ref_export_wire, _ref_merge, _ref_merge_wire, _subset
 
 pytestmark = pytest.mark.gpu
 
@@ -45,6 +46,70 @@ def test_merge_matches_reference(emqx):
         assert np.array_equal(m.row_ptr.cpu().numpy().view(np.uint32).astype(np.int64), row)
         assert np.array_equal(m.filter_id.cpu().numpy().view(np.uint32).astype(np.int64), fid)
         assert np.array_equal(m.exact_id.cpu().numpy().view(np.uint32).astype(np.int64), ex)
+    eng.close()
+
+
+def test_merge_wire_matches_reference(emqx):
+    """Wire parts (counts >= 255 through the overflow list) merged on the device equal the
+    restatement, and equal emqxgm_merge over the same parts in dense form."""
+    from emqx_amd import dist as D
+    eng = emqx.Engine()
+    rng = np.random.default_rng(2)
+    cu = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    for n, g in ((0, 2), (1, 1), (1000, 3), (70000, 8)):
+        owner = rng.integers(-1, g, n)
+        wires, dense = [], []
+        for r in range(g):
+            cnt = rng.integers(0, 4, n)
+            if n:
+                cnt[rng.integers(0, n, 5)] = rng.integers(255, 600, 5)
+            row = np.zeros(n + 1, np.uint32)
+            np.cumsum(cnt, out=row[1:])
+            gid = rng.integers(0, 10 ** 6, int(row[-1])).astype(np.uint32)
+            exg = np.where(owner == r, rng.integers(0, 10 ** 6, n), 0xFFFFFFFF).astype(np.uint32)
+            wires.append(_ref_export_wire(row, gid, exg))
+            dense.append(tuple(cu(a.view(np.int32)) for a in (row, gid, exg)))
+        parts = [D.WirePart(cu(c), cu(f.view(np.int32)), cu(x.view(np.int32)), cu(o.view(np.int32)))
+                 for c, f, x, o in wires]
+        m = D.merge_wire(eng, parts, n)
+        row, fid, ex = _ref_merge_wire(wires, n)
+        assert np.array_equal(m.row_ptr.cpu().numpy().view(np.uint32).astype(np.int64), row)
+        assert np.array_equal(m.filter_id.cpu().numpy().view(np.uint32).astype(np.int64), fid)
+        assert np.array_equal(m.exact_id.cpu().numpy().view(np.uint32).astype(np.int64), ex)
+        md = D.merge_parts(eng, dense, n)
+        assert torch.equal(md.row_ptr, m.row_ptr) and torch.equal(md.filter_id, m.filter_id)
+        assert torch.equal(md.exact_id, m.exact_id)
+    eng.close()
+
+
+def test_export_wire_matches_restatement(emqx):
+    import workloads
+    w = workloads.generate(2, 30000, 4000)
+    eng = emqx.Engine()
+    eng.route_ref_many(w.fbytes, w.foff)
+    wi = np.nonzero(w.fwild)[0]
+    wb, wo = _subset(w, wi)
+    eng.trie_insert_many(wb, wo)
+    eng.commit()
+    db = torch.from_numpy(w.tbytes).cuda()
+    do = torch.from_numpy(w.toff.view(np.int32)).cuda()
+    torch.cuda.synchronize()
+    r = eng.match_device(db.data_ptr(), do.data_ptr(), w.nt, int(w.toff[-1]))
+    row = torch.empty(w.nt + 1, dtype=torch.int32, device="cuda")
+    fid = torch.empty(r.n_pairs, dtype=torch.int32, device="cuda")
+    ex = torch.empty(w.nt, dtype=torch.int32, device="cuda")
+    eng.export(r, 0, row.data_ptr(), fid.data_ptr(), ex.data_ptr())
+    c8 = torch.empty(w.nt, dtype=torch.uint8, device="cuda")
+    f2 = torch.empty(r.n_pairs, dtype=torch.int32, device="cuda")
+    xs = torch.empty(2 * w.nt, dtype=torch.int32, device="cuda")
+    ov = torch.empty(2 * w.nt, dtype=torch.int32, device="cuda")
+    nx, no = eng.export_wire(r, 0, c8.data_ptr(), f2.data_ptr(), xs.data_ptr(), ov.data_ptr())
+    u = lambda t: t.cpu().numpy().view(np.uint32)  # noqa: E731
+    c, f, x, o = _ref_export_wire(u(row), u(fid), u(ex))
+    assert np.array_equal(c8.cpu().numpy(), c) and np.array_equal(u(f2), f)
+    assert nx == len(x) // 2 and no == len(o) // 2 and nx > 0
+    key = lambda a: sorted(map(tuple, a.reshape(-1, 2).tolist()))  # noqa: E731
+    assert key(u(xs)[:2 * nx]) == key(x) and key(u(ov)[:2 * no]) == key(o)
     eng.close()
 
 
@@ -107,9 +172,12 @@ def _rank(rank, world, port, q):
         sm = D.ShardedMatcher(eng, torch.from_numpy(gid.view(np.int32)).to(dev), dev)
         tb = torch.from_numpy(w.tbytes).to(dev) if rank == 0 else None
         to = torch.from_numpy(w.toff.view(np.int32)).to(dev) if rank == 0 else None
-        for _ in range(2):  # twice: buffers are reused across steps
-            m = sm.step(tb, to)
+        shape = (int(w.toff[-1]), w.nt)
+        # three pipelined steps (batch k+1 broadcast while batch k is walked; buffers reused)
+        ms = list(sm.run([(tb, to)] * 3, [shape] * 3))
+        m = ms[-1]
         if rank == 0:
+            assert all(x is not None for x in ms) and sm.bytes_to_root > 0
             full = RefIndex(True)
             full.add_many(w.fbytes, w.foff, 2 + w.fwild)
             frow, fids, fex = full.match(w.tbytes, w.toff)
