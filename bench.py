@@ -403,9 +403,9 @@ def _window_sweep(Batcher, eng, w, sizes):
         state = {"pos": 0, "done": 0}
 
         def collect():
-            r = b.collect(inflight.pop(0))
-            lat.append(r.latency_ns)
-            state["done"] += len(r.tag)
+            n_, _, _, ns = b.collect(inflight.pop(0), materialize=False)
+            lat.append(ns)
+            state["done"] += n_
 
         def run(total):
             added = 0
@@ -434,9 +434,10 @@ def _window_sweep(Batcher, eng, w, sizes):
                        "latency_us_p50": round(float(np.percentile(la, 50)), 1),
                        "latency_us_p99": round(float(np.percentile(la, 99)), 1)}
     out["includes"] = ("topics packed into pinned windows, H2D, the device pass, row pointers + "
-                       "filter ids + exact ids to pinned host memory, each pair's filter bytes "
-                       "copied into the window's arena (emqxgm_batcher_*), 3 windows in flight; "
-                       "latency = flush -> collected")
+                       "filter ids + exact ids and every pair's filter bytes (gathered on the "
+                       "device) in pinned host memory (emqxgm_batcher_*), 3 windows in flight; "
+                       "latency = flush -> collected; the caller's reading of the result (the "
+                       "NIF's term building) is not included")
     return out
 
 
@@ -468,13 +469,19 @@ def _filter_sharded_run(Engine, D, args, w, dbat, rank, world, dev, local):
     seng, gid = _build_engine(Engine, w, mine, args, local)
     log(f"[rank {rank}] filter shard: {len(mine)} filters in {time.time() - t0:.1f}s")
     sm = D.ShardedMatcher(seng, torch.from_numpy(gid.view(np.int32)).to(dev), dev)
+    # the root's batch shapes, once, outside the timed region (every rank drew its own batches
+    # for the replica measurement)
+    cdev = "cpu" if D._comm_on_cpu() else dev
+    shp = torch.tensor([b[2] for b in dbat], dtype=torch.int64, device=cdev)
+    dist.broadcast(shp, 0)
+    root_nb = [int(x) for x in shp.tolist()]
 
     def batches(k0, k):
         return [((dbat[(k0 + i) % len(dbat)][0], dbat[(k0 + i) % len(dbat)][1]) if rank == 0
                  else (None, None)) for i in range(k)]
 
     def shapes(k0, k):
-        return [(dbat[(k0 + i) % len(dbat)][2], w.nt) for i in range(k)]
+        return [(root_nb[(k0 + i) % len(dbat)], w.nt) for i in range(k)]
     for _ in sm.run(batches(0, args.warmup), shapes(0, args.warmup)):
         pass
     torch.cuda.synchronize()
@@ -493,7 +500,7 @@ def _filter_sharded_run(Engine, D, args, w, dbat, rank, world, dev, local):
     to_root = torch.tensor([sm.bytes_to_root], dtype=torch.float64, device=dev)
     dist.all_reduce(to_root, op=dist.ReduceOp.MAX)
     seng.close()
-    nb = float(np.mean([b[2] for b in dbat]))
+    nb = float(np.mean(root_nb))
     dense = (8 * w.nt + 4) * (world - 1) + 4 * pairs * (world - 1) / world
     return {"value": round(w.nt / step_s, 1), "unit": "topics/s", "ms_per_step": round(step_s * 1e3, 4),
             "scaling": "strong", "parallelism": f"filter-shard x{world}",

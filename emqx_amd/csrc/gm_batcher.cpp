@@ -41,9 +41,13 @@ struct Window {
   uint64_t id = 0, ticket = 0;
   int state = 0;  // 0 open / free, 1 in flight, 2 collected
   uint64_t flush_ns = 0, done_ns = 0;
-  std::vector<uint64_t> r_tag, r_foff;
-  std::vector<uint32_t> r_row, r_fid, r_exact;
-  std::vector<uint8_t> r_fb;
+  // the collected result: tags copied (the slot's tag list is refilled when it reopens), the
+  // rest read in place from the host pipe's pinned buffers, valid until EMQXGM_HOST_PIPES more
+  // windows are flushed (the pipe's next ticket)
+  std::vector<uint64_t> r_tag;
+  emqxgm_batch_out r{};
+  const uint32_t* r_foff = nullptr;
+  const uint8_t* r_fb = nullptr;
 };
 
 }  // namespace
@@ -183,31 +187,23 @@ int emqxgm_batcher_collect(emqxgm_batcher_t* b, uint64_t window, emqxgm_window_o
   if (!wp) return -ENOENT;
   Window& w = *wp;
   if (w.state == 1) {
-    emqxgm_batch_out o;
-    const uint32_t* fo = nullptr;
-    const uint8_t* fb = nullptr;
     // every pair's filter bytes gathered on the device from its copy of the string pool (the
     // host registry per pair costs two random DRAM reads: ~250 ns per cfg3 topic, r03)
-    int rc = emqxgm_match_batch_wait_filters(b->h, w.ticket, &o, &fo, &fb);
+    int rc = emqxgm_match_batch_wait_filters(b->h, w.ticket, &w.r, &w.r_foff, &w.r_fb);
     if (rc) return rc;
-    w.r_row.assign(o.row_ptr, o.row_ptr + o.n + 1);
-    w.r_fid.assign(o.filter_id, o.filter_id + o.n_pairs);
-    w.r_exact.assign(o.exact_id, o.exact_id + o.n);
     w.r_tag = w.tag;
-    w.r_foff.assign(fo, fo + o.n_pairs + 1);
-    w.r_fb.assign(fb, fb + fo[o.n_pairs]);
     w.state = 2;
     w.done_ns = mono_ns();
     b->in_flight -= 1;
   }
-  out->n = (uint32_t)w.r_exact.size();
-  out->n_pairs = (uint32_t)w.r_fid.size();
+  out->n = w.r.n;
+  out->n_pairs = w.r.n_pairs;
   out->tag = w.r_tag.data();
-  out->row = w.r_row.data();
-  out->filter_id = w.r_fid.data();
-  out->foff = w.r_foff.data();
-  out->fbytes = w.r_fb.data();
-  out->exact_id = w.r_exact.data();
+  out->row = w.r.row_ptr;
+  out->filter_id = w.r.filter_id;
+  out->foff = w.r_foff;
+  out->fbytes = w.r_fb;
+  out->exact_id = w.r.exact_id;
   out->flush_ns = w.flush_ns;
   out->done_ns = w.done_ns;
   return 0;

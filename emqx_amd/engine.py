@@ -63,7 +63,7 @@ class _BatcherCfg(C.Structure):
 class _WindowOut(C.Structure):
     _fields_ = [("n", C.c_uint32), ("n_pairs", C.c_uint32), ("tag", C.POINTER(C.c_uint64)),
                 ("row", C.POINTER(C.c_uint32)), ("filter_id", C.POINTER(C.c_uint32)),
-                ("foff", C.POINTER(C.c_uint64)), ("fbytes", C.POINTER(C.c_uint8)),
+                ("foff", C.POINTER(C.c_uint32)), ("fbytes", C.POINTER(C.c_uint8)),
                 ("exact_id", C.POINTER(C.c_uint32)), ("flush_ns", C.c_uint64),
                 ("done_ns", C.c_uint64)]
 
@@ -583,7 +583,7 @@ class Window:
     tag: np.ndarray        # uint64 [n]
     row: np.ndarray        # uint32 [n+1]
     filter_id: np.ndarray  # uint32 [n_pairs]
-    foff: np.ndarray       # uint64 [n_pairs+1]
+    foff: np.ndarray       # uint32 [n_pairs+1]
     fbytes: bytes
     exact_id: np.ndarray   # uint32 [n]
     latency_ns: int
@@ -640,16 +640,20 @@ class Batcher:
         self._eng._check(self._lib.emqxgm_batcher_flush(self._b, C.byref(w)), "batcher_flush")
         return int(w.value)
 
-    def collect(self, window: int) -> Window:
+    def collect(self, window: int, materialize: bool = True):
+        """The window's result as a Window (copies); materialize=False only completes it and
+        returns (topics, pairs, filter bytes, flush -> collected ns) without reading it."""
         o = _WindowOut()
         self._eng._check(self._lib.emqxgm_batcher_collect(self._b, window, C.byref(o)),
                          "batcher_collect")
         n, m = o.n, o.n_pairs
+        if not materialize:
+            return n, m, (int(o.foff[m]) if m else 0), int(o.done_ns - o.flush_ns)
 
         def arr(p, k, dt):
             return np.ctypeslib.as_array(p, shape=(k,)).copy() if k else np.zeros(0, dt)
         nb = int(o.foff[m]) if m else 0
         return Window(arr(o.tag, n, np.uint64), arr(o.row, n + 1, np.uint32),
-                      arr(o.filter_id, m, np.uint32), arr(o.foff, m + 1, np.uint64),
+                      arr(o.filter_id, m, np.uint32), arr(o.foff, m + 1, np.uint32),
                       C.string_at(o.fbytes, nb) if nb else b"", arr(o.exact_id, n, np.uint32),
                       int(o.done_ns - o.flush_ns))

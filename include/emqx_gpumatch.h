@@ -354,7 +354,7 @@ typedef struct emqxgm_window_out {
   const uint64_t* tag;        /* [n] the caller's tag of each topic (e.g. its waiter) */
   const uint32_t* row;        /* [n+1] topic i's trie filters are pairs row[i] .. row[i+1] */
   const uint32_t* filter_id;  /* [n_pairs] */
-  const uint64_t* foff;       /* [n_pairs + 1] pair j's filter bytes: fbytes[foff[j] .. foff[j+1]) */
+  const uint32_t* foff;       /* [n_pairs + 1] pair j's filter bytes: fbytes[foff[j] .. foff[j+1]) */
   const uint8_t* fbytes;
   const uint32_t* exact_id;   /* [n] route key equal to the topic, or EMQXGM_NONE */
   uint64_t flush_ns, done_ns; /* CLOCK_MONOTONIC at the flush and when the result was complete */
@@ -377,8 +377,9 @@ int emqxgm_batcher_due(emqxgm_batcher_t* b, uint64_t now_ns);
 /* Submits the open window and opens an empty one; *window = the window's id (0: it was empty,
  * nothing submitted).  -EBUSY when EMQXGM_HOST_PIPES windows are flushed and not collected. */
 int emqxgm_batcher_flush(emqxgm_batcher_t* b, uint64_t* window);
-/* Completes window `window` (flushed, not yet collected; the oldest first is cheapest) and
- * returns its result. */
+/* Completes window `window` (flushed; the oldest first is cheapest) and returns its result,
+ * read in place from the host pipe's pinned buffers: valid until EMQXGM_HOST_PIPES more windows
+ * are flushed (collecting it again before that returns the same result). */
 int emqxgm_batcher_collect(emqxgm_batcher_t* b, uint64_t window, emqxgm_window_out* out);
 
 /* ---- filter-sharded layout over several GPUs (the subscription set partitioned by
