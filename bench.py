@@ -468,7 +468,7 @@ def _filter_sharded_run(Engine, D, args, w, dbat, rank, world, dev, local):
     mine = np.nonzero(D.filter_shards(w.fbytes, w.foff, world) == rank)[0]
     seng, gid = _build_engine(Engine, w, mine, args, local)
     log(f"[rank {rank}] filter shard: {len(mine)} filters in {time.time() - t0:.1f}s")
-    sm = D.ShardedMatcher(seng, torch.from_numpy(gid.view(np.int32)).to(dev), dev)
+    sm = D.ShardedMatcher(seng, torch.from_numpy(gid.view(np.int32)).to(dev), dev, n_global=w.nf)
     # the root's batch shapes, once, outside the timed region (every rank drew its own batches
     # for the replica measurement)
     cdev = "cpu" if D._comm_on_cpu() else dev
@@ -510,9 +510,9 @@ def _filter_sharded_run(Engine, D, args, w, dbat, rank, world, dev, local):
             "bytes_to_root_per_step": int(to_root.item()),
             "bytes_to_root_dense_r02_estimate": int(dense),
             "step": "rank 0's batch broadcast (RCCL; batch k+1 while the engines walk batch k), "
-                    "matched on each shard, results in the compact wire form (u8 counts, global "
-                    "ids, sparse exact hits) to rank 0 by grouped send/recv, merged by "
-                    "emqxgm_merge_wire"}
+                    "matched on each shard, results in the compact wire form (2-bit or u8 counts, "
+                    "24- or 32-bit global ids, sparse exact hits) to rank 0 by grouped "
+                    "send/recv, merged by emqxgm_merge_wire"}
 
 
 def _last_nz(v):

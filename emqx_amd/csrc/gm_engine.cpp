@@ -3140,52 +3140,65 @@ int emqxgm_merge(emqxgm_t* h, uint32_t parts, const uint32_t* const* rows,
   return 0;
 }
 
-int emqxgm_export_wire(emqxgm_t* h, const emqxgm_dev_out* r, const uint32_t* id_map, uint8_t* cnt8,
-                       uint32_t* fid, uint32_t* xs, uint32_t* ovf, uint32_t counts[2]) {
-  if (!h || !r || !counts || (r->n && (!cnt8 || !xs || !ovf)) || (r->n_pairs && !fid)) return -EINVAL;
+int emqxgm_export_wire(emqxgm_t* h, const emqxgm_dev_out* r, const uint32_t* id_map,
+                       uint32_t flags, void* cnt, void* fid, uint32_t* xs, uint32_t* ovf,
+                       uint32_t counts[2]) {
+  if (!h || !r || !counts || (flags & ~3u) || (r->n && (!cnt || !xs || !ovf)) ||
+      (r->n_pairs && !fid))
+    return -EINVAL;
   std::lock_guard<std::mutex> g(h->mmu);
   if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
   hipStream_t s = h->sync.stream;
   if (int rc = grow_buf(h, h->d_merge, 16)) return rc;
   uint32_t* ctr = (uint32_t*)h->d_merge.p;
   HIPCHK(h, launch_wire_export(r->row_ptr, r->filter_id, r->exact_id, r->n, r->n_pairs, id_map,
-                               cnt8, fid, (uint2*)xs, (uint2*)ovf, ctr, s));
+                               flags, (uint8_t*)cnt, (uint8_t*)fid, (uint2*)xs, (uint2*)ovf, ctr, s));
   HIPCHK(h, hipMemcpyAsync(counts, ctr, 8, hipMemcpyDeviceToHost, s));
   HIPCHK(h, hipStreamSynchronize(s));
   return 0;
 }
 
-int emqxgm_merge_wire(emqxgm_t* h, uint32_t parts, const uint8_t* const* cnt8s,
-                      const uint32_t* const* fids, const uint32_t* const* xss, const uint32_t* n_xs,
-                      const uint32_t* const* ovfs, const uint32_t* n_ovf, uint32_t n,
-                      uint32_t* out_row, uint32_t* out_fid, uint32_t* out_exact, uint32_t* n_pairs) {
-  if (!h || !out_row || (parts && (!cnt8s || !fids || !xss || !n_xs || !ovfs || !n_ovf)) ||
+int emqxgm_merge_wire(emqxgm_t* h, uint32_t parts, const uint32_t* flags, const void* const* cnts,
+                      const void* const* fids, const uint32_t* n_pairs_part,
+                      const uint32_t* const* xss, const uint32_t* n_xs, const uint32_t* const* ovfs,
+                      const uint32_t* n_ovf, uint32_t n, uint32_t* out_row, uint32_t* out_fid,
+                      uint32_t* out_exact, uint32_t* n_pairs) {
+  if (!h || !out_row ||
+      (parts && (!flags || !cnts || !fids || !n_pairs_part || !xss || !n_xs || !ovfs || !n_ovf)) ||
       (n && !out_exact))
     return -EINVAL;
   std::lock_guard<std::mutex> g(h->mmu);
   if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
   hipStream_t s = h->sync.stream;
-  // scratch: [pointer table 3 x parts | parts x (n+1) row words | n count words | total | scan]
+  // scratch: [pointer table 3 x parts | parts x (n+1) row words | widened ids of 24-bit parts |
+  //           n count words | total | scan]
+  uint64_t wide = 0;
+  for (uint32_t r = 0; r < parts; ++r) wide += (flags[r] & 2u) ? n_pairs_part[r] : 0;
   const uint64_t tw = scan_tmp_words(std::max<uint32_t>(n, 1));
   const uint64_t rows_off = (3ull * parts + 1) * 8;
-  const uint64_t need = rows_off + ((uint64_t)parts * (n + 1) + n + 2 + tw) * 4;
+  const uint64_t need = rows_off + ((uint64_t)parts * (n + 1) + wide + n + 2 + tw) * 4;
   if (int rc = grow_buf(h, h->d_merge, need)) return rc;
   uint8_t* d = (uint8_t*)h->d_merge.p;
   uint32_t* prow = (uint32_t*)(d + rows_off);
-  uint32_t* cnt = prow + (uint64_t)parts * (n + 1);
+  uint32_t* pid = prow + (uint64_t)parts * (n + 1);
+  uint32_t* cnt = pid + wide;
   uint32_t* total = cnt + n;
   uint32_t* tmp = total + 2;
-  for (uint32_t r = 0; r < parts; ++r)
-    HIPCHK(h, launch_wire_rows(cnt8s[r], (const uint2*)ovfs[r], n_ovf[r], n, cnt, tmp,
-                               prow + (uint64_t)r * (n + 1), s));
-  HIPCHK(h, launch_wire_exact((const uint2* const*)xss, n_xs, parts, n, out_exact, s));
-  // then the merge of emqxgm_merge over {part rows, part ids, the merged exact ids}
   std::vector<const uint32_t*> pp(3ull * parts);
   for (uint32_t r = 0; r < parts; ++r) {
+    HIPCHK(h, launch_wire_rows((const uint8_t*)cnts[r], flags[r], (const uint2*)ovfs[r], n_ovf[r], n,
+                               cnt, tmp, prow + (uint64_t)r * (n + 1), s));
     pp[3 * r] = prow + (uint64_t)r * (n + 1);
-    pp[3 * r + 1] = fids[r];
+    pp[3 * r + 1] = (const uint32_t*)fids[r];
     pp[3 * r + 2] = out_exact;
+    if (flags[r] & 2u) {
+      HIPCHK(h, launch_wire_ids((const uint8_t*)fids[r], n_pairs_part[r], pid, s));
+      pp[3 * r + 1] = pid;
+      pid += n_pairs_part[r];
+    }
   }
+  HIPCHK(h, launch_wire_exact((const uint2* const*)xss, n_xs, parts, n, out_exact, s));
+  // then the merge of emqxgm_merge over {part rows, part ids, the merged exact ids}
   if (parts) HIPCHK(h, hipMemcpyAsync(d, pp.data(), pp.size() * 8, hipMemcpyHostToDevice, s));
   HIPCHK(h, launch_merge((const uint32_t* const*)d, parts, n, cnt, tmp, out_row, out_fid, out_exact,
                          total, s));

@@ -228,14 +228,19 @@ hipError_t launch_export(const uint32_t* row, const uint32_t* fid, const uint32_
 hipError_t launch_merge(const uint32_t* const* parts, uint32_t np, uint32_t n, uint32_t* cnt,
                         uint32_t* tmp, uint32_t* orow, uint32_t* ofid, uint32_t* oexact,
                         uint32_t* total, hipStream_t s);
-// The compact wire form of a shard's result: u8 counts, mapped ids, sparse
-// (topic, exact id) xs and (topic, count) ovf lists; ctr[0] / ctr[1] = their lengths.
+// The compact wire form of a shard's result: counts (u8, or two bit planes with
+// flags & 1), mapped ids (u32, or u16 + u8 planes with flags & 2), sparse (topic, exact id) xs
+// and (topic, count) ovf lists; ctr[0] / ctr[1] = their lengths.
 hipError_t launch_wire_export(const uint32_t* row, const uint32_t* fid, const uint32_t* exact,
-                              uint32_t n, uint32_t pairs, const uint32_t* map, uint8_t* cnt8,
-                              uint32_t* ofid, uint2* xs, uint2* ovf, uint32_t* ctr, hipStream_t s);
-// a received part's row pointers [n+1] from its counts and overflow list (cnt/tmp scratch)
-hipError_t launch_wire_rows(const uint8_t* cnt8, const uint2* ovf, uint32_t novf, uint32_t n,
-                            uint32_t* cnt, uint32_t* tmp, uint32_t* row, hipStream_t s);
+                              uint32_t n, uint32_t pairs, const uint32_t* map, uint32_t flags,
+                              uint8_t* cnt, uint8_t* ofid, uint2* xs, uint2* ovf, uint32_t* ctr,
+                              hipStream_t s);
+// a received part's row pointers [n+1] from its counts and overflow list (counts/tmp scratch)
+hipError_t launch_wire_rows(const uint8_t* cnt, uint32_t flags, const uint2* ovf, uint32_t novf,
+                            uint32_t n, uint32_t* counts, uint32_t* tmp, uint32_t* row,
+                            hipStream_t s);
+// a received part's 24-bit ids widened to u32
+hipError_t launch_wire_ids(const uint8_t* fid, uint32_t pairs, uint32_t* out, hipStream_t s);
 // the merged exact ids [n]: NONE, then every part's (topic, id) entries (host arrays of device
 // pointers / lengths)
 hipError_t launch_wire_exact(const uint2* const* xs, const uint32_t* nx, uint32_t parts, uint32_t n,

@@ -258,10 +258,14 @@ __global__ __launch_bounds__(WG) void k_merge_fill(const uint32_t* const* parts,
   }
 }
 
-// ---- the compact wire form of a shard's result (filter-sharded layout over xGMI): per topic a
-// u8 pair count (255: the count is in the overflow list), the pairs' global ids in topic order,
-// and sparse lists of (topic, exact id) and (topic, count >= 255).  Sparse entries are appended
-// with one atomic per wave (their order is free: the root scatters them). ----
+// ---- the compact wire form of a shard's result (filter-sharded layout over xGMI): per-topic
+// pair counts (u8, or with WIRE_CNT2 two bit planes of 64 topics -- 2 bits a topic), the pairs'
+// global ids (u32, or with WIRE_ID24 a u16 low half + a u8 high byte), and sparse lists of
+// (topic, exact id) and (topic, count) for the counts the width cannot hold (>= 255 / >= 3).
+// Sparse entries are appended with one atomic per wave (their order is free: the root
+// scatters them). ----
+constexpr uint32_t WIRE_CNT2 = 1u, WIRE_ID24 = 2u;  // include/emqx_gpumatch.h EMQXGM_WIRE_*
+
 __device__ __forceinline__ uint32_t wave_append(bool v, uint32_t* ctr) {
   const uint64_t m = __ballot(v);
   uint32_t base = 0;
@@ -273,30 +277,66 @@ __device__ __forceinline__ uint32_t wave_append(bool v, uint32_t* ctr) {
 __global__ __launch_bounds__(WG) void k_wire_export(const uint32_t* row, const uint32_t* fid,
                                                     const uint32_t* exact, uint32_t n,
                                                     uint32_t pairs, const uint32_t* map,
-                                                    uint8_t* cnt8, uint32_t* ofid, uint2* xs,
-                                                    uint2* ovf, uint32_t* ctr) {
-  const uint32_t m = max(n, pairs);
-  // every lane of a wave runs the same trip count (wave_append is a wave-wide ballot)
+                                                    uint32_t flags, uint8_t* cnt, uint8_t* ofid,
+                                                    uint2* xs, uint2* ovf, uint32_t* ctr) {
   const uint32_t stride = gridDim.x * WG;
-  const uint32_t trips = (m + stride - 1) / stride;
-  for (uint32_t k = 0; k < trips; ++k) {
-    const uint32_t i = k * stride + blockIdx.x * WG + threadIdx.x;
+  const bool c2 = (flags & WIRE_CNT2) != 0;
+  const uint32_t cap = c2 ? 3u : 255u;
+  // topics in wave-aligned groups of 64 (a count plane word is one wave's ballot); every lane
+  // of a block runs the same trip count (wave_append is a wave-wide ballot)
+  const uint32_t n64 = (n + 63u) & ~63u;
+  for (uint32_t base = blockIdx.x * WG; base < n64; base += stride) {
+    const uint32_t i = base + threadIdx.x;
     const bool tv = i < n;
     const uint32_t c = tv ? row[i + 1] - row[i] : 0u;
     const uint32_t e = tv ? exact[i] : NONE;
-    if (tv) cnt8[i] = (uint8_t)min(c, 255u);
-    const bool big = tv && c >= 255u, hit = tv && e != NONE;
+    if (c2) {
+      const uint32_t code = min(c, 3u);
+      const uint64_t p0 = __ballot(code & 1u), p1 = __ballot((code >> 1) & 1u);
+      if (lane_id() == 0 && i < n64 && i - lane_id() < n) {
+        uint64_t* pl = (uint64_t*)cnt + 2ull * (i >> 6);
+        pl[0] = p0;
+        pl[1] = p1;
+      }
+    } else if (tv) {
+      cnt[i] = (uint8_t)min(c, 255u);
+    }
+    const bool big = tv && c >= cap, hit = tv && e != NONE;
     const uint32_t po = wave_append(big, &ctr[1]);
     if (big) ovf[po] = make_uint2(i, c);
     const uint32_t px = wave_append(hit, &ctr[0]);
     if (hit) xs[px] = make_uint2(i, map ? map[e] : e);
-    if (i < pairs) ofid[i] = map ? map[fid[i]] : fid[i];
+  }
+  for (uint32_t j = blockIdx.x * WG + threadIdx.x; j < pairs; j += stride) {
+    const uint32_t id = map ? map[fid[j]] : fid[j];
+    if (flags & WIRE_ID24) {
+      ((uint16_t*)ofid)[j] = (uint16_t)id;
+      ofid[2ull * pairs + j] = (uint8_t)(id >> 16);
+    } else {
+      ((uint32_t*)ofid)[j] = id;
+    }
   }
 }
 
-// one part's counts from its wire form (overflow entries patched in by k_wire_patch)
-__global__ __launch_bounds__(WG) void k_wire_counts(const uint8_t* cnt8, uint32_t n, uint32_t* cnt) {
-  for (uint32_t i = blockIdx.x * WG + threadIdx.x; i < n; i += gridDim.x * WG) cnt[i] = cnt8[i];
+// one part's counts from its wire form (counts its width cannot hold are patched in from the
+// overflow list by k_wire_patch)
+__global__ __launch_bounds__(WG) void k_wire_counts(const uint8_t* cnt, uint32_t flags, uint32_t n,
+                                                    uint32_t* out) {
+  for (uint32_t i = blockIdx.x * WG + threadIdx.x; i < n; i += gridDim.x * WG) {
+    if (flags & WIRE_CNT2) {
+      const uint64_t* pl = (const uint64_t*)cnt + 2ull * (i >> 6);
+      const uint32_t b = i & 63u;
+      out[i] = (uint32_t)((pl[0] >> b) & 1ull) | ((uint32_t)((pl[1] >> b) & 1ull) << 1);
+    } else {
+      out[i] = cnt[i];
+    }
+  }
+}
+
+// a part's 24-bit ids widened to u32
+__global__ __launch_bounds__(WG) void k_wire_ids(const uint8_t* fid, uint32_t pairs, uint32_t* out) {
+  for (uint32_t j = blockIdx.x * WG + threadIdx.x; j < pairs; j += gridDim.x * WG)
+    out[j] = (uint32_t)((const uint16_t*)fid)[j] | ((uint32_t)fid[2ull * pairs + j] << 16);
 }
 
 // dst[e.x] = e.y for the m sparse entries (overflow counts; exact ids)
@@ -581,25 +621,35 @@ hipError_t launch_merge(const uint32_t* const* parts, uint32_t np, uint32_t n, u
 }
 
 hipError_t launch_wire_export(const uint32_t* row, const uint32_t* fid, const uint32_t* exact,
-                              uint32_t n, uint32_t pairs, const uint32_t* map, uint8_t* cnt8,
-                              uint32_t* ofid, uint2* xs, uint2* ovf, uint32_t* ctr, hipStream_t s) {
+                              uint32_t n, uint32_t pairs, const uint32_t* map, uint32_t flags,
+                              uint8_t* cnt, uint8_t* ofid, uint2* xs, uint2* ovf, uint32_t* ctr,
+                              hipStream_t s) {
   hipError_t e = hipMemsetAsync(ctr, 0, 8, s);
   if (e != hipSuccess) return e;
-  const uint64_t m = std::max<uint64_t>(n, pairs);
+  const uint64_t m = std::max<uint64_t>((n + 63ull) & ~63ull, pairs);
   if (m == 0) return hipSuccess;
   hipLaunchKernelGGL(k_wire_export, dim3(grid_for(m, 8192)), dim3(WG), 0, s, row, fid, exact, n,
-                     pairs, map, cnt8, ofid, xs, ovf, ctr);
+                     pairs, map, flags, cnt, ofid, xs, ovf, ctr);
   return hipGetLastError();
 }
 
-hipError_t launch_wire_rows(const uint8_t* cnt8, const uint2* ovf, uint32_t novf, uint32_t n,
-                            uint32_t* cnt, uint32_t* tmp, uint32_t* row, hipStream_t s) {
+hipError_t launch_wire_rows(const uint8_t* cnt, uint32_t flags, const uint2* ovf, uint32_t novf,
+                            uint32_t n, uint32_t* counts, uint32_t* tmp, uint32_t* row,
+                            hipStream_t s) {
   if (n) {
-    hipLaunchKernelGGL(k_wire_counts, dim3(grid_for(n, 8192)), dim3(WG), 0, s, cnt8, n, cnt);
+    hipLaunchKernelGGL(k_wire_counts, dim3(grid_for(n, 8192)), dim3(WG), 0, s, cnt, flags, n,
+                       counts);
     if (novf)
-      hipLaunchKernelGGL(k_wire_patch, dim3(grid_for(novf, 8192)), dim3(WG), 0, s, ovf, novf, cnt);
+      hipLaunchKernelGGL(k_wire_patch, dim3(grid_for(novf, 8192)), dim3(WG), 0, s, ovf, novf,
+                         counts);
   }
-  return launch_scan(cnt, row, n, tmp, nullptr, s);
+  return launch_scan(counts, row, n, tmp, nullptr, s);
+}
+
+hipError_t launch_wire_ids(const uint8_t* fid, uint32_t pairs, uint32_t* out, hipStream_t s) {
+  if (pairs)
+    hipLaunchKernelGGL(k_wire_ids, dim3(grid_for(pairs, 8192)), dim3(WG), 0, s, fid, pairs, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_wire_exact(const uint2* const* xs, const uint32_t* nx, uint32_t parts, uint32_t n,

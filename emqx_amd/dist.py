@@ -90,64 +90,83 @@ def broadcast_batch(tbytes: Optional[torch.Tensor], toff: Optional[torch.Tensor]
     return tbytes.to(device), toff.to(device)
 
 
+WIRE_CNT2, WIRE_ID24 = 1, 2  # include/emqx_gpumatch.h EMQXGM_WIRE_*
+
+
+def wire_flags(n: int, pairs: int, n_global: int) -> int:
+    """The wire form for a result: 2-bit counts when pairs are sparse (at most one per two
+    topics: few counts reach 3), 24-bit ids when every global id fits."""
+    return (WIRE_CNT2 if 2 * pairs <= n else 0) | (WIRE_ID24 if n_global <= (1 << 24) else 0)
+
+
+def wire_sizes(flags: int, n: int, pairs: int) -> Tuple[int, int]:
+    """Bytes of the count and id sections."""
+    cnt = 16 * ((n + 63) // 64) if flags & WIRE_CNT2 else n
+    return cnt, (3 if flags & WIRE_ID24 else 4) * pairs
+
+
 @dataclass
 class WirePart:
-    """One shard's result in the compact wire form (emqxgm_export_wire): u8 pair counts per
-    topic (255: see ovf), the pairs' global ids, (topic, exact id) and (topic, count) pairs."""
-    cnt8: torch.Tensor  # uint8 [n]
-    fid: torch.Tensor   # int32 [pairs]
+    """One shard's result in the compact wire form (emqxgm_export_wire): pair counts (u8 or two
+    bit planes), the pairs' global ids (u32 or u16 + u8 planes), and (topic, exact id) /
+    (topic, count) pairs of the topics that equal a route key / outgrow the count width."""
+    flags: int
+    pairs: int
+    cnt: torch.Tensor   # uint8 [wire_sizes[0]]
+    fid: torch.Tensor   # uint8 [wire_sizes[1]]
     xs: torch.Tensor    # int32 [2 * nx]
     ovf: torch.Tensor   # int32 [2 * novf]
 
     def nbytes(self) -> int:
-        return sum(int(t.numel()) * t.element_size() for t in (self.cnt8, self.fid, self.xs, self.ovf))
+        return sum(int(t.numel()) * t.element_size() for t in (self.cnt, self.fid, self.xs, self.ovf))
 
 
 def gather_wire_to_root(part: WirePart, root: int = 0, group=None) -> Optional[List[WirePart]]:
-    """Each rank's wire part to `root`: the (pairs, exact, overflow) lengths with one all_gather
-    of 3 x G integers (the root's one host synchronisation: it sizes the receives), then sized
-    point-to-point receives on the root only -- per non-root rank n + 4 pairs + 8 (exact hits +
-    overflows) bytes cross xGMI, against 8 n + 4 pairs for dense u32 row pointers and exact ids.
-    Returns on the root the G parts in rank order (its own included), None elsewhere."""
+    """Each rank's wire part to `root`: (flags, pairs, exact, overflow) with one all_gather of
+    4 x G integers (the root's one host synchronisation: it sizes the receives), then sized
+    point-to-point receives on the root only.  Per non-root rank a 2-bit-count, 24-bit-id part
+    is n / 4 + 3 pairs + 8 (exact hits + overflows) bytes, against 8 n + 4 pairs for dense u32
+    row pointers and exact ids.  Returns on the root the G parts in rank order (its own
+    included), None elsewhere."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    dev = part.cnt8.device
+    dev = part.cnt.device
     cpu = _comm_on_cpu(group)
     cdev = "cpu" if cpu else dev
-    lens = torch.tensor([part.fid.numel(), part.xs.numel() // 2, part.ovf.numel() // 2],
-                        dtype=torch.int64, device=cdev)
-    alll = [torch.zeros(3, dtype=torch.int64, device=cdev) for _ in range(world)]
+    lens = torch.tensor([part.flags, part.pairs, part.xs.numel() // 2, part.ovf.numel() // 2,
+                         part.cnt.numel()], dtype=torch.int64, device=cdev)
+    alll = [torch.zeros(5, dtype=torch.int64, device=cdev) for _ in range(world)]
     dist.all_gather(alll, lens, group=group)
     if rank != root:
-        ops = [dist.P2POp(dist.isend, part.cnt8.to(cdev), root, group)]
-        for t in (part.fid, part.xs, part.ovf):
+        ops = []
+        for t in (part.cnt, part.fid, part.xs, part.ovf):
             if t.numel():
                 ops.append(dist.P2POp(dist.isend, t.to(cdev), root, group))
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
         return None
     ls = torch.stack(alll).tolist()
-    n = part.cnt8.numel()
     parts: List[WirePart] = []
     ops = []
     for r in range(world):
         if r == root:
             parts.append(part)
             continue
-        p, nx, no = (int(x) for x in ls[r])
-        q = WirePart(torch.empty(n, dtype=torch.uint8, device=cdev),
-                     torch.empty(p, dtype=torch.int32, device=cdev),
+        fl, p, nx, no, nc = (int(x) for x in ls[r])
+        q = WirePart(fl, p, torch.empty(nc, dtype=torch.uint8, device=cdev),
+                     torch.empty((3 if fl & WIRE_ID24 else 4) * p, dtype=torch.uint8, device=cdev),
                      torch.empty(2 * nx, dtype=torch.int32, device=cdev),
                      torch.empty(2 * no, dtype=torch.int32, device=cdev))
-        ops.append(dist.P2POp(dist.irecv, q.cnt8, r, group))
-        for t in (q.fid, q.xs, q.ovf):
+        for t in (q.cnt, q.fid, q.xs, q.ovf):
             if t.numel():
                 ops.append(dist.P2POp(dist.irecv, t, r, group))
         parts.append(q)
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
-    return [WirePart(*(t.to(dev) for t in (q.cnt8, q.fid, q.xs, q.ovf))) for q in parts]
+    return [WirePart(q.flags, q.pairs, *(t.to(dev) for t in (q.cnt, q.fid, q.xs, q.ovf)))
+            for q in parts]
 
 
 @dataclass
@@ -180,16 +199,17 @@ def merge_parts(eng, parts: Sequence[Part], n: int) -> Merged:
 
 def merge_wire(eng, parts: Sequence[WirePart], n: int) -> Merged:
     """Merge the shards' wire parts topic by topic on the device (emqxgm_merge_wire)."""
-    dev = parts[0].cnt8.device
+    dev = parts[0].cnt.device
     if dev.type != "cuda":
         raise RuntimeError("merge_wire runs on the GPU (emqxgm_merge_wire); there is no CPU merge")
-    total = sum(int(p.fid.numel()) for p in parts)
+    total = sum(p.pairs for p in parts)
     row = torch.empty(n + 1, dtype=torch.int32, device=dev)
     fid = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
     ex = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
     torch.cuda.current_stream(dev).synchronize()  # the parts came in on torch's streams
     ptr = lambda t: t.data_ptr() if t.numel() else 0  # noqa: E731
-    got = eng.merge_wire([ptr(p.cnt8) for p in parts], [ptr(p.fid) for p in parts],
+    got = eng.merge_wire([p.flags for p in parts], [ptr(p.cnt) for p in parts],
+                         [ptr(p.fid) for p in parts], [p.pairs for p in parts],
                          [ptr(p.xs) for p in parts], [p.xs.numel() // 2 for p in parts],
                          [ptr(p.ovf) for p in parts], [p.ovf.numel() // 2 for p in parts], n,
                          row.data_ptr(), fid.data_ptr() if total else 0, ex.data_ptr())
@@ -206,22 +226,24 @@ class ShardedMatcher:
     then batch k's result goes to rank 0 in the wire form and is merged there.  The batch shape
     (bytes, topics) is given to every rank, so no size message precedes a broadcast."""
 
-    def __init__(self, eng, gid_map: torch.Tensor, device, group=None, root: int = 0):
+    def __init__(self, eng, gid_map: torch.Tensor, device, group=None, root: int = 0,
+                 n_global: int = 1 << 32):
         self.eng = eng
         self.gid_map = gid_map
         self.device = device
         self.group = group
         self.root = root
+        self.n_global = n_global  # global filter ids < n_global (24-bit ids when <= 2^24)
         self._wire = None
         self.bytes_to_root = 0   # per step, summed over the ranks that send (set on the root)
         self.bytes_broadcast = 0
 
     def _wire_bufs(self, n: int, pairs: int):
-        cap_n, cap_p = (0, 0) if self._wire is None else (self._wire[0].numel(), self._wire[1].numel())
+        cap_n, cap_p = (0, 0) if self._wire is None else (self._wire[2].numel() // 2, self._wire[1].numel() // 4)
         if n > cap_n or pairs > cap_p:
-            n2, p2 = max(n, cap_n, 1), max(pairs, cap_p, 1)
-            self._wire = (torch.empty(n2, dtype=torch.uint8, device=self.device),
-                          torch.empty(p2, dtype=torch.int32, device=self.device),
+            n2, p2 = max(n, cap_n, 64), max(pairs, cap_p, 1)
+            self._wire = (torch.empty(n2 + 64, dtype=torch.uint8, device=self.device),
+                          torch.empty(4 * p2, dtype=torch.uint8, device=self.device),
                           torch.empty(2 * n2, dtype=torch.int32, device=self.device),
                           torch.empty(2 * n2, dtype=torch.int32, device=self.device))
         return self._wire
@@ -243,11 +265,13 @@ class ShardedMatcher:
 
     def _finish(self, ticket, n: int) -> Optional[Merged]:
         r = self.eng.match_device_wait(ticket)
-        cnt8, fid, xs, ovf = self._wire_bufs(n, r.n_pairs)
-        nx, no = self.eng.export_wire(r, self.gid_map.data_ptr(), cnt8.data_ptr() if n else 0,
+        cnt, fid, xs, ovf = self._wire_bufs(n, r.n_pairs)
+        fl = wire_flags(n, r.n_pairs, self.n_global)
+        nc, nf = wire_sizes(fl, n, r.n_pairs)
+        nx, no = self.eng.export_wire(r, self.gid_map.data_ptr(), fl, cnt.data_ptr() if n else 0,
                                       fid.data_ptr() if r.n_pairs else 0, xs.data_ptr(),
                                       ovf.data_ptr())
-        part = WirePart(cnt8[:n], fid[:r.n_pairs], xs[:2 * nx], ovf[:2 * no])
+        part = WirePart(fl, r.n_pairs, cnt[:nc], fid[:nf], xs[:2 * nx], ovf[:2 * no])
         parts = gather_wire_to_root(part, self.root, self.group)
         if parts is None:
             return None

@@ -125,9 +125,10 @@ SYMBOLS = {
     "emqxgm_walk_census_levels": (C.c_int, [_P, _U64P, C.c_uint32]),
     "emqxgm_export": (C.c_int, [_P, C.POINTER(_DevOut), _P, _P, _P, _P]),
     "emqxgm_merge": (C.c_int, [_P, C.c_uint32, _P, _P, _P, C.c_uint32, _P, _P, _P, _U32P]),
-    "emqxgm_export_wire": (C.c_int, [_P, C.POINTER(_DevOut), _P, _P, _P, _P, _P, _U32P]),
-    "emqxgm_merge_wire": (C.c_int, [_P, C.c_uint32, _P, _P, _P, _P, _P, _P, C.c_uint32, _P, _P, _P,
-                                    _U32P]),
+    "emqxgm_export_wire": (C.c_int, [_P, C.POINTER(_DevOut), _P, C.c_uint32, _P, _P, _P, _P,
+                                     _U32P]),
+    "emqxgm_merge_wire": (C.c_int, [_P, C.c_uint32, _P, _P, _P, _P, _P, _P, _P, _P, C.c_uint32,
+                                    _P, _P, _P, _U32P]),
     "emqxgm_route_add": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32]),
     "emqxgm_route_delete": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32]),
     "emqxgm_set_local_node": (C.c_int, [_P, C.c_uint32]),
@@ -512,7 +513,10 @@ class Engine:
                                            C.byref(tot)), "merge")
         return int(tot.value)
 
-    def export_wire(self, r: "DeviceResult", id_map: int, cnt8: int, fid: int, xs: int,
+    WIRE_CNT2 = 1  # EMQXGM_WIRE_CNT2
+    WIRE_ID24 = 2  # EMQXGM_WIRE_ID24
+
+    def export_wire(self, r: "DeviceResult", id_map: int, flags: int, cnt: int, fid: int, xs: int,
                     ovf: int) -> Tuple[int, int]:
         """emqxgm_export_wire: a device-resident result in its compact wire form (device
         pointers); returns (exact entries, overflow entries)."""
@@ -520,23 +524,25 @@ class Engine:
                     r.n_words or None)
         c = (C.c_uint32 * 2)()
         self._check(self._lib.emqxgm_export_wire(self._h, C.byref(o), C.c_void_p(id_map or None),
-                                                 C.c_void_p(cnt8 or None), C.c_void_p(fid or None),
-                                                 C.c_void_p(xs or None), C.c_void_p(ovf or None), c),
-                    "export_wire")
+                                                 flags, C.c_void_p(cnt or None),
+                                                 C.c_void_p(fid or None), C.c_void_p(xs or None),
+                                                 C.c_void_p(ovf or None), c), "export_wire")
         return int(c[0]), int(c[1])
 
-    def merge_wire(self, cnt8s: Sequence[int], fids: Sequence[int], xss: Sequence[int],
-                   n_xs: Sequence[int], ovfs: Sequence[int], n_ovf: Sequence[int], n: int,
-                   out_row: int, out_fid: int, out_exact: int) -> int:
+    def merge_wire(self, flags: Sequence[int], cnts: Sequence[int], fids: Sequence[int],
+                   pairs: Sequence[int], xss: Sequence[int], n_xs: Sequence[int],
+                   ovfs: Sequence[int], n_ovf: Sequence[int], n: int, out_row: int, out_fid: int,
+                   out_exact: int) -> int:
         """emqxgm_merge_wire: merge per-shard wire results (device pointers); returns pairs."""
-        k = len(cnt8s)
+        k = len(cnts)
         arr = C.c_void_p * max(k, 1)
         u32 = C.c_uint32 * max(k, 1)
         tot = C.c_uint32(0)
+        nz = lambda xs: arr(*[x or None for x in xs])  # noqa: E731
         self._check(self._lib.emqxgm_merge_wire(
-            self._h, k, arr(*cnt8s), arr(*[f or None for f in fids]), arr(*[x or None for x in xss]),
-            u32(*n_xs), arr(*[o or None for o in ovfs]), u32(*n_ovf), n, C.c_void_p(out_row),
-            C.c_void_p(out_fid or None), C.c_void_p(out_exact or None), C.byref(tot)), "merge_wire")
+            self._h, k, u32(*flags), nz(cnts), nz(fids), u32(*pairs), nz(xss), u32(*n_xs),
+            nz(ovfs), u32(*n_ovf), n, C.c_void_p(out_row), C.c_void_p(out_fid or None),
+            C.c_void_p(out_exact or None), C.byref(tot)), "merge_wire")
         return int(tot.value)
 
     def walk_census(self, d_bytes: int, d_off: int, n: int, bytes_len: int) -> dict:

@@ -398,18 +398,26 @@ int emqxgm_merge(emqxgm_t* h, uint32_t parts, const uint32_t* const* rows,
                  uint32_t* out_row, uint32_t* out_fid, uint32_t* out_exact, uint32_t* n_pairs);
 
 /* The compact wire form of a shard's result for the exchange to the root:
- * cnt8[n] = per-topic pair count (255: the count is in ovf), fid[n_pairs] = the pairs' ids mapped
- * through id_map (NULL = identity), xs = (topic, exact id) pairs of the topics that equal a route
- * key, ovf = (topic, count) pairs of the topics with >= 255 pairs; xs and ovf are device arrays
- * of 2 x n u32, counts[0] / counts[1] = their entries.  emqxgm_merge_wire merges `parts` such
- * results (host arrays of device pointers / lengths) into one CSR exactly as emqxgm_merge does.
- * Both return when the device work is complete. */
-int emqxgm_export_wire(emqxgm_t* h, const emqxgm_dev_out* r, const uint32_t* id_map, uint8_t* cnt8,
-                       uint32_t* fid, uint32_t* xs, uint32_t* ovf, uint32_t counts[2]);
-int emqxgm_merge_wire(emqxgm_t* h, uint32_t parts, const uint8_t* const* cnt8s,
-                      const uint32_t* const* fids, const uint32_t* const* xss, const uint32_t* n_xs,
-                      const uint32_t* const* ovfs, const uint32_t* n_ovf, uint32_t n,
-                      uint32_t* out_row, uint32_t* out_fid, uint32_t* out_exact, uint32_t* n_pairs);
+ *   cnt  per-topic pair counts: n u8 (255 = in ovf), or with EMQXGM_WIRE_CNT2 two bit planes per
+ *        64 topics (16 B per 64 topics, 2 bits a topic; 3 = in ovf) -- for sparse results;
+ *   fid  the pairs' ids mapped through id_map (NULL = identity): n_pairs u32, or with
+ *        EMQXGM_WIRE_ID24 (every id < 2^24) n_pairs u16 low halves then n_pairs u8 high bytes;
+ *   xs   (topic, exact id) u32 pairs of the topics that equal a route key;
+ *   ovf  (topic, count) u32 pairs of the counts the count width cannot hold.
+ * xs and ovf are device arrays of 2 x n u32; counts[0] / counts[1] = their entries.
+ * emqxgm_merge_wire merges `parts` such results (host arrays of device pointers, flags and
+ * lengths) into one CSR exactly as emqxgm_merge does.  Both return when the device work is
+ * complete. */
+#define EMQXGM_WIRE_CNT2 1u
+#define EMQXGM_WIRE_ID24 2u
+int emqxgm_export_wire(emqxgm_t* h, const emqxgm_dev_out* r, const uint32_t* id_map,
+                       uint32_t flags, void* cnt, void* fid, uint32_t* xs, uint32_t* ovf,
+                       uint32_t counts[2]);
+int emqxgm_merge_wire(emqxgm_t* h, uint32_t parts, const uint32_t* flags, const void* const* cnts,
+                      const void* const* fids, const uint32_t* n_pairs_part,
+                      const uint32_t* const* xss, const uint32_t* n_xs, const uint32_t* const* ovfs,
+                      const uint32_t* n_ovf, uint32_t n, uint32_t* out_row, uint32_t* out_fid,
+                      uint32_t* out_exact, uint32_t* n_pairs);
 
 /* Diagnostic pass (instrumented walk kernel, not the production launch): runs the device
  * match and returns out[0] = trie states matched (SURVEY 8d S(t) summed over the batch),

@@ -114,8 +114,9 @@ hipError_t launch_copy_out(const CopyOut&, const CopyOut&, const CopyOut&, hipSt
 hipError_t launch_export(const uint32_t*, const uint32_t*, const uint32_t*, uint32_t, uint32_t, const uint32_t*, uint32_t*, uint32_t*, uint32_t*, hipStream_t) { NOT_HERE; }
 hipError_t launch_merge(const uint32_t* const*, uint32_t, uint32_t, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, hipStream_t) { NOT_HERE; }
 
-hipError_t launch_wire_export(const uint32_t*, const uint32_t*, const uint32_t*, uint32_t, uint32_t, const uint32_t*, uint8_t*, uint32_t*, uint2*, uint2*, uint32_t*, hipStream_t) { NOT_HERE; }
-hipError_t launch_wire_rows(const uint8_t*, const uint2*, uint32_t, uint32_t, uint32_t*, uint32_t*, uint32_t*, hipStream_t) { NOT_HERE; }
+hipError_t launch_wire_export(const uint32_t*, const uint32_t*, const uint32_t*, uint32_t, uint32_t, const uint32_t*, uint32_t, uint8_t*, uint8_t*, uint2*, uint2*, uint32_t*, hipStream_t) { NOT_HERE; }
+hipError_t launch_wire_rows(const uint8_t*, uint32_t, const uint2*, uint32_t, uint32_t, uint32_t*, uint32_t*, uint32_t*, hipStream_t) { NOT_HERE; }
+hipError_t launch_wire_ids(const uint8_t*, uint32_t, uint32_t*, hipStream_t) { NOT_HERE; }
 hipError_t launch_wire_exact(const uint2* const*, const uint32_t*, uint32_t, uint32_t, uint32_t*, hipStream_t) { NOT_HERE; }
 hipError_t launch_filter_len(const uint32_t*, uint32_t, const uint64_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, hipStream_t) { NOT_HERE; }
 hipError_t launch_filter_gather(const uint32_t*, uint32_t, const uint64_t*, const uint8_t*, const uint32_t*, uint8_t*, hipStream_t) { NOT_HERE; }

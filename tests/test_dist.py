@@ -60,29 +60,55 @@ def parts_len(p):
     return int(p[0][-1])
 
 
-def _ref_export_wire(row, gid, exg):
-    """numpy restatement of emqxgm_export_wire (gm_kernels.hip k_wire_export): u8 counts (255:
-    see ovf), ids, (topic, exact id) and (topic, count >= 255) pairs (any order)."""
+def _ref_export_wire(row, gid, exg, flags=0):
+    """numpy restatement of emqxgm_export_wire (gm_kernels.hip k_wire_export): counts as u8
+    (255: see ovf) or, flags & 1, as two bit planes of 64 topics (3: see ovf); ids as u32 or,
+    flags & 2, as u16 low halves then u8 high bytes; (topic, exact id) and (topic, count) pairs
+    (any order).  Returns (cnt bytes, fid bytes, xs, ovf)."""
     cnt = np.diff(row.astype(np.int64))
-    t = np.arange(len(cnt), dtype=np.int64)
-    hit, big = exg != 0xFFFFFFFF, cnt >= 255
+    n = len(cnt)
+    t = np.arange(n, dtype=np.int64)
+    cap = 3 if flags & 1 else 255
+    hit, big = exg != 0xFFFFFFFF, cnt >= cap
     xs = np.stack([t[hit], exg[hit].astype(np.int64)], 1).reshape(-1)
     ovf = np.stack([t[big], cnt[big]], 1).reshape(-1)
-    return (np.minimum(cnt, 255).astype(np.uint8), gid.astype(np.uint32), xs.astype(np.uint32),
-            ovf.astype(np.uint32))
+    if flags & 1:
+        code = np.zeros(((n + 63) // 64) * 64, np.uint64)
+        code[:n] = np.minimum(cnt, 3)
+        g = code.reshape(-1, 64)
+        w = (np.uint64(1) << np.arange(64, dtype=np.uint64))
+        p0 = ((g & np.uint64(1)) * w).sum(1, dtype=np.uint64)
+        p1 = (((g >> np.uint64(1)) & np.uint64(1)) * w).sum(1, dtype=np.uint64)
+        cb = np.stack([p0, p1], 1).reshape(-1).view(np.uint8)
+    else:
+        cb = np.minimum(cnt, 255).astype(np.uint8)
+    gid = gid.astype(np.uint32)
+    fb = (np.concatenate([(gid & 0xFFFF).astype(np.uint16).view(np.uint8), (gid >> 16).astype(np.uint8)])
+          if flags & 2 else gid.view(np.uint8))
+    return cb, fb, xs.astype(np.uint32), ovf.astype(np.uint32)
 
 
 def _ref_merge_wire(parts, n):
-    """numpy restatement of emqxgm_merge_wire: each part's rows from its counts and overflow
-    list, the exact ids from the sparse pairs, then _ref_merge."""
+    """numpy restatement of emqxgm_merge_wire over (flags, pairs, cnt bytes, fid bytes, xs, ovf)
+    parts: each part's rows from its counts and overflow list, its ids widened, the exact ids
+    from the sparse pairs, then _ref_merge."""
     dense = []
     ex = np.full(n, 0xFFFFFFFF, np.uint32)
-    for cnt8, fid, xs, ovf in parts:
-        cnt = cnt8.astype(np.int64)
+    for flags, pairs, cb, fb, xs, ovf in parts:
+        if flags & 1:
+            pl = cb.view(np.uint64).reshape(-1, 2)
+            b = np.arange(n, dtype=np.uint64)
+            g = (b >> np.uint64(6)).astype(np.int64)
+            sh = b & np.uint64(63)
+            cnt = (((pl[g, 0] >> sh) & np.uint64(1)) | (((pl[g, 1] >> sh) & np.uint64(1)) << np.uint64(1))).astype(np.int64)
+        else:
+            cnt = cb.astype(np.int64)
         o = ovf.reshape(-1, 2).astype(np.int64)
         cnt[o[:, 0]] = o[:, 1]
         row = np.zeros(n + 1, np.int64)
         np.cumsum(cnt, out=row[1:])
+        fid = (fb[:2 * pairs].view(np.uint16).astype(np.uint32) | (fb[2 * pairs:].astype(np.uint32) << 16)
+               if flags & 2 else fb.view(np.uint32))
         x = xs.reshape(-1, 2).astype(np.int64)
         ex[x[:, 0]] = x[:, 1]
         dense.append((row, fid))
@@ -90,9 +116,11 @@ def _ref_merge_wire(parts, n):
     return _ref_merge([(i32(r), i32(f), i32(ex)) for r, f in dense], n)
 
 
-def test_wire_restatement_round_trip():
-    """Counts of 255 and more go through the overflow list; exact ids through the sparse pairs."""
-    rng = np.random.default_rng(5)
+@pytest.mark.parametrize("flags", [0, 1, 2, 3])
+def test_wire_restatement_round_trip(flags):
+    """Counts the width cannot hold go through the overflow list; exact ids through the sparse
+    pairs; 24-bit ids through the two planes."""
+    rng = np.random.default_rng(5 + flags)
     n = 3000
     parts_dense, parts_wire = [], []
     owner = rng.integers(-1, 3, n)
@@ -101,14 +129,14 @@ def test_wire_restatement_round_trip():
         cnt[rng.integers(0, n, 20)] = rng.integers(250, 700, 20)
         row = np.zeros(n + 1, np.uint32)
         np.cumsum(cnt, out=row[1:])
-        gid = rng.integers(0, 10 ** 6, int(row[-1])).astype(np.uint32)
+        gid = rng.integers(0, 1 << 24 if flags & 2 else 1 << 32, int(row[-1])).astype(np.uint32)
         exg = np.where(owner == r, rng.integers(0, 10 ** 6, n), 0xFFFFFFFF).astype(np.uint32)
         i32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint32).view(np.int32))  # noqa: E731
         parts_dense.append((i32(row), i32(gid), i32(exg)))
-        parts_wire.append(_ref_export_wire(row, gid, exg))
+        parts_wire.append((flags, len(gid)) + _ref_export_wire(row, gid, exg, flags))
     a, b = _ref_merge(parts_dense, n), _ref_merge_wire(parts_wire, n)
     assert all(np.array_equal(x, y) for x, y in zip(a, b))
-    assert sum(len(w[3]) for w in parts_wire) > 0  # overflow entries were exercised
+    assert sum(len(w[5]) for w in parts_wire) > 0  # overflow entries were exercised
 
 
 def _worker(rank, world, port, q):
@@ -132,19 +160,19 @@ def _worker(rank, world, port, q):
         gid = mine[ids.astype(np.int64)].astype(np.uint32)
         exg = np.where(ex == D.NONE, D.NONE, mine[np.minimum(ex, len(mine) - 1).astype(np.int64)])
         i32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint32).view(np.int32))  # noqa: E731
-        cnt8, fid, xs, ovf = _ref_export_wire(row, gid, exg.astype(np.uint32))
-        part = D.WirePart(torch.from_numpy(cnt8), i32(fid), i32(xs), i32(ovf))
+        fl = D.wire_flags(w.nt, len(gid), w.nf) if rank == 0 else 3  # rank 1: the sparse form
+        cb, fb, xs, ovf = _ref_export_wire(row, gid, exg.astype(np.uint32), fl)
+        part = D.WirePart(fl, len(gid), torch.from_numpy(cb), torch.from_numpy(fb), i32(xs), i32(ovf))
         parts = D.gather_wire_to_root(part)
         if rank != 0:
             assert parts is None
         else:
             u = lambda t: t.numpy().view(np.uint32) if t.dtype == torch.int32 else t.numpy()  # noqa: E731
-            merged = _ref_merge_wire([tuple(u(t) for t in (p.cnt8, p.fid, p.xs, p.ovf))
+            merged = _ref_merge_wire([(p.flags, p.pairs) + tuple(u(t) for t in (p.cnt, p.fid, p.xs, p.ovf))
                                       for p in parts], w.nt)
             p1 = parts[1]
-            sent = p1.nbytes()
-            assert sent == w.nt + 4 * p1.fid.numel() + 4 * (p1.xs.numel() + p1.ovf.numel())
-            assert sent < 4 * (w.nt + 1) + 4 * w.nt + 4 * p1.fid.numel()  # the dense CSR + exact
+            assert p1.flags == 3 and p1.nbytes() == (16 * ((w.nt + 63) // 64) + 3 * p1.pairs
+                                                     + 4 * (p1.xs.numel() + p1.ovf.numel()))
             full = RefIndex(True)
             full.add_many(w.fbytes, w.foff, 2 + w.fwild)
             frow, fids, fex = full.match(w.tbytes, w.toff)

@@ -49,28 +49,30 @@ def test_merge_matches_reference(emqx):
     eng.close()
 
 
-def test_merge_wire_matches_reference(emqx):
-    """Wire parts (counts >= 255 through the overflow list) merged on the device equal the
-    restatement, and equal emqxgm_merge over the same parts in dense form."""
+@pytest.mark.parametrize("flags", [0, 1, 2, 3])
+def test_merge_wire_matches_reference(emqx, flags):
+    """Wire parts (counts beyond the width through the overflow list, 24-bit id planes) merged on
+    the device equal the restatement, and equal emqxgm_merge over the same parts in dense form."""
     from emqx_amd import dist as D
     eng = emqx.Engine()
-    rng = np.random.default_rng(2)
+    rng = np.random.default_rng(2 + flags)
     cu = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
     for n, g in ((0, 2), (1, 1), (1000, 3), (70000, 8)):
         owner = rng.integers(-1, g, n)
-        wires, dense = [], []
+        wires, dense, parts = [], [], []
         for r in range(g):
             cnt = rng.integers(0, 4, n)
             if n:
                 cnt[rng.integers(0, n, 5)] = rng.integers(255, 600, 5)
             row = np.zeros(n + 1, np.uint32)
             np.cumsum(cnt, out=row[1:])
-            gid = rng.integers(0, 10 ** 6, int(row[-1])).astype(np.uint32)
+            gid = rng.integers(0, 1 << 24 if flags & 2 else 10 ** 9, int(row[-1])).astype(np.uint32)
             exg = np.where(owner == r, rng.integers(0, 10 ** 6, n), 0xFFFFFFFF).astype(np.uint32)
-            wires.append(_ref_export_wire(row, gid, exg))
+            cb, fb, x, o = _ref_export_wire(row, gid, exg, flags)
+            wires.append((flags, len(gid), cb, fb, x, o))
             dense.append(tuple(cu(a.view(np.int32)) for a in (row, gid, exg)))
-        parts = [D.WirePart(cu(c), cu(f.view(np.int32)), cu(x.view(np.int32)), cu(o.view(np.int32)))
-                 for c, f, x, o in wires]
+            parts.append(D.WirePart(flags, len(gid), cu(cb), cu(fb), cu(x.view(np.int32)),
+                                    cu(o.view(np.int32))))
         m = D.merge_wire(eng, parts, n)
         row, fid, ex = _ref_merge_wire(wires, n)
         assert np.array_equal(m.row_ptr.cpu().numpy().view(np.uint32).astype(np.int64), row)
@@ -82,7 +84,8 @@ def test_merge_wire_matches_reference(emqx):
     eng.close()
 
 
-def test_export_wire_matches_restatement(emqx):
+@pytest.mark.parametrize("flags", [0, 3])
+def test_export_wire_matches_restatement(emqx, flags):
     import workloads
     w = workloads.generate(2, 30000, 4000)
     eng = emqx.Engine()
@@ -99,14 +102,14 @@ def test_export_wire_matches_restatement(emqx):
     fid = torch.empty(r.n_pairs, dtype=torch.int32, device="cuda")
     ex = torch.empty(w.nt, dtype=torch.int32, device="cuda")
     eng.export(r, 0, row.data_ptr(), fid.data_ptr(), ex.data_ptr())
-    c8 = torch.empty(w.nt, dtype=torch.uint8, device="cuda")
-    f2 = torch.empty(r.n_pairs, dtype=torch.int32, device="cuda")
+    c8 = torch.empty(w.nt + 64, dtype=torch.uint8, device="cuda")
+    f2 = torch.empty(4 * r.n_pairs, dtype=torch.uint8, device="cuda")
     xs = torch.empty(2 * w.nt, dtype=torch.int32, device="cuda")
     ov = torch.empty(2 * w.nt, dtype=torch.int32, device="cuda")
-    nx, no = eng.export_wire(r, 0, c8.data_ptr(), f2.data_ptr(), xs.data_ptr(), ov.data_ptr())
+    nx, no = eng.export_wire(r, 0, flags, c8.data_ptr(), f2.data_ptr(), xs.data_ptr(), ov.data_ptr())
     u = lambda t: t.cpu().numpy().view(np.uint32)  # noqa: E731
-    c, f, x, o = _ref_export_wire(u(row), u(fid), u(ex))
-    assert np.array_equal(c8.cpu().numpy(), c) and np.array_equal(u(f2), f)
+    c, f, x, o = _ref_export_wire(u(row), u(fid), u(ex), flags)
+    assert np.array_equal(c8.cpu().numpy()[:len(c)], c) and np.array_equal(f2.cpu().numpy()[:len(f)], f)
     assert nx == len(x) // 2 and no == len(o) // 2 and nx > 0
     key = lambda a: sorted(map(tuple, a.reshape(-1, 2).tolist()))  # noqa: E731
     assert key(u(xs)[:2 * nx]) == key(x) and key(u(ov)[:2 * no]) == key(o)
@@ -169,7 +172,7 @@ def _rank(rank, world, port, q):
         gid = np.full(int(max(rid.max(), tid.max(initial=0))) + 1, 0xFFFFFFFF, np.uint32)
         gid[rid] = mine
         gid[tid] = mine[wsel]
-        sm = D.ShardedMatcher(eng, torch.from_numpy(gid.view(np.int32)).to(dev), dev)
+        sm = D.ShardedMatcher(eng, torch.from_numpy(gid.view(np.int32)).to(dev), dev, n_global=w.nf)
         tb = torch.from_numpy(w.tbytes).to(dev) if rank == 0 else None
         to = torch.from_numpy(w.toff.view(np.int32)).to(dev) if rank == 0 else None
         shape = (int(w.toff[-1]), w.nt)
