@@ -20,6 +20,9 @@ namespace {
 
 constexpr uint32_t WG = 256;
 constexpr uint32_t CH = STAGE_CHUNK;  // staged-pair slots reserved per wave per atomic
+#ifndef GM_SMALL_GRID  // A/B builds may override it
+#define GM_SMALL_GRID 1
+#endif
 #ifndef GM_TBLK  // A/B builds may override it
 #define GM_TBLK 128
 #endif
@@ -494,9 +497,16 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   a.spill = sc.spill;
   a.spill_items = sc.spill_items;
   a.lanes = g.lanes;
+  // a batch that gives the full grid less than one topic per lane launches only the blocks it
+  // fills (at least one per CU): the waves a full grid adds only queue failed claims on the
+  // exhausted shard counters (r03: a cfg3 walk took 79 us at 64k topics and 80 us at 262k)
+  uint32_t blocks = g.blocks;
+#if GM_SMALL_GRID
+  blocks = std::min<uint32_t>(blocks, std::max<uint32_t>((n + WG - 1) / WG, g.cus));
+#endif
   // a batch too small to give every wave TBLK topics is spread over all of them instead
   // (a 100k-topic batch would otherwise keep 3 in 4 waves idle)
-  const uint32_t waves = g.lanes / 64;
+  const uint32_t waves = blocks * (WG / 64);
   const uint32_t per_wave = waves ? (n + waves - 1) / waves : TBLK;
   a.tblk = per_wave >= TBLK ? TBLK : ((per_wave + 7) & ~7u) < 8 ? 8 : ((per_wave + 7) & ~7u);
   a.census = census;
@@ -509,21 +519,21 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   // at once, so that no block of the persistent grid starts after the others have drained
   constexpr uint32_t LDS_CU = 160u * 1024u;
   constexpr uint32_t DEEP_PER_CU = LDS_CU / walk_lds_bytes(DP);
-  const dim3 grid(level >= WALK_DEEP ? std::min<uint32_t>(g.blocks, g.cus * DEEP_PER_CU) : g.blocks);
+  const dim3 grid(level >= WALK_DEEP ? std::min<uint32_t>(blocks, g.cus * DEEP_PER_CU) : blocks);
   if (census) {
     if (level >= WALK_SPILL)
       hipLaunchKernelGGL((k_walk<true, true, DP>), grid, dim3(WG), 0, s, a);
     else if (level == WALK_DEEP)
       hipLaunchKernelGGL((k_walk<true, false, DP>), grid, dim3(WG), 0, s, a);
     else
-      hipLaunchKernelGGL((k_walk<true, false, SH>), dim3(g.blocks), dim3(WG), 0, s, a);
+      hipLaunchKernelGGL((k_walk<true, false, SH>), grid, dim3(WG), 0, s, a);
   } else {
     if (level >= WALK_SPILL)
       hipLaunchKernelGGL((k_walk<false, true, DP>), grid, dim3(WG), 0, s, a);
     else if (level == WALK_DEEP)
       hipLaunchKernelGGL((k_walk<false, false, DP>), grid, dim3(WG), 0, s, a);
     else
-      hipLaunchKernelGGL((k_walk<false, false, SH>), dim3(g.blocks), dim3(WG), 0, s, a);
+      hipLaunchKernelGGL((k_walk<false, false, SH>), grid, dim3(WG), 0, s, a);
   }
   return hipGetLastError();
 }

@@ -7,4 +7,5 @@ mkdir -p build
 name=$1; shift
 C=emqx_amd/csrc
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wall -Wno-unused-function \
-  -Wno-unused-result "$@" $C/gm_kernels.hip $C/gm_engine.cpp $C/gm_retain.cpp -o build/lib_$name.so
+  -Wno-unused-result "$@" $C/gm_kernels.hip $C/gm_engine.cpp $C/gm_retain.cpp $C/gm_batcher.cpp \
+  -o build/lib_$name.so
