@@ -20,6 +20,9 @@ namespace {
 
 constexpr uint32_t WG = 256;
 constexpr uint32_t CH = STAGE_CHUNK;  // staged-pair slots reserved per wave per atomic
+#ifndef GM_STATIC_ONE  // A/B builds may override it
+#define GM_STATIC_ONE 1
+#endif
 #ifndef GM_SMALL_GRID  // A/B builds may override it
 #define GM_SMALL_GRID 1
 #endif
@@ -497,10 +500,15 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   a.spill = sc.spill;
   a.spill_items = sc.spill_items;
   a.lanes = g.lanes;
-  // a batch that gives the full grid less than one topic per lane launches only the blocks it
-  // fills (at least one per CU): the waves a full grid adds only queue failed claims on the
-  // exhausted shard counters (r03: a cfg3 walk took 79 us at 64k topics and 80 us at 262k)
-  uint32_t blocks = g.blocks;
+  constexpr uint32_t SH = WALK_STK_SHALLOW, DP = WALK_STK_DEEP;
+  // the deep-stack variants fit fewer blocks per CU (LDS): launch only as many as are resident
+  // at once, so that no block of the persistent grid starts after the others have drained
+  constexpr uint32_t LDS_CU = 160u * 1024u;
+  constexpr uint32_t DEEP_PER_CU = LDS_CU / walk_lds_bytes(DP);
+  uint32_t blocks = level >= WALK_DEEP ? std::min<uint32_t>(g.blocks, g.cus * DEEP_PER_CU) : g.blocks;
+  // a batch that gives the grid less than one topic per lane launches only the blocks it fills
+  // (at least one per CU): the waves a full grid adds only queue failed claims on the exhausted
+  // shard counters (r03: a cfg3 walk took 79 us at 64k topics and 80 us at 262k)
 #if GM_SMALL_GRID
   blocks = std::min<uint32_t>(blocks, std::max<uint32_t>((n + WG - 1) / WG, g.cus));
 #endif
@@ -509,17 +517,15 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   const uint32_t waves = blocks * (WG / 64);
   const uint32_t per_wave = waves ? (n + waves - 1) / waves : TBLK;
   a.tblk = per_wave >= TBLK ? TBLK : ((per_wave + 7) & ~7u) < 8 ? 8 : ((per_wave + 7) & ~7u);
+  // at most one topic per lane of the launched grid: lane gl walks topic gl, no claims (r03:
+  // the failed claims of every wave on the exhausted counters dominated small batches)
+  a.static_one = GM_STATIC_ONE && (uint64_t)n <= (uint64_t)blocks * WG ? 1u : 0u;
   a.census = census;
   a.leafp_mask = ix.leafp_mask;
   a.root_sig = ix.root_sig;
   a.rh0 = ix.rh0;
   a.rh1 = ix.rh1;
-  constexpr uint32_t SH = WALK_STK_SHALLOW, DP = WALK_STK_DEEP;
-  // the deep-stack variants fit fewer blocks per CU (LDS): launch only as many as are resident
-  // at once, so that no block of the persistent grid starts after the others have drained
-  constexpr uint32_t LDS_CU = 160u * 1024u;
-  constexpr uint32_t DEEP_PER_CU = LDS_CU / walk_lds_bytes(DP);
-  const dim3 grid(level >= WALK_DEEP ? std::min<uint32_t>(blocks, g.cus * DEEP_PER_CU) : blocks);
+  const dim3 grid(blocks);
   if (census) {
     if (level >= WALK_SPILL)
       hipLaunchKernelGGL((k_walk<true, true, DP>), grid, dim3(WG), 0, s, a);
