@@ -1617,8 +1617,11 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
     HIPCHK(h, hipMemsetAsync(s.census, 0,
                              (CENSUS_HDR + 3 * (h->geom.lanes / 64)) * sizeof(unsigned long long),
                              st));
+  c.census = census;
+  c.walk_level = (census ? E.census_level : E.walk_level).load(std::memory_order_relaxed);
+  const uint32_t stat = ix.trie_empty ? 0u : walk_static_chunks(h->geom, n, c.walk_level, s.p_cap);
   roctx_mark(h->roctx, "k_tok");
-  HIPCHK(h, launch_tok(d_bytes, d_off, n, ix, s, st));
+  HIPCHK(h, launch_tok(d_bytes, d_off, n, ix, s, st, stat * STAGE_CHUNK));
   if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[4], st));
   roctx_mark(h->roctx, "k_exact");
   HIPCHK(h, launch_exact(d_bytes, d_off, n, ix, s, h->geom, st));
@@ -1628,10 +1631,8 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
   } else {
     // per-topic reject counts: only the verification passes write (and then read) them
     if (ix.needs_verify || legacy) HIPCHK(h, hipMemsetAsync(s.rej, 0, (size_t)n * 4, st));
-    c.census = census;
-    c.walk_level = (census ? E.census_level : E.walk_level).load(std::memory_order_relaxed);
     roctx_mark(h->roctx, "k_walk");
-    HIPCHK(h, launch_walk(ix, s, n, h->geom, st, census ? s.census : nullptr, c.walk_level));
+    HIPCHK(h, launch_walk(ix, s, n, h->geom, st, census ? s.census : nullptr, c.walk_level, stat));
     if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[2], st));
     if (!legacy) {
       // pairs of filters made of short (exact) tokens need no byte check (gm_verify.inc)

@@ -146,7 +146,7 @@ uint32_t scan_tmp_words(uint32_t n);
 // deeper levels (wh, at off[t] + t + level); exact route-key ids (exact_id, NONE if absent)
 // of wildcard names when there are no plain keys, else X_WILDPEND marks for launch_exact
 hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
-                      Scratch& sc, hipStream_t s);
+                      Scratch& sc, hipStream_t s, uint32_t pair_top0);
 // exact route-key ids of every name (after launch_tok; a no-op when there are no plain keys)
 hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
                         Scratch& sc, const WalkGeom& g, hipStream_t s);
@@ -197,9 +197,13 @@ hipError_t launch_fanout(const DevIndex& ix, const Scratch& sc, FanScratch& fs, 
 
 // census != nullptr selects the diagnostic walk (adds to census[0..CENSUS_N)); level (WalkLevel)
 // the probe-item stack: shallow or deep in LDS, or deep continued in global memory (spill)
+// the walk's workgroup count and its static staged-pair chunks (one per wave, or 0); k_tok
+// starts CTL_PAIR_TOP at static_chunks * STAGE_CHUNK
+uint32_t walk_blocks(const WalkGeom& g, uint32_t n, uint32_t level);
+uint32_t walk_static_chunks(const WalkGeom& g, uint32_t n, uint32_t level, uint32_t pcap);
 hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGeom& g,
                        hipStream_t s, unsigned long long* census = nullptr,
-                       uint32_t level = WALK_SHALLOW);
+                       uint32_t level = WALK_SHALLOW, uint32_t stat_chunks = 0);
 // production: verify (flags + counts) -> [scan] -> deferred scatter
 hipError_t launch_verify(const uint8_t* bytes, const uint32_t* off, const DevIndex& ix,
                          Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_t s);

@@ -23,6 +23,9 @@ constexpr uint32_t CH = STAGE_CHUNK;  // staged-pair slots reserved per wave per
 #ifndef GM_STATIC_ONE  // A/B builds may override it
 #define GM_STATIC_ONE 1
 #endif
+#ifndef GM_STATIC_CHUNK  // A/B builds may override it
+#define GM_STATIC_CHUNK 1
+#endif
 #ifndef GM_SMALL_GRID  // A/B builds may override it
 #define GM_SMALL_GRID 1
 #endif
@@ -435,9 +438,10 @@ static ExactArgs exact_args(const DevIndex& ix) {
 }
 
 hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
-                      Scratch& sc, hipStream_t s) {
+                      Scratch& sc, hipStream_t s, uint32_t pair_top0) {
   if (n == 0) return hipSuccess;
   TokArgs a;
+  a.pair_top0 = pair_top0;
   a.bytes = bytes;
   a.off = off;
   a.n = n;
@@ -478,8 +482,38 @@ hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, c
   return hipGetLastError();
 }
 
+// Workgroups of one walk launch.  The deep-stack variants fit fewer blocks per CU (LDS): only
+// as many are launched as are resident at once, so that no block of the persistent grid starts
+// after the others have drained.  A batch that gives the grid less than one topic per lane
+// launches only the blocks it fills (at least one per CU): the waves a full grid adds only queue
+// failed claims on the exhausted shard counters (r03: a cfg3 walk took 79 us at 64k topics and
+// 80 us at 262k).
+uint32_t walk_blocks(const WalkGeom& g, uint32_t n, uint32_t level) {
+  constexpr uint32_t LDS_CU = 160u * 1024u;
+  constexpr uint32_t DEEP_PER_CU = LDS_CU / walk_lds_bytes(WALK_STK_DEEP);
+  uint32_t blocks = level >= WALK_DEEP ? std::min<uint32_t>(g.blocks, g.cus * DEEP_PER_CU) : g.blocks;
+#if GM_SMALL_GRID
+  blocks = std::min<uint32_t>(blocks, std::max<uint32_t>((n + WG - 1) / WG, g.cus));
+#endif
+  return blocks;
+}
+
+// Staged-pair chunks handed out before the walk starts: wave w of the launch owns chunk w from
+// its first flush on (only later chunks take an atomic on CTL_PAIR_TOP, which k_tok sets to the
+// end of the static ones).  0 when the staging buffer cannot hold one chunk per wave.
+uint32_t walk_static_chunks(const WalkGeom& g, uint32_t n, uint32_t level, uint32_t pcap) {
+#if GM_STATIC_CHUNK
+  const uint64_t waves = (uint64_t)walk_blocks(g, n, level) * (WG / 64);
+  return waves * CH <= pcap ? (uint32_t)waves : 0u;
+#else
+  (void)g, (void)n, (void)level, (void)pcap;
+  return 0u;
+#endif
+}
+
 hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGeom& g,
-                       hipStream_t s, unsigned long long* census, uint32_t level) {
+                       hipStream_t s, unsigned long long* census, uint32_t level,
+                       uint32_t stat_chunks) {
   WalkArgs a;
   a.rec = sc.rec;
   a.wh = sc.wh;
@@ -501,17 +535,7 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   a.spill_items = sc.spill_items;
   a.lanes = g.lanes;
   constexpr uint32_t SH = WALK_STK_SHALLOW, DP = WALK_STK_DEEP;
-  // the deep-stack variants fit fewer blocks per CU (LDS): launch only as many as are resident
-  // at once, so that no block of the persistent grid starts after the others have drained
-  constexpr uint32_t LDS_CU = 160u * 1024u;
-  constexpr uint32_t DEEP_PER_CU = LDS_CU / walk_lds_bytes(DP);
-  uint32_t blocks = level >= WALK_DEEP ? std::min<uint32_t>(g.blocks, g.cus * DEEP_PER_CU) : g.blocks;
-  // a batch that gives the grid less than one topic per lane launches only the blocks it fills
-  // (at least one per CU): the waves a full grid adds only queue failed claims on the exhausted
-  // shard counters (r03: a cfg3 walk took 79 us at 64k topics and 80 us at 262k)
-#if GM_SMALL_GRID
-  blocks = std::min<uint32_t>(blocks, std::max<uint32_t>((n + WG - 1) / WG, g.cus));
-#endif
+  const uint32_t blocks = walk_blocks(g, n, level);
   // a batch too small to give every wave TBLK topics is spread over all of them instead
   // (a 100k-topic batch would otherwise keep 3 in 4 waves idle)
   const uint32_t waves = blocks * (WG / 64);
@@ -520,6 +544,7 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   // at most one topic per lane of the launched grid: lane gl walks topic gl, no claims (r03:
   // the failed claims of every wave on the exhausted counters dominated small batches)
   a.static_one = GM_STATIC_ONE && (uint64_t)n <= (uint64_t)blocks * WG ? 1u : 0u;
+  a.stat_chunks = stat_chunks;
   a.census = census;
   a.leafp_mask = ix.leafp_mask;
   a.root_sig = ix.root_sig;
