@@ -113,14 +113,16 @@ constexpr uint32_t REJ_SCAN_MAX = 4096;  // rejects the deferred scatter handles
 // (profiles/r02/session2/ab_walk_stack.txt, ab_walk_stack_deep.txt): pipelined step 1.59 ms
 // spilling past 6, 1.38 ms past 8, 1.21 ms with 12 or 14 (3 blocks per CU), 1.45 ms with 16
 // (2 blocks per CU); cfg3 never leaves the shallow stack (an 8-deep one cost it ~1.5%).
-#ifndef GM_WALK_STK_SHALLOW  // A/B builds may override it
-#define GM_WALK_STK_SHALLOW 6
+// Walk item stacks per variant level: SHALLOW and DEEP keep compact 32-bit items in LDS (12 at
+// four blocks per CU, 24 at three: gm_walk.inc CPT), SPILL keeps 12 {node, level} pairs in LDS
+// and continues in global memory.  GM_WALK_CPT=0 (A/B builds): 8-B items, 6 / 12 / 12 + spill.
+#ifndef GM_WALK_CPT
+#define GM_WALK_CPT 1
 #endif
-constexpr uint32_t WALK_STK_SHALLOW = GM_WALK_STK_SHALLOW;
-#ifndef GM_WALK_STK_DEEP  // A/B builds may override it
-#define GM_WALK_STK_DEEP 12
-#endif
-constexpr uint32_t WALK_STK_DEEP = GM_WALK_STK_DEEP;
+constexpr bool WALK_CPT = GM_WALK_CPT != 0;
+constexpr uint32_t WALK_STK_SHALLOW = WALK_CPT ? 12 : 6;
+constexpr uint32_t WALK_STK_DEEP = WALK_CPT ? 24 : 12;
+constexpr uint32_t WALK_STK_SPILL = 12;
 enum WalkLevel : uint32_t { WALK_SHALLOW = 0, WALK_DEEP = 1, WALK_SPILL = 2 };
 constexpr uint32_t WALK_SPILL_MIN = 32;  // initial spill items per lane (grown on overflow)
 // spill items per lane that no walk can exceed: a resolved probe pushes <= 4 items spanning

@@ -490,8 +490,10 @@ hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, c
 // 80 us at 262k).
 uint32_t walk_blocks(const WalkGeom& g, uint32_t n, uint32_t level) {
   constexpr uint32_t LDS_CU = 160u * 1024u;
-  constexpr uint32_t DEEP_PER_CU = LDS_CU / walk_lds_bytes(WALK_STK_DEEP);
-  uint32_t blocks = level >= WALK_DEEP ? std::min<uint32_t>(g.blocks, g.cus * DEEP_PER_CU) : g.blocks;
+  const uint32_t lds = level >= WALK_SPILL ? walk_lds_bytes(WALK_STK_SPILL)
+                       : level == WALK_DEEP ? walk_lds_bytes(WALK_STK_DEEP, WALK_CPT)
+                                            : walk_lds_bytes(WALK_STK_SHALLOW, WALK_CPT);
+  uint32_t blocks = std::min<uint32_t>(g.blocks, g.cus * (LDS_CU / lds));
 #if GM_SMALL_GRID
   blocks = std::min<uint32_t>(blocks, std::max<uint32_t>((n + WG - 1) / WG, g.cus));
 #endif
@@ -534,7 +536,8 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   a.spill = sc.spill;
   a.spill_items = sc.spill_items;
   a.lanes = g.lanes;
-  constexpr uint32_t SH = WALK_STK_SHALLOW, DP = WALK_STK_DEEP;
+  constexpr uint32_t SH = WALK_STK_SHALLOW, DP = WALK_STK_DEEP, SP = WALK_STK_SPILL;
+  constexpr bool C = WALK_CPT;
   const uint32_t blocks = walk_blocks(g, n, level);
   // a batch too small to give every wave TBLK topics is spread over all of them instead
   // (a 100k-topic batch would otherwise keep 3 in 4 waves idle)
@@ -553,18 +556,18 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   const dim3 grid(blocks);
   if (census) {
     if (level >= WALK_SPILL)
-      hipLaunchKernelGGL((k_walk<true, true, DP>), grid, dim3(WG), 0, s, a);
+      hipLaunchKernelGGL((k_walk<true, true, SP>), grid, dim3(WG), 0, s, a);
     else if (level == WALK_DEEP)
-      hipLaunchKernelGGL((k_walk<true, false, DP>), grid, dim3(WG), 0, s, a);
+      hipLaunchKernelGGL((k_walk<true, false, DP, C>), grid, dim3(WG), 0, s, a);
     else
-      hipLaunchKernelGGL((k_walk<true, false, SH>), grid, dim3(WG), 0, s, a);
+      hipLaunchKernelGGL((k_walk<true, false, SH, C>), grid, dim3(WG), 0, s, a);
   } else {
     if (level >= WALK_SPILL)
-      hipLaunchKernelGGL((k_walk<false, true, DP>), grid, dim3(WG), 0, s, a);
+      hipLaunchKernelGGL((k_walk<false, true, SP>), grid, dim3(WG), 0, s, a);
     else if (level == WALK_DEEP)
-      hipLaunchKernelGGL((k_walk<false, false, DP>), grid, dim3(WG), 0, s, a);
+      hipLaunchKernelGGL((k_walk<false, false, DP, C>), grid, dim3(WG), 0, s, a);
     else
-      hipLaunchKernelGGL((k_walk<false, false, SH>), grid, dim3(WG), 0, s, a);
+      hipLaunchKernelGGL((k_walk<false, false, SH, C>), grid, dim3(WG), 0, s, a);
   }
   return hipGetLastError();
 }

@@ -376,6 +376,41 @@ def test_staging_overflow_rerun_and_deep_stack(emqx):
         assert got == (exp0 if i < 600 else exp1)
 
 
+def test_compact_items_deep_levels(emqx):
+    """The walk's LDS items are 32-bit (node | kind | level < 16).  An item past the 12-item
+    shallow stack, or of level >= 16 (filters of 16+ levels), flags the pass, which is redone one
+    variant up (24 compact items, then {node, level} pairs with the global spill).  A batch
+    mixing such topics with shallow ones: rows equal the oracle's."""
+    import itertools
+    filters = []
+    for k in range(9):
+        for combo in itertools.product(["a", "+"], repeat=k):
+            filters.append(("/".join(list(combo) + ["#"])).encode())
+    filters += [b"/".join([b"a"] * k) for k in (1, 5, 15, 16, 17, 20)]
+    filters += [b"/".join([b"+"] * 17 + [b"b"]), b"/".join([b"a"] * 16 + [b"+", b"#"])]
+    rng = random.Random(7)
+    topics = []
+    for i in range(3000):
+        n = rng.choice([1, 2, 3, 6, 9, 12, 15, 16, 17, 18, 20, 24])
+        topics.append(b"/".join(rng.choice([b"a", b"a", b"b"]) for _ in range(n)))
+    eng = emqx.Engine()
+    for f in filters:
+        eng.trie_insert(f)
+    eng.commit()
+    res = eng.match(topics)
+    assert eng.stats()["reruns"] >= 1
+    py = R.Trie()
+    for f in filters:
+        py.insert(f)
+    for i, t in enumerate(topics):
+        got = sorted(eng.filter_bytes(int(f)) for f in res.row(i))
+        assert got == sorted(py.match(t)), t
+    # the shallow-only batch of the same index runs on the learnt variant: same answer
+    res2 = eng.match(topics[:100])
+    for i in range(100):
+        assert list(res2.row(i)) == list(res.row(i))
+
+
 # ---------------------------------------------------------------- synthetic configs vs oracle
 
 def _load_both(emqx, w, **kw):

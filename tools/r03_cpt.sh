@@ -1,0 +1,12 @@
+#!/bin/bash
+# r03: GPU tests + smoke with compact walk items, then the A/B against 8-B items (build/lib_nocpt)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+T=${1:-r03_cpt}
+O=$R/gpurun_out/$T
+mkdir -p $O
+cd $R
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > $O/pytest.log 2>&1 || exit 1
+timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > $O/smoke.log 2>&1 || exit 1
+SPECS="1:0 2:0 3:0 3:65536" STEPS=30 bash tools/r03_ab_lib.sh $T/ab nocpt || exit 1
