@@ -125,18 +125,31 @@ int emqxgm_batcher_add_many(emqxgm_batcher_t* b, const uint8_t* bytes, const uin
   if (!b || (n && (!offsets || (!bytes && offsets[n] != offsets[0])))) return -EINVAL;
   std::lock_guard<std::mutex> g(b->mu);
   Window& w = b->w[b->open];
+  // the run of topics that fits, then one copy of its bytes (a copy per topic cost ~15 ns each:
+  // ~1 ms per 64k-topic window, r03)
+  const uint32_t used = w.off[w.n];
+  const uint32_t room_t = b->cfg.window_topics - w.n;
   uint32_t k = 0;
-  for (; k < n; ++k) {
-    if (offsets[k + 1] < offsets[k]) return k ? (int)k : -EINVAL;
-    const uint32_t len = offsets[k + 1] - offsets[k], used = w.off[w.n];
-    if (len > b->cfg.window_bytes) return k ? (int)k : -E2BIG;
-    if (w.n >= b->cfg.window_topics || len > b->cfg.window_bytes - used) break;
-    if (w.n == 0) w.first_ns = mono_ns();
-    if (len) memcpy(w.bytes + used, bytes + offsets[k], len);
-    w.off[w.n + 1] = used + len;
-    w.tag.push_back(tag0 + k);
-    w.n += 1;
+  int err = 0;
+  for (; k < n && k < room_t; ++k) {
+    if (offsets[k + 1] < offsets[k]) {
+      err = -EINVAL;
+      break;
+    }
+    const uint32_t len = offsets[k + 1] - offsets[k];
+    if (len > b->cfg.window_bytes) {
+      err = -E2BIG;
+      break;
+    }
+    if ((uint64_t)offsets[k + 1] - offsets[0] > (uint64_t)b->cfg.window_bytes - used) break;
   }
+  if (k == 0) return err;
+  if (w.n == 0) w.first_ns = mono_ns();
+  const uint32_t o0 = offsets[0];
+  if (offsets[k] != o0) memcpy(w.bytes + used, bytes + o0, offsets[k] - o0);
+  for (uint32_t j = 1; j <= k; ++j) w.off[w.n + j] = used + (offsets[j] - o0);
+  for (uint32_t j = 0; j < k; ++j) w.tag.push_back(tag0 + j);
+  w.n += k;
   return (int)k;
 }
 

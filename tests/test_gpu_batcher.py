@@ -143,3 +143,40 @@ def test_batcher_protocol_edges(emqx):
     with pytest.raises(emqx.EngineError, match="ENOENT"):
         b.collect(12345)
     b.close()
+
+
+def test_batcher_add_many_packs_like_add(emqx):
+    """add_many (the bulk form: one copy of the run of topics that fits) packs a window exactly
+    like add one by one: the same answers per tag, partial adds when the window fills by topics
+    or by bytes, a base offset != 0, and the errors of a bad first topic."""
+    eng = emqx.Engine()
+    for f in (b"a/+", b"a/#", b"#", b"b/+/c"):
+        eng.route_ref(f)
+        eng.trie_insert(f)
+    eng.route_ref(b"a/b")
+    eng.commit()
+    rng = random.Random(5)
+    topics = [rng.choice([b"a/b", b"a", b"", b"b/x/c", b"a/b/c/d", b"zz"]) for _ in range(300)]
+    lens = np.array([len(t) for t in topics], np.uint32)
+    pad = b"PAD"  # offsets start past 0: the run is copied from bytes[off[0]:]
+    buf = np.frombuffer(pad + b"".join(topics), np.uint8)
+    off = np.zeros(len(topics) + 1, np.uint32)
+    np.cumsum(lens, out=off[1:])
+    off += len(pad)
+    one = _drive(emqx, emqx.Batcher(eng, window_topics=64, window_bytes=160), topics, 1)
+    b = emqx.Batcher(eng, window_topics=64, window_bytes=160)
+    got, i = {}, 0
+    while i < len(topics):
+        k = b.add_many(buf, off[i:], i)
+        assert 0 < k <= 64 and int(off[i + k] - off[i]) <= 160
+        i += k
+        w = b.collect(b.flush())
+        for j in range(len(w.tag)):
+            got[int(w.tag[j])] = (w.filters(j), int(w.exact_id[j]))
+    assert got == one
+    with pytest.raises(emqx.EngineError, match="EINVAL"):
+        b.add_many(buf, np.array([5, 3], np.uint32))
+    with pytest.raises(emqx.EngineError, match="E2BIG"):
+        b.add_many(np.zeros(200, np.uint8), np.array([0, 200], np.uint32))
+    assert b.add_many(buf, np.array([3, 6, 2], np.uint32)) == 1  # stops before the bad offset
+    b.close()
