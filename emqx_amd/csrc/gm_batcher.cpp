@@ -1,7 +1,7 @@
 // gm_batcher.cpp -- the NIF batcher core (include/emqx_gpumatch.h "NIF batcher core"), a layer
 // over the engine's public C-ABI: publish topics of concurrent callers are packed into a window
 // in pinned host memory, a window is submitted whole through the host pipes
-// (emqxgm_match_batch_submit / _wait_filters), and a collected window comes back with every
+// (emqxgm_match_batch_submit_filters / _wait_filters), and a collected window comes back with every
 // pair's filter bytes, gathered on the device.
 //
 // The reference matches each publish in the publisher's own process
@@ -168,7 +168,9 @@ int emqxgm_batcher_flush(emqxgm_batcher_t* b, uint64_t* window) {
   if (w.n == 0) return 0;
   if (b->in_flight >= EMQXGM_HOST_PIPES) return -EBUSY;
   uint64_t tk = 0;
-  const int rc = emqxgm_match_batch_submit(b->h, w.bytes, w.off, w.n, &tk);
+  // the filter-byte gather and every result copy go behind the pass: one synchronisation at
+  // collect (emqxgm_match_batch_wait_filters)
+  const int rc = emqxgm_match_batch_submit_filters(b->h, w.bytes, w.off, w.n, &tk);
   if (rc) return rc;
   w.ticket = tk;
   w.id = b->next_id++;

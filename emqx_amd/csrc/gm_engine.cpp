@@ -469,6 +469,13 @@ struct emqxgm {
     DevBuf d_fb;
     Pinned h_fboff, h_fb;
     uint64_t fb_bytes = 0;
+    // emqxgm_match_batch_submit_filters: the gather and every copy were enqueued behind the
+    // pass, sized by the estimates below; the wait then takes one stream synchronisation
+    bool fb_async = false;
+    uint64_t fb_pairs_copy = 0, fb_bytes_copy = 0;  // pairs / bytes the packed block holds
+    Pinned h_blk;                                   // the packed block (FbLayout)
+    bool fb_fast = false;                           // the last completion came from the block
+    double fb_ppt = 0, fb_bpp = 0;                  // pairs per topic, bytes per pair (decaying max)
   } hpipes[EMQXGM_HOST_PIPES];
   uint64_t next_hticket = 1;
   hipStream_t pipe_streams[EMQXGM_HOST_PIPES] = {};  // pipe_stream(): shared by both pipe kinds
@@ -2049,11 +2056,27 @@ int host_pipe_complete(emqxgm* h, emqxgm::HostPipe& p, bool gather = false) {
     rc = run_device(h, p.c, p.d_bytes, p.d_off, p.n, p.bytes_len, &p.pairs);
     rows_copied = false;
   }
-  if (rc == 0 && gather) rc = host_pipe_gather(h, p);
+  // submitted with the gather behind the pass: done when its copies covered the window
+  const uint32_t blk_total = p.fb_async ? *(const uint32_t*)p.h_blk.p : 0u;
+  const bool async_done = rc == 0 && gather && p.fb_async && rows_copied &&
+                          p.pairs <= p.fb_pairs_copy && blk_total <= p.fb_bytes_copy;
+  if (async_done) p.fb_bytes = p.pairs ? blk_total : 0;
+  p.fb_fast = async_done;
+  if (rc == 0 && gather && !async_done) rc = host_pipe_gather(h, p);
+  p.fb_async = false;
   p.c.epoch.reset();
   if (rc < 0) {
     p.state = 0;
     return rc;
+  }
+  if (gather && p.n) {  // the next async window's copy sizes follow the recent windows
+    const double ppt = (double)p.pairs / p.n, bpp = p.pairs ? (double)p.fb_bytes / p.pairs : 0.0;
+    p.fb_ppt = std::max(ppt, 0.9 * p.fb_ppt);
+    p.fb_bpp = std::max(bpp, 0.9 * p.fb_bpp);
+  }
+  if (async_done) {  // filter ids, exact ids, byte offsets and bytes are in the packed block
+    p.state = 2;
+    return 0;
   }
   const Scratch& s = p.c.sc;
   const bool mode1 = h->host_out_mode == 1;
@@ -2848,8 +2871,11 @@ int emqxgm_match_device_wait(emqxgm_t* h, uint64_t ticket, emqxgm_dev_out* out) 
   return 0;
 }
 
-int emqxgm_match_batch_submit(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets,
-                              uint32_t n, uint64_t* ticket) {
+}  // extern "C"
+namespace {
+int host_pipe_enqueue_gather(emqxgm* h, emqxgm::HostPipe& p);
+int batch_submit(emqxgm* h, const uint8_t* bytes, const uint32_t* offsets, uint32_t n,
+                 uint64_t* ticket, bool want_fb) {
   if (!h || !ticket || !offsets || offsets[0] != 0 || (!bytes && offsets[n])) return -EINVAL;
   if (n > h->cfg.batch_max) return -E2BIG;
   // a decreasing offset would make k_tok / k_exact read a topic of ~4 G bytes past the batch
@@ -2882,6 +2908,7 @@ int emqxgm_match_batch_submit(emqxgm_t* h, const uint8_t* bytes, const uint32_t*
   p.n = n;
   p.bytes_len = nb;
   p.pairs = 0;
+  p.fb_async = false;
   if (n == 0) {
     p.h_row[0] = 0;
     p.state = 2;
@@ -2889,7 +2916,7 @@ int emqxgm_match_batch_submit(emqxgm_t* h, const uint8_t* bytes, const uint32_t*
     if (nb) HIPCHK(h, hipMemcpyAsync(p.d_bytes, bytes, nb, hipMemcpyHostToDevice, p.c.stream));
     HIPCHK(h, hipMemcpyAsync(p.d_off, offsets, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, p.c.stream));
     if ((rc = pass_submit(h, p.c, p.d_bytes, p.d_off, n, false, false)) ||
-        (rc = host_pipe_copy_out(h, p)))
+        (rc = host_pipe_copy_out(h, p)) || (want_fb && (rc = host_pipe_enqueue_gather(h, p))))
       return rc;
     p.state = 1;
   }
@@ -2897,6 +2924,58 @@ int emqxgm_match_batch_submit(emqxgm_t* h, const uint8_t* bytes, const uint32_t*
   h->next_hticket += 1;
   *ticket = tk;
   return 0;
+}
+
+// The pairs' filter bytes gathered behind the pass (its epoch is held until the wait, so the
+// device string pool stays) and packed with the byte offsets, the filter ids and the exact ids
+// into one block that one copy brings into the pipe's pinned memory, all stream-ordered.  The
+// block holds the pairs and bytes the pipe's recent windows suggest for n topics (x1.2); a
+// window beyond them is finished in the wait, synchronously (host_pipe_gather).
+int host_pipe_enqueue_gather(emqxgm* h, emqxgm::HostPipe& p) {
+  const Scratch& s = p.c.sc;
+  const DevIndex& ix = p.c.epoch->ix;
+  const uint32_t cap = s.p_cap;  // no pass stages more pairs than this (else it is redone)
+  const double ppt = p.fb_ppt > 0 ? p.fb_ppt : 4.0, bpp = p.fb_bpp > 0 ? p.fb_bpp : 32.0;
+  // (ppt and bpp are decaying maxima of the pipe's recent windows: x1.2 of headroom on top)
+  const double exp_p = ppt * p.n;
+  const uint32_t want_p = (uint32_t)std::min<uint64_t>(cap, (uint64_t)(1.2 * exp_p) + 256);
+  const uint64_t want_b = (uint64_t)(1.2 * bpp * exp_p) + 4096;
+  const FbLayout L(p.n, want_p);
+  const uint64_t blk = L.bytes + want_b;
+  const uint64_t tw = scan_tmp_words(cap);
+  const uint64_t words = 2ull * cap + 1 + tw + 2;  // scratch: lengths, offsets, total, scan
+  const uint64_t at = ((words * 4 + 255) / 256) * 256;
+  int rc = 0;
+  if ((rc = grow_dev(h, p.d_fb, at + blk, p.c.stream)) ||
+      (rc = pinned_reserve(h, p.h_blk, (size_t)blk, false)))
+    return rc;
+  uint32_t* len = (uint32_t*)p.d_fb.p;
+  uint32_t* ooff = len + cap;
+  uint32_t* total = ooff + cap + 1;
+  uint32_t* tmp = total + 2;
+  uint8_t* block = (uint8_t*)p.d_fb.p + at;
+  const uint32_t* npairs = s.ctl + CTL_TOTAL;  // written by the pass's scan
+  hipStream_t st = p.c.stream;
+  HIPCHK(h, launch_filter_len_dev(s.out, npairs, cap, ix.foff, len, ooff, tmp, total, st));
+  HIPCHK(h, launch_fb_pack(s.out, npairs, ix.foff, ix.fbytes, ooff, total, s.exact_id, p.n, want_p,
+                           want_b, block, st));
+  HIPCHK(h, hipMemcpyAsync(p.h_blk.p, block, (size_t)blk, hipMemcpyDeviceToHost, st));
+  p.fb_pairs_copy = want_p;
+  p.fb_bytes_copy = want_b;
+  p.fb_async = true;
+  return 0;
+}
+}  // namespace
+extern "C" {
+
+int emqxgm_match_batch_submit(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets,
+                              uint32_t n, uint64_t* ticket) {
+  return batch_submit(h, bytes, offsets, n, ticket, false);
+}
+
+int emqxgm_match_batch_submit_filters(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets,
+                                      uint32_t n, uint64_t* ticket) {
+  return batch_submit(h, bytes, offsets, n, ticket, true);
 }
 
 int emqxgm_match_batch_wait(emqxgm_t* h, uint64_t ticket, emqxgm_batch_out* out) {
@@ -2932,6 +3011,7 @@ int emqxgm_match_batch_wait_filters(emqxgm_t* h, uint64_t ticket, emqxgm_batch_o
     return -ENOENT;
   }
   const bool empty = p.state == 2;  // an empty batch: no pass ran
+  if (empty) p.fb_fast = false;
   int rc = host_pipe_complete(h, p, true);
   if (rc || (rc = pinned_reserve(h, p.h_fboff, 4, true)) || (rc = pinned_reserve(h, p.h_fb, 1, true)))
     return rc;
@@ -2940,6 +3020,15 @@ int emqxgm_match_batch_wait_filters(emqxgm_t* h, uint64_t ticket, emqxgm_batch_o
   out->n = p.n;
   out->n_pairs = p.pairs;
   out->row_ptr = p.h_row;
+  if (p.fb_fast) {  // one block: FbLayout for the pipe's n and copy sizes
+    const FbLayout L(p.n, (uint32_t)p.fb_pairs_copy);
+    const uint8_t* b = (const uint8_t*)p.h_blk.p;
+    out->filter_id = (const uint32_t*)(b + L.fid);
+    out->exact_id = (const uint32_t*)(b + L.exact);
+    *foff = (const uint32_t*)(b + L.ooff);
+    *fbytes = b + L.bytes;
+    return 0;
+  }
   out->filter_id = p.h_fid;
   out->exact_id = p.exact_none ? p.h_none : p.h_exact;
   *foff = (const uint32_t*)p.h_fboff.p;

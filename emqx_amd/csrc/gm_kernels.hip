@@ -143,9 +143,18 @@ __device__ __forceinline__ void load16(const uint32_t* in, uint64_t i0, uint32_t
   }
 }
 
+// n_dev (optional): the element count is min(*n_dev, n), read on the device (n is then the
+// capacity the grid was sized for); blocks past the last tile return at once.
+__device__ __forceinline__ uint32_t scan_count(uint32_t n, const uint32_t* n_dev) {
+  return n_dev ? min(*n_dev, n) : n;
+}
+
 __global__ __launch_bounds__(WG) void k_scan_partials(const uint32_t* __restrict__ in, uint32_t n,
-                                                      uint32_t* __restrict__ part) {
+                                                      uint32_t* __restrict__ part,
+                                                      const uint32_t* __restrict__ n_dev) {
   __shared__ uint32_t s_w[WG / 64];
+  n = scan_count(n, n_dev);
+  if (blockIdx.x > 0 && (uint64_t)blockIdx.x * SCAN_TILE >= n) return;
   uint32_t v[16];
   load16(in, (uint64_t)blockIdx.x * SCAN_TILE + 16ull * threadIdx.x, n, v);
   uint32_t acc = 0;
@@ -161,9 +170,15 @@ __global__ __launch_bounds__(WG) void k_scan_partials(const uint32_t* __restrict
 __global__ __launch_bounds__(WG) void k_scan_final(const uint32_t* __restrict__ in, uint32_t n,
                                                    const uint32_t* __restrict__ part, uint32_t nb,
                                                    uint32_t* __restrict__ out,
-                                                   uint32_t* __restrict__ out_n,
-                                                   uint32_t* __restrict__ total_dst) {
+                                                   uint32_t* __restrict__ total_dst,
+                                                   const uint32_t* __restrict__ n_dev) {
   __shared__ uint32_t s_w[WG / 64];
+  if (n_dev) {
+    n = scan_count(n, n_dev);
+    nb = n ? (n + SCAN_TILE - 1) / SCAN_TILE : 1u;
+    if (blockIdx.x >= nb) return;
+  }
+  uint32_t* const out_n = out + n;
   uint32_t pre = 0;
   for (uint32_t i = threadIdx.x; i < blockIdx.x; i += WG) pre += part[i];
   uint32_t carry;
@@ -363,24 +378,84 @@ __global__ __launch_bounds__(WG) void k_fill_u32(uint32_t* dst, uint32_t n, uint
 // ---- the matched filters' bytes for the host (the NIF's filter binaries): lengths from the
 // device copy of the string pool's offsets, a scan, then each pair's bytes gathered ----
 __global__ __launch_bounds__(WG) void k_filter_len(const uint32_t* fid, uint32_t pairs,
-                                                   const uint64_t* foff, uint32_t* len) {
+                                                   const uint64_t* foff, uint32_t* len,
+                                                   const uint32_t* pairs_dev) {
+  pairs = pairs_dev ? min(*pairs_dev, pairs) : pairs;
   for (uint32_t j = blockIdx.x * WG + threadIdx.x; j < pairs; j += gridDim.x * WG) {
     const uint32_t f = fid[j];
     len[j] = (uint32_t)(foff[f + 1] - foff[f]);
   }
 }
 
-// one lane per pair; a filter's bytes are contiguous in the pool, so after its first line every
-// load of the lane hits the same line
-__global__ __launch_bounds__(WG) void k_filter_gather(const uint32_t* fid, uint32_t pairs,
-                                                      const uint64_t* foff, const uint8_t* pool,
-                                                      const uint32_t* ooff, uint8_t* out) {
+// Bytes [0, n) of the pool from byte s into d: aligned dword loads, eight (plus one) in flight
+// per step, funnel-shifted into bytes (a byte-by-byte loop waited on every load: 28 round trips
+// for a 28-B filter).  Reads only the dwords that hold the filter's bytes.
+__device__ __forceinline__ void copy_filter(const uint8_t* __restrict__ pool, uint64_t s, uint32_t n,
+                                            uint8_t* __restrict__ d) {
+  if (n == 0) return;
+  const uint32_t* w = (const uint32_t*)(pool + (s & ~3ull));
+  const uint32_t sh = (uint32_t)(s & 3u), last = (sh + n - 1) >> 2;
+  for (uint32_t i = 0; i < n; i += 32) {
+    const uint32_t w0 = i >> 2;
+    uint32_t v[9];
+#pragma unroll
+    for (uint32_t k = 0; k < 9; ++k) v[k] = w[min(w0 + k, last)];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      const uint32_t x = __builtin_amdgcn_alignbyte(v[k + 1], v[k], sh);
+#pragma unroll
+      for (uint32_t b = 0; b < 4; ++b)
+        if (i + 4 * k + b < n) d[i + 4 * k + b] = (uint8_t)(x >> (8 * b));
+    }
+  }
+}
+
+// one lane per pair
+__global__ __launch_bounds__(WG) void k_filter_gather(const uint32_t* __restrict__ fid, uint32_t pairs,
+                                                      const uint64_t* __restrict__ foff,
+                                                      const uint8_t* __restrict__ pool,
+                                                      const uint32_t* __restrict__ ooff,
+                                                      uint8_t* __restrict__ out) {
   for (uint32_t j = blockIdx.x * WG + threadIdx.x; j < pairs; j += gridDim.x * WG) {
-    const uint32_t f = fid[j];
-    const uint8_t* src = pool + foff[f];
-    uint8_t* dst = out + ooff[j];
-    const uint32_t n = ooff[j + 1] - ooff[j];
-    for (uint32_t i = 0; i < n; ++i) dst[i] = src[i];
+    const uint32_t o = ooff[j];
+    copy_filter(pool, foff[fid[j]], ooff[j + 1] - o, out + o);
+  }
+}
+
+// A host window's whole result in one block for one D2H copy (emqxgm_match_batch_submit_filters):
+// {byte total, byte offsets [pairs+1], filter ids [pairs], exact ids [n], bytes}, at offsets the
+// host chose for cap_p pairs and cap_b bytes.  The pair count and the byte total are read on the
+// device; a window beyond the caps writes only its total (the host finishes it synchronously).
+struct FbPack {
+  const uint32_t* fid;
+  const uint32_t* pairs_dev;
+  const uint64_t* foff;
+  const uint8_t* pool;
+  const uint32_t* ooff;   // the scan of the pairs' filter lengths (pairs + 1 entries)
+  const uint32_t* total;  // bytes of all pairs
+  const uint32_t* exact;
+  uint32_t n, cap_p;
+  uint64_t cap_b;
+  uint32_t* b_total;
+  uint32_t* b_ooff;
+  uint32_t* b_fid;
+  uint32_t* b_exact;
+  uint8_t* b_bytes;
+};
+
+__global__ __launch_bounds__(WG) void k_fb_pack(FbPack A) {
+  const uint32_t pairs = *A.pairs_dev, total = *A.total;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *A.b_total = total;
+  if (pairs > A.cap_p || total > A.cap_b) return;
+  const uint32_t m = max(pairs + 1, A.n);
+  for (uint32_t i = blockIdx.x * WG + threadIdx.x; i < m; i += gridDim.x * WG) {
+    if (i < A.n) A.b_exact[i] = A.exact[i];
+    if (i <= pairs) A.b_ooff[i] = A.ooff[i];
+    if (i < pairs) {
+      const uint32_t f = A.fid[i], o = A.ooff[i];
+      A.b_fid[i] = f;
+      copy_filter(A.pool, A.foff[f], A.ooff[i + 1] - o, A.b_bytes + o);
+    }
   }
 }
 
@@ -418,9 +493,9 @@ hipError_t launch_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* 
     if (e == hipSuccess && total_dst) e = hipMemsetAsync(total_dst, 0, 4, s);
     return e;
   }
-  hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(WG), 0, s, in, n, tmp);
-  hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(WG), 0, s, in, n, tmp, nb, out, out + n,
-                     total_dst);
+  hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(WG), 0, s, in, n, tmp, (const uint32_t*)nullptr);
+  hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(WG), 0, s, in, n, tmp, nb, out, total_dst,
+                     (const uint32_t*)nullptr);
   return hipGetLastError();
 }
 
@@ -711,8 +786,20 @@ hipError_t launch_filter_len(const uint32_t* fid, uint32_t pairs, const uint64_t
                              hipStream_t s) {
   if (pairs)
     hipLaunchKernelGGL(k_filter_len, dim3(grid_for(pairs, 8192)), dim3(WG), 0, s, fid, pairs, foff,
-                       len);
+                       len, (const uint32_t*)nullptr);
   return launch_scan(len, ooff, pairs, tmp, total, s);
+}
+
+hipError_t launch_filter_len_dev(const uint32_t* fid, const uint32_t* pairs_dev, uint32_t cap,
+                                 const uint64_t* foff, uint32_t* len, uint32_t* ooff, uint32_t* tmp,
+                                 uint32_t* total, hipStream_t s) {
+  const uint32_t c = std::max<uint32_t>(cap, 1);
+  hipLaunchKernelGGL(k_filter_len, dim3(grid_for(c, 1024)), dim3(WG), 0, s, fid, c, foff, len, pairs_dev);
+  const uint32_t nb = (c + SCAN_TILE - 1) / SCAN_TILE;
+  hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(WG), 0, s, (const uint32_t*)len, c, tmp, pairs_dev);
+  hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(WG), 0, s, (const uint32_t*)len, c, (const uint32_t*)tmp,
+                     nb, ooff, total, pairs_dev);
+  return hipGetLastError();
 }
 
 hipError_t launch_filter_gather(const uint32_t* fid, uint32_t pairs, const uint64_t* foff,
@@ -721,6 +808,31 @@ hipError_t launch_filter_gather(const uint32_t* fid, uint32_t pairs, const uint6
   if (pairs)
     hipLaunchKernelGGL(k_filter_gather, dim3(grid_for(pairs, 8192)), dim3(WG), 0, s, fid, pairs,
                        foff, pool, ooff, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_fb_pack(const uint32_t* fid, const uint32_t* pairs_dev, const uint64_t* foff,
+                          const uint8_t* pool, const uint32_t* ooff, const uint32_t* total,
+                          const uint32_t* exact, uint32_t n, uint32_t cap_p, uint64_t cap_b,
+                          uint8_t* block, hipStream_t s) {
+  const FbLayout L(n, cap_p);
+  FbPack a;
+  a.fid = fid;
+  a.pairs_dev = pairs_dev;
+  a.foff = foff;
+  a.pool = pool;
+  a.ooff = ooff;
+  a.total = total;
+  a.exact = exact;
+  a.n = n;
+  a.cap_p = cap_p;
+  a.cap_b = cap_b;
+  a.b_total = (uint32_t*)(block + L.total);
+  a.b_ooff = (uint32_t*)(block + L.ooff);
+  a.b_fid = (uint32_t*)(block + L.fid);
+  a.b_exact = (uint32_t*)(block + L.exact);
+  a.b_bytes = block + L.bytes;
+  hipLaunchKernelGGL(k_fb_pack, dim3(grid_for(std::max<uint32_t>(cap_p + 1, n), 2048)), dim3(WG), 0, s, a);
   return hipGetLastError();
 }
 

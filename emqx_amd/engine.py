@@ -118,6 +118,7 @@ SYMBOLS = {
     "emqxgm_host_free": (None, [_P, C.c_void_p]),
     "emqxgm_match_device_wait": (C.c_int, [_P, C.c_uint64, C.POINTER(_DevOut)]),
     "emqxgm_match_batch_submit": (C.c_int, [_P, _P, _P, C.c_uint32, _U64P]),
+    "emqxgm_match_batch_submit_filters": (C.c_int, [_P, _P, _P, C.c_uint32, _U64P]),
     "emqxgm_match_batch_wait": (C.c_int, [_P, C.c_uint64, C.POINTER(_BatchOut)]),
     "emqxgm_match_batch_wait_filters": (C.c_int, [_P, C.c_uint64, C.POINTER(_BatchOut),
                                                   C.POINTER(_U32P), C.POINTER(_U8P)]),
@@ -465,15 +466,35 @@ class Engine:
 
     HOST_PIPES = 3  # EMQXGM_HOST_PIPES
 
-    def match_batch_submit(self, buf: np.ndarray, off: np.ndarray) -> int:
+    def match_batch_submit(self, buf: np.ndarray, off: np.ndarray, filters: bool = False) -> int:
         """emqxgm_match_batch_submit: host-in pass (H2D, device pass, results to pinned host
         memory) enqueued on one of HOST_PIPES streams.  `buf` / `off` (uint8 / uint32, off[0] ==
-        0) must stay alive and unchanged until the wait: keep a reference."""
+        0) must stay alive and unchanged until the wait: keep a reference.  filters=True:
+        emqxgm_match_batch_submit_filters (the filter-byte gather and every copy behind the pass,
+        for match_batch_wait_filters)."""
         assert off.dtype == np.uint32 and buf.dtype == np.uint8
         t = C.c_uint64(0)
-        self._check(self._lib.emqxgm_match_batch_submit(self._h, _ptr(buf), _ptr(off), len(off) - 1,
-                                                        C.byref(t)), "match_batch_submit")
+        fn = (self._lib.emqxgm_match_batch_submit_filters if filters
+              else self._lib.emqxgm_match_batch_submit)
+        self._check(fn(self._h, _ptr(buf), _ptr(off), len(off) - 1, C.byref(t)), "match_batch_submit")
         return int(t.value)
+
+    def match_batch_wait_filters(self, ticket: int):
+        """emqxgm_match_batch_wait_filters: (MatchResult, byte offsets [n_pairs + 1], filter
+        bytes), copies."""
+        o = _BatchOut()
+        fo, fb = _U32P(), _U8P()
+        self._check(self._lib.emqxgm_match_batch_wait_filters(self._h, ticket, C.byref(o),
+                                                              C.byref(fo), C.byref(fb)),
+                    "match_batch_wait_filters")
+        n, m = o.n, o.n_pairs
+        row = np.ctypeslib.as_array(o.row_ptr, shape=(n + 1,)).astype(np.uint64)
+        fid = np.ctypeslib.as_array(o.filter_id, shape=(m,)).copy() if m else np.zeros(0, np.uint32)
+        ex = np.ctypeslib.as_array(o.exact_id, shape=(n,)).copy() if n else np.zeros(0, np.uint32)
+        foff = np.ctypeslib.as_array(fo, shape=(m + 1,)).copy()
+        nb = int(foff[-1])
+        fbytes = np.ctypeslib.as_array(fb, shape=(nb,)).copy() if nb else np.zeros(0, np.uint8)
+        return MatchResult(row, fid, ex), foff, fbytes
 
     def match_batch_wait(self, ticket: int, copy: bool = True) -> MatchResult:
         """emqxgm_match_batch_wait: the host-resident result (row pointers as uint64 when copied;

@@ -231,6 +231,15 @@ int emqxgm_match_batch_wait(emqxgm_t* h, uint64_t ticket, emqxgm_batch_out* out)
  * build each caller's filter binaries without touching the host registry per pair. */
 int emqxgm_match_batch_wait_filters(emqxgm_t* h, uint64_t ticket, emqxgm_batch_out* out,
                                     const uint32_t** foff, const uint8_t** fbytes);
+/* _submit for a ticket that will be completed with _wait_filters: the filter-byte gather and the
+ * copies of every result array (filter ids, byte offsets, bytes, exact ids) are enqueued behind
+ * the pass -- packed on the device into one block that one copy brings into pinned memory --
+ * sized by the pairs and bytes per topic of the pipe's recent windows (x1.2), so that
+ * _wait_filters takes one stream synchronisation instead of four; a window beyond those sizes is
+ * finished there synchronously.  Same arguments, errors and results as _submit + _wait_filters
+ * (the NIF batcher core submits its windows this way). */
+int emqxgm_match_batch_submit_filters(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets,
+                                      uint32_t n, uint64_t* ticket);
 
 /* ---- publish fan-out (emqx_broker.erl:218-355) -------------------------------------------
  * Routes with dest identity: a plain route {Filter, Node} passes group = EMQXGM_NONE; a shared-

@@ -180,3 +180,39 @@ def test_batcher_add_many_packs_like_add(emqx):
         b.add_many(np.zeros(200, np.uint8), np.array([0, 200], np.uint32))
     assert b.add_many(buf, np.array([3, 6, 2], np.uint32)) == 1  # stops before the bad offset
     b.close()
+
+
+def test_submit_filters_one_sync_equals_sync_gather(emqx):
+    """emqxgm_match_batch_submit_filters enqueues the filter-byte gather and one packed copy of
+    every result array behind the pass, sized from the pipe's recent windows; a window beyond
+    those sizes (the first ones, a sudden denser window) is finished synchronously in the wait.
+    Windows of changing size and density: identical to submit + the synchronous gather, and each
+    pair's bytes are its filter's."""
+    import workloads
+    w = workloads.generate(1, None, 120_000)
+    eng = emqx.Engine()
+    eng.route_ref_many(w.fbytes, w.foff)
+    eng.trie_insert_many(w.fbytes, w.foff)
+    for i in range(0, w.nt, 9):  # some names are route keys: exact ids in the block
+        eng.route_ref(w.topic(i))
+    eng.commit()
+    off = w.toff.astype(np.int64)
+    dense = np.frombuffer(b"l0w0/l1w0/l2w0/l3w0" * 1, np.uint8)
+    plan = [(0, 4096), (4096, 4096), (8192, 30000), (38192, 0), (38192, 100), (38292, 4096),
+            (42388, 60000), (102388, 4096)]
+    for k, (i, m) in enumerate(plan):
+        buf = w.tbytes[off[i]:off[i + m]].copy()
+        o = (off[i:i + m + 1] - off[i]).astype(np.uint32)
+        if k == 5:  # a window of one dense topic repeated: far more pairs per topic than before
+            buf = np.tile(dense, m)
+            o = (np.arange(m + 1) * dense.size).astype(np.uint32)
+        res = []
+        for filters in (True, False):
+            t = eng.match_batch_submit(buf, o, filters=filters)
+            res.append(eng.match_batch_wait_filters(t))
+        (a, fa, ba), (b, fb, bb) = res
+        assert np.array_equal(a.row_ptr, b.row_ptr) and np.array_equal(a.filter_id, b.filter_id)
+        assert np.array_equal(a.exact_id, b.exact_id), k
+        assert np.array_equal(fa, fb) and np.array_equal(ba, bb), k
+        for j in range(0, a.filter_id.size, 97):
+            assert ba[fa[j]:fa[j + 1]].tobytes() == eng.filter_bytes(int(a.filter_id[j]))
