@@ -121,7 +121,10 @@ constexpr uint32_t REJ_SCAN_MAX = 4096;  // rejects the deferred scatter handles
 #endif
 constexpr bool WALK_CPT = GM_WALK_CPT != 0;
 constexpr uint32_t WALK_STK_SHALLOW = WALK_CPT ? 12 : 6;
-constexpr uint32_t WALK_STK_DEEP = WALK_CPT ? 24 : 12;
+#ifndef GM_WALK_STK_DEEP_CPT  // A/B builds may override it
+#define GM_WALK_STK_DEEP_CPT 24
+#endif
+constexpr uint32_t WALK_STK_DEEP = WALK_CPT ? GM_WALK_STK_DEEP_CPT : 12;
 constexpr uint32_t WALK_STK_SPILL = 12;
 enum WalkLevel : uint32_t { WALK_SHALLOW = 0, WALK_DEEP = 1, WALK_SPILL = 2 };
 constexpr uint32_t WALK_SPILL_MIN = 32;  // initial spill items per lane (grown on overflow)
