@@ -1566,7 +1566,8 @@ int ensure_scratch(emqxgm* h, PassCtx& c, uint32_t n, uint64_t words, uint32_t p
       (rc = dev_alloc(h, c, (void**)&s.rlist, (size_t)h->reject_cap * 8)))
     return rc;
   s.r_cap = h->reject_cap;
-  HIPCHK(h, hipHostMalloc((void**)&s.ctl_host, CTL_N * 4, hipHostMallocDefault));
+  HIPCHK(h, hipHostMalloc((void**)&s.ctl_host, CTL_N * 4, hipHostMallocMapped | hipHostMallocPortable));
+  HIPCHK(h, hipHostGetDevicePointer((void**)&s.ctl_host_dev, s.ctl_host, 0));
   s.n_cap = ncap;
   s.w_cap = wcap;
   s.p_cap = pcap;
@@ -1608,6 +1609,9 @@ int pass_prepare(emqxgm* h, PassCtx& c, uint32_t n, uint64_t bytes_len) {
   return 0;
 }
 
+#ifndef GM_CTL_KERNEL  // A/B builds may override it: the control words to the host by a kernel
+#define GM_CTL_KERNEL 1
+#endif
 // Every launch of one pass against epoch E on the context's stream (caller holds emu).
 int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
                  const uint32_t* d_off, uint32_t n, bool legacy, bool census) {
@@ -1619,7 +1623,8 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
   if (hipEventQuery(E.ready) != hipSuccess) HIPCHK(h, hipStreamWaitEvent(st, E.ready, 0));
   if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[0], st));
   RoctxRange rr(h->roctx, census ? "emqxgm.pass.census" : "emqxgm.pass");
-  HIPCHK(h, hipMemsetAsync(s.ctl, 0, CTL_N * 4, st));
+  // k_tok starts the control words (no memset launch); CTL_XHIT compares to this pass's number
+  s.xseq = s.xseq + 1 ? s.xseq + 1 : 1;
   if (census)
     HIPCHK(h, hipMemsetAsync(s.census, 0,
                              (CENSUS_HDR + 3 * (h->geom.lanes / 64)) * sizeof(unsigned long long),
@@ -1628,7 +1633,11 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
   c.walk_level = (census ? E.census_level : E.walk_level).load(std::memory_order_relaxed);
   const uint32_t stat = ix.trie_empty ? 0u : walk_static_chunks(h->geom, n, c.walk_level, s.p_cap);
   roctx_mark(h->roctx, "k_tok");
-  HIPCHK(h, launch_tok(d_bytes, d_off, n, ix, s, st, stat * STAGE_CHUNK));
+  // (per-topic reject counts: only the verification passes write -- and then read -- them;
+  // k_tok zeroes them as it goes, like the control words: a memset launch between the passes of
+  // two pipes serialised them, r03)
+  HIPCHK(h, launch_tok(d_bytes, d_off, n, ix, s, st, stat * STAGE_CHUNK,
+                       !ix.trie_empty && (ix.needs_verify || legacy)));
   if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[4], st));
   roctx_mark(h->roctx, "k_exact");
   HIPCHK(h, launch_exact(d_bytes, d_off, n, ix, s, h->geom, st));
@@ -1636,8 +1645,6 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
   if (ix.trie_empty) {
     HIPCHK(h, hipMemsetAsync(s.row, 0, (size_t)(n + 1) * 4, st));
   } else {
-    // per-topic reject counts: only the verification passes write (and then read) them
-    if (ix.needs_verify || legacy) HIPCHK(h, hipMemsetAsync(s.rej, 0, (size_t)n * 4, st));
     roctx_mark(h->roctx, "k_walk");
     HIPCHK(h, launch_walk(ix, s, n, h->geom, st, census ? s.census : nullptr, c.walk_level, stat));
     if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[2], st));
@@ -1655,7 +1662,11 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
     }
   }
   if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[3], st));
+#if GM_CTL_KERNEL
+  HIPCHK(h, launch_ctl_out(s.ctl, s.ctl_host_dev, st));
+#else
   HIPCHK(h, hipMemcpyAsync(s.ctl_host, s.ctl, CTL_N * 4, hipMemcpyDeviceToHost, st));
+#endif
   return 0;
 }
 
@@ -2093,7 +2104,7 @@ int host_pipe_complete(emqxgm* h, emqxgm::HostPipe& p, bool gather = false) {
   }
   // a redone pass refreshed ctl_host
   const bool exact_copied = rows_copied && mode1;
-  p.exact_none = !exact_copied && s.ctl_host[CTL_XHIT] == 0;
+  p.exact_none = !exact_copied && s.ctl_host[CTL_XHIT] != s.xseq;
   if (!exact_copied && !p.exact_none) {
     HIPCHK(h, hipMemcpyAsync(p.h_exact, s.exact_id, (size_t)p.n * 4, hipMemcpyDeviceToHost, p.c.stream));
     enq = true;

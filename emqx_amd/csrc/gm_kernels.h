@@ -59,6 +59,7 @@ struct Scratch {
   uint32_t p_cap = 0;   // pair staging capacity
   uint3* stg = nullptr;       // staged pairs {topic, filter, rank | REJ_BIT} (12 B), CH-slot chunks
   uint32_t* chk = nullptr;    // per staged chunk: pairs in it (written by the walk)
+  uint32_t xseq = 1;          // this pass's sequence number (CTL_XHIT), set by the engine
   uint32_t o_cap = 0;
   uint32_t* out = nullptr;    // [pairs] CSR filter ids
   uint32_t* out2 = nullptr;   // legacy fix-up target
@@ -70,7 +71,8 @@ struct Scratch {
   uint32_t spill_lanes = 0;   // walk lanes the spill was sized for
   uint2* rlist = nullptr;     // rejected (topic, rank) list
   uint32_t r_cap = 0;
-  uint32_t* ctl_host = nullptr;  // pinned host mirror of ctl
+  uint32_t* ctl_host = nullptr;  // pinned host mirror of ctl (mapped: k_ctl_out writes it)
+  uint32_t* ctl_host_dev = nullptr;  // its device-side address
   unsigned long long* census = nullptr;  // [CENSUS_N] diagnostic walk counters
 };
 
@@ -79,7 +81,8 @@ enum : int {
   CTL_PAIR_TOP = 1,   // staged pair slots reserved
   CTL_ANY_REJ = 2,    // a verification rejected some pair
   CTL_TOTAL = 3,      // total pairs (row[n]) copied here
-  CTL_XHIT = 4,       // some name of the batch has an exact route key (else exact_id is all NONE)
+  CTL_XHIT = 4,       // == Scratch::xseq: some name of the batch has an exact route key (else
+                      // exact_id is all NONE); the word is never cleared, k_tok zeroes the rest
   CTL_NREJ = 5,       // rejected pairs appended to rlist
   CTL_LEGACY = 6,     // deferred scatter could not place rejects: re-run with the fix-up path
   CTL_ERR = 7,        // walk item stack outgrew its spill: re-run with a larger spill
@@ -151,7 +154,7 @@ uint32_t scan_tmp_words(uint32_t n);
 // deeper levels (wh, at off[t] + t + level); exact route-key ids (exact_id, NONE if absent)
 // of wildcard names when there are no plain keys, else X_WILDPEND marks for launch_exact
 hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
-                      Scratch& sc, hipStream_t s, uint32_t pair_top0);
+                      Scratch& sc, hipStream_t s, uint32_t pair_top0, bool zero_rej);
 // exact route-key ids of every name (after launch_tok; a no-op when there are no plain keys)
 hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
                         Scratch& sc, const WalkGeom& g, hipStream_t s);
@@ -227,6 +230,9 @@ struct CopyOut {
   const uint32_t* n_dev;
   uint32_t cap;
 };
+// The pass's control words into the mapped host mirror (one block; replaces a D2H copy, which
+// the runtime runs as a blit with more overhead between two pipes' passes).
+hipError_t launch_ctl_out(const uint32_t* ctl, uint32_t* ctl_host_dev, hipStream_t s);
 hipError_t launch_copy_out(const CopyOut& a, const CopyOut& b, const CopyOut& c, hipStream_t s);
 // Filter-sharded layout: a shard's result copied with its ids mapped to global ids (map NULL:
 // identity), and np shards' results merged (parts: np x {row, fid, exact} device pointers, in

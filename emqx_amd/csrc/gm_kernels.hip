@@ -23,6 +23,9 @@ constexpr uint32_t CH = STAGE_CHUNK;  // staged-pair slots reserved per wave per
 #ifndef GM_STATIC_ONE  // A/B builds may override it
 #define GM_STATIC_ONE 1
 #endif
+#ifndef GM_SMALL_WS  // A/B builds may override it: probe slots of the one-topic-per-lane walk
+#define GM_SMALL_WS 2  // r03: 4 slots (158 VGPRs) cost cfg3 64k-topic walks 0.019 -> 0.023 ms
+#endif
 #ifndef GM_STATIC_CHUNK  // A/B builds may override it
 #define GM_STATIC_CHUNK 1
 #endif
@@ -226,6 +229,10 @@ __global__ __launch_bounds__(WG) void k_row64(const uint32_t* row, uint64_t base
 
 // Three result arrays into pinned host memory (blockIdx.y picks one): 16-B stores over the
 // body, the ragged tail by the first block.
+__global__ __launch_bounds__(WG) void k_ctl_out(const uint32_t* ctl, uint32_t* dst) {
+  for (uint32_t i = threadIdx.x; i < CTL_N; i += WG) dst[i] = ctl[i];
+}
+
 __global__ __launch_bounds__(WG) void k_copy_out(CopyOut a0, CopyOut a1, CopyOut a2) {
   const CopyOut d = blockIdx.y == 0 ? a0 : blockIdx.y == 1 ? a1 : a2;
   const uint32_t n = d.n_dev ? min(*d.n_dev, d.cap) : d.n;
@@ -499,8 +506,9 @@ hipError_t launch_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* 
   return hipGetLastError();
 }
 
-static ExactArgs exact_args(const DevIndex& ix) {
+static ExactArgs exact_args(const DevIndex& ix, uint32_t xseq) {
   ExactArgs x;
+  x.xseq = xseq;
   x.exact = ix.exact;
   x.xovf = ix.xovf;
   x.xmask = ix.xmask;
@@ -513,10 +521,11 @@ static ExactArgs exact_args(const DevIndex& ix) {
 }
 
 hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
-                      Scratch& sc, hipStream_t s, uint32_t pair_top0) {
+                      Scratch& sc, hipStream_t s, uint32_t pair_top0, bool zero_rej) {
   if (n == 0) return hipSuccess;
   TokArgs a;
   a.pair_top0 = pair_top0;
+  a.rej = zero_rej ? sc.rej : nullptr;
   a.bytes = bytes;
   a.off = off;
   a.n = n;
@@ -528,9 +537,9 @@ hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, con
   a.test_mask = ix.test_mask;
   a.wild_empty = ix.wild_empty;
   if (ix.plain_empty)
-    hipLaunchKernelGGL(k_tok<false>, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a, exact_args(ix));
+    hipLaunchKernelGGL(k_tok<false>, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a, exact_args(ix, sc.xseq));
   else
-    hipLaunchKernelGGL(k_tok<true>, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a, exact_args(ix));
+    hipLaunchKernelGGL(k_tok<true>, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a, exact_args(ix, sc.xseq));
   return hipGetLastError();
 }
 
@@ -543,10 +552,10 @@ hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, c
   if ((!forced && (buckets * 64ull <= XRANGE_MIN_TABLE || n < XRANGE_MIN_NAMES)) ||
       buckets >= NONE) {
     hipLaunchKernelGGL(k_exact, dim3(grid_for(n, 1u << 20)), dim3(WG), 0, s, bytes, off, n,
-                       sc.exact_id, exact_args(ix), ix.wild_empty, sc.ctl);
+                       sc.exact_id, exact_args(ix, sc.xseq), ix.wild_empty, sc.ctl);
     return hipGetLastError();
   }
-  const ExactArgs X = exact_args(ix);
+  const ExactArgs X = exact_args(ix, sc.xseq);
   hipLaunchKernelGGL(k_xhash, dim3(grid_for(n, 1u << 20)), dim3(WG), 0, s, bytes, off, n,
                      sc.exact_id, X, ix.wild_empty, sc.xh);
   for (uint64_t lo = 0; lo < buckets; lo += rb) {
@@ -636,6 +645,12 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
       hipLaunchKernelGGL((k_walk<true, false, DP, C>), grid, dim3(WG), 0, s, a);
     else
       hipLaunchKernelGGL((k_walk<true, false, SH, C>), grid, dim3(WG), 0, s, a);
+  } else if (a.static_one && GM_SMALL_WS != WSLOTS && level < WALK_SPILL && blocks <= 3 * g.cus) {
+    // one topic per lane: the 4-slot variants (fewer, wider iterations; three blocks per CU)
+    if (level == WALK_DEEP)
+      hipLaunchKernelGGL((k_walk<false, false, DP, C, GM_SMALL_WS>), grid, dim3(WG), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_walk<false, false, SH, C, GM_SMALL_WS>), grid, dim3(WG), 0, s, a);
   } else {
     if (level >= WALK_SPILL)
       hipLaunchKernelGGL((k_walk<false, true, SP>), grid, dim3(WG), 0, s, a);
@@ -833,6 +848,11 @@ hipError_t launch_fb_pack(const uint32_t* fid, const uint32_t* pairs_dev, const 
   a.b_exact = (uint32_t*)(block + L.exact);
   a.b_bytes = block + L.bytes;
   hipLaunchKernelGGL(k_fb_pack, dim3(grid_for(std::max<uint32_t>(cap_p + 1, n), 2048)), dim3(WG), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_ctl_out(const uint32_t* ctl, uint32_t* ctl_host_dev, hipStream_t s) {
+  hipLaunchKernelGGL(k_ctl_out, dim3(1), dim3(WG), 0, s, ctl, ctl_host_dev);
   return hipGetLastError();
 }
 

@@ -100,7 +100,7 @@ hipError_t launch_patch(const PatchEnt* ents, uint32_t n, const uint32_t* src, h
 // the match pipeline does not run in the harness (it walks the tables on the CPU itself)
 #define NOT_HERE return hipErrorUnknown
 hipError_t launch_scan(const uint32_t*, uint32_t*, uint32_t, uint32_t*, uint32_t*, hipStream_t) { NOT_HERE; }
-hipError_t launch_tok(const uint8_t*, const uint32_t*, uint32_t, const DevIndex&, Scratch&, hipStream_t, uint32_t) { NOT_HERE; }
+hipError_t launch_tok(const uint8_t*, const uint32_t*, uint32_t, const DevIndex&, Scratch&, hipStream_t, uint32_t, bool) { NOT_HERE; }
 hipError_t launch_exact(const uint8_t*, const uint32_t*, uint32_t, const DevIndex&, Scratch&, const WalkGeom&, hipStream_t) { NOT_HERE; }
 hipError_t launch_walk(const DevIndex&, Scratch&, uint32_t, const WalkGeom&, hipStream_t, unsigned long long*, uint32_t, uint32_t) { NOT_HERE; }
 uint32_t walk_blocks(const WalkGeom&, uint32_t, uint32_t) { return 0; }
@@ -113,6 +113,7 @@ hipError_t launch_row64(const uint32_t*, uint64_t, uint64_t*, uint32_t, hipStrea
 hipError_t launch_fanout(const DevIndex&, const Scratch&, FanScratch&, uint32_t, bool, hipStream_t) { NOT_HERE; }
 hipError_t launch_rules(const uint8_t*, const uint32_t*, uint32_t, const uint8_t*, const uint32_t*, const uint32_t*, uint32_t, uint64_t, uint32_t*, hipStream_t) { NOT_HERE; }
 hipError_t launch_copy_out(const CopyOut&, const CopyOut&, const CopyOut&, hipStream_t) { NOT_HERE; }
+hipError_t launch_ctl_out(const uint32_t*, uint32_t*, hipStream_t) { NOT_HERE; }
 hipError_t launch_export(const uint32_t*, const uint32_t*, const uint32_t*, uint32_t, uint32_t, const uint32_t*, uint32_t*, uint32_t*, uint32_t*, hipStream_t) { NOT_HERE; }
 hipError_t launch_merge(const uint32_t* const*, uint32_t, uint32_t, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, hipStream_t) { NOT_HERE; }
 
