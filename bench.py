@@ -69,6 +69,8 @@ def main():
                          "('' = skip); rank 0, N=1, with the host-in/host-out timing")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="device passes in flight (default: EMQXGM_PIPES)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one pass at a time (emqxgm_match_device) instead of two in flight")
     ap.add_argument("--no-route-keys", action="store_true",
@@ -151,6 +153,7 @@ def main():
     # one batch's walk tail overlaps the next batch's tokenizer and walk; drain() completes the
     # last one inside the timed region.  Every batch is matched in full either way.
     pipelined = not args.no_pipeline
+    dev_inflight = min(args.inflight or eng.PIPES, eng.PIPES)
     pending = []
     turn = [0]
 
@@ -166,7 +169,7 @@ def main():
     def step_pipe():
         b_, o_, n_ = next_batch()
         pending.append(eng.match_device_submit(b_.data_ptr(), o_.data_ptr(), w.nt, n_))
-        if len(pending) == eng.PIPES:
+        if len(pending) == dev_inflight:
             eng.match_device_wait(pending.pop(0))
 
     def drain():
@@ -343,7 +346,7 @@ def main():
                                         for k, v in census["loads_by_level"].items()},
                 "pipeline_ms_per_batch": round(pipe_ms, 4),
                 "tune": args.tune,
-                "passes_in_flight": eng.PIPES if pipelined else 1,
+                "passes_in_flight": dev_inflight if pipelined else 1,
                 "one_pass_at_a_time": (None if sync_ms is None else {
                     "value": round(topics_total / (sync_ms * 1e-3), 1), "ms_per_step": round(sync_ms, 4)}),
                 "pairs_per_s": round(census["pairs"] * (topics_total / w.nt) / (elapsed / args.steps), 1),

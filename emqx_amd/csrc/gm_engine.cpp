@@ -1408,8 +1408,12 @@ int publish_epoch(emqxgm* h, bool delta) {
   }
   if (!h->patches.ents.empty()) {
     int rc = 0;
+    // every pass was enqueued under emu, which this commit holds: an event recorded now on a
+    // reader's stream follows its last pass (no event per pass: r03)
     for_each_reader(h, [&](PassCtx& c) {
-      if (!rc && c.done_rec && hipStreamWaitEvent(h->wstream, c.done, 0) != hipSuccess)
+      if (!rc && c.stream && c.done &&
+          (hipEventRecord(c.done, c.stream) != hipSuccess ||
+           hipStreamWaitEvent(h->wstream, c.done, 0) != hipSuccess))
         rc = fail(h, hipErrorUnknown, "hipStreamWaitEvent(writer, reader pass)");
     });
     if (rc || (rc = patch_flush(h))) return rc;
@@ -1673,8 +1677,12 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
 // Marks the end of the table reads a context enqueued (caller holds emu): a later delta commit
 // orders its patches behind this point.
 int mark_done(emqxgm* h, PassCtx& c) {
+#ifdef GM_AB_PASS_EVENT  // A/B builds: an event per pass, as until r03
   HIPCHK(h, hipEventRecord(c.done, c.stream));
   c.done_rec = true;
+#else
+  (void)h, (void)c;
+#endif
   return 0;
 }
 

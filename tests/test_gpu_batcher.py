@@ -163,7 +163,30 @@ def test_batcher_add_many_packs_like_add(emqx):
     off = np.zeros(len(topics) + 1, np.uint32)
     np.cumsum(lens, out=off[1:])
     off += len(pad)
-    one = _drive(emqx, emqx.Batcher(eng, window_topics=64, window_bytes=160), topics, 1)
+    # the reference packing: one add per topic, a flush whenever the window is full or has no
+    # room for the next topic (-ENOSPC), never on time (window_us far away)
+    one = {}
+    b1 = emqx.Batcher(eng, window_topics=64, window_bytes=160, window_us=10**9)
+
+    def flush1():
+        wid = b1.flush()
+        if not wid:
+            return
+        w1 = b1.collect(wid)
+        for j in range(len(w1.tag)):
+            one[int(w1.tag[j])] = (w1.filters(j), int(w1.exact_id[j]))
+
+    for i, t in enumerate(topics):
+        try:
+            full = b1.add(t, i)
+        except emqx.EngineError as e:
+            assert "ENOSPC" in str(e)
+            flush1()
+            full = b1.add(t, i)
+        if full:
+            flush1()
+    flush1()
+    b1.close()
     b = emqx.Batcher(eng, window_topics=64, window_bytes=160)
     got, i = {}, 0
     while i < len(topics):

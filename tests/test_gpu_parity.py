@@ -680,7 +680,7 @@ def _dev_to_host(d, n):
 
 
 def test_pipelined_passes(emqx):
-    """emqxgm_match_device_submit/_wait: several batches in flight on two pipes give exactly the
+    """emqxgm_match_device_submit/_wait: several batches in flight on the pipes give exactly the
     synchronous results; a staging overflow inside a pipe is redone; empty batches; -EBUSY for a
     third submission before the first wait; a commit completes the passes in flight against the
     index they were submitted on."""
@@ -724,9 +724,14 @@ def test_pipelined_passes(emqx):
     db, do = dev[0]
     n0 = len(batches[0][1]) - 1
     t_a = eng.match_device_submit(db.data_ptr(), do.data_ptr(), n0, int(batches[0][1][-1]))
-    with pytest.raises(emqx.EngineError):  # pipe of the last ticket still holds its pass
+    extra = [eng.match_device_submit(db.data_ptr(), do.data_ptr(), n0, int(batches[0][1][-1]))
+             for _ in range(eng.PIPES - 2)]  # every pipe holds a pass now
+    with pytest.raises(emqx.EngineError):  # pipe of the oldest ticket still holds its pass
         eng.match_device_submit(db.data_ptr(), do.data_ptr(), n0, int(batches[0][1][-1]))
     got.append(_dev_to_host(eng.match_device_wait(tickets[-1]), len(batches[-1][1]) - 1))
+    for t in extra:
+        assert all(np.array_equal(x, y) for x, y in zip(_dev_to_host(eng.match_device_wait(t), n0),
+                                                        want[0]))
     for i, (a, b) in enumerate(zip(want, got)):
         for x, y in zip(a, b):
             assert np.array_equal(x, y), i
