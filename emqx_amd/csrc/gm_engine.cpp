@@ -1616,6 +1616,9 @@ int pass_prepare(emqxgm* h, PassCtx& c, uint32_t n, uint64_t bytes_len) {
 #ifndef GM_CTL_KERNEL  // A/B builds may override it: the control words to the host by a kernel
 #define GM_CTL_KERNEL 1
 #endif
+#ifndef GM_CTL_IN_SCAN  // A/B builds may override it: ... by the row scan's last block
+#define GM_CTL_IN_SCAN 1
+#endif
 // Every launch of one pass against epoch E on the context's stream (caller holds emu).
 int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
                  const uint32_t* d_off, uint32_t n, bool legacy, bool census) {
@@ -1627,6 +1630,7 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
   if (hipEventQuery(E.ready) != hipSuccess) HIPCHK(h, hipStreamWaitEvent(st, E.ready, 0));
   if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[0], st));
   RoctxRange rr(h->roctx, census ? "emqxgm.pass.census" : "emqxgm.pass");
+  bool ctl_sent = false;  // the control words already go to the host mirror
   // k_tok starts the control words (no memset launch); CTL_XHIT compares to this pass's number
   s.xseq = s.xseq + 1 ? s.xseq + 1 : 1;
   if (census)
@@ -1640,8 +1644,10 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
   // (per-topic reject counts: only the verification passes write -- and then read -- them;
   // k_tok zeroes them as it goes, like the control words: a memset launch between the passes of
   // two pipes serialised them, r03)
+  uint32_t claim0[WALK_SHARDS] = {};
+  if (!ix.trie_empty) walk_claim_init(h->geom, n, c.walk_level, claim0);
   HIPCHK(h, launch_tok(d_bytes, d_off, n, ix, s, st, stat * STAGE_CHUNK,
-                       !ix.trie_empty && (ix.needs_verify || legacy)));
+                       !ix.trie_empty && (ix.needs_verify || legacy), claim0));
   if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[4], st));
   roctx_mark(h->roctx, "k_exact");
   HIPCHK(h, launch_exact(d_bytes, d_off, n, ix, s, h->geom, st));
@@ -1657,20 +1663,28 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
       roctx_mark(h->roctx && ix.needs_verify, "k_verify");
       if (ix.needs_verify) HIPCHK(h, launch_verify(d_bytes, d_off, ix, s, n, h->geom, st));
       roctx_mark(h->roctx, "k_scan");
+#if GM_CTL_IN_SCAN
+      // the scan's last block mirrors the control words to the host (no launch of its own)
+      HIPCHK(h, launch_scan_ctl(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, s.ctl, s.ctl_host_dev, st));
+      ctl_sent = true;
+#else
       HIPCHK(h, launch_scan(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, st));
+#endif
       roctx_mark(h->roctx, "k_scatter");
-      HIPCHK(h, launch_scatter(s, n, h->geom, st));
+      HIPCHK(h, launch_scatter(s, n, h->geom, st, ctl_sent));
     } else {
       HIPCHK(h, launch_scan(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, st));
       HIPCHK(h, launch_verify_scatter(d_bytes, d_off, ix, s, n, st));
     }
   }
   if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[3], st));
+  if (!ctl_sent) {
 #if GM_CTL_KERNEL
-  HIPCHK(h, launch_ctl_out(s.ctl, s.ctl_host_dev, st));
+    HIPCHK(h, launch_ctl_out(s.ctl, s.ctl_host_dev, st));
 #else
-  HIPCHK(h, hipMemcpyAsync(s.ctl_host, s.ctl, CTL_N * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipMemcpyAsync(s.ctl_host, s.ctl, CTL_N * 4, hipMemcpyDeviceToHost, st));
 #endif
+  }
   return 0;
 }
 

@@ -154,7 +154,8 @@ uint32_t scan_tmp_words(uint32_t n);
 // deeper levels (wh, at off[t] + t + level); exact route-key ids (exact_id, NONE if absent)
 // of wildcard names when there are no plain keys, else X_WILDPEND marks for launch_exact
 hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
-                      Scratch& sc, hipStream_t s, uint32_t pair_top0, bool zero_rej);
+                      Scratch& sc, hipStream_t s, uint32_t pair_top0, bool zero_rej,
+                      const uint32_t* claim0 = nullptr);
 // exact route-key ids of every name (after launch_tok; a no-op when there are no plain keys)
 hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
                         Scratch& sc, const WalkGeom& g, hipStream_t s);
@@ -209,13 +210,20 @@ hipError_t launch_fanout(const DevIndex& ix, const Scratch& sc, FanScratch& fs, 
 // starts CTL_PAIR_TOP at static_chunks * STAGE_CHUNK
 uint32_t walk_blocks(const WalkGeom& g, uint32_t n, uint32_t level);
 uint32_t walk_static_chunks(const WalkGeom& g, uint32_t n, uint32_t level, uint32_t pcap);
+// the claim counters' start values past the walk's static first claims (k_tok sets them)
+void walk_claim_init(const WalkGeom& g, uint32_t n, uint32_t level, uint32_t claim0[WALK_SHARDS]);
 hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGeom& g,
                        hipStream_t s, unsigned long long* census = nullptr,
                        uint32_t level = WALK_SHALLOW, uint32_t stat_chunks = 0);
 // production: verify (flags + counts) -> [scan] -> deferred scatter
 hipError_t launch_verify(const uint8_t* bytes, const uint32_t* off, const DevIndex& ix,
                          Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_t s);
-hipError_t launch_scatter(Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_t s);
+hipError_t launch_scatter(Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_t s,
+                          bool mirror_ctl = false);
+// a pass's row scan whose last block also copies the control words to the host mirror
+hipError_t launch_scan_ctl(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* tmp,
+                           uint32_t* total_dst, const uint32_t* ctl, uint32_t* ctl_host_dev,
+                           hipStream_t s);
 // legacy path (reject list overflow): scan -> verify+scatter -> compaction
 hipError_t launch_verify_scatter(const uint8_t* bytes, const uint32_t* off, const DevIndex& ix,
                                  Scratch& sc, uint32_t n, hipStream_t s);

@@ -26,6 +26,9 @@ constexpr uint32_t CH = STAGE_CHUNK;  // staged-pair slots reserved per wave per
 #ifndef GM_SMALL_WS  // A/B builds may override it: probe slots of the one-topic-per-lane walk
 #define GM_SMALL_WS 2  // r03: 4 slots (158 VGPRs) cost cfg3 64k-topic walks 0.019 -> 0.023 ms
 #endif
+#ifndef GM_STATIC_CLAIM  // A/B builds may override it
+#define GM_STATIC_CLAIM 1
+#endif
 #ifndef GM_STATIC_CHUNK  // A/B builds may override it
 #define GM_STATIC_CHUNK 1
 #endif
@@ -174,7 +177,9 @@ __global__ __launch_bounds__(WG) void k_scan_final(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ part, uint32_t nb,
                                                    uint32_t* __restrict__ out,
                                                    uint32_t* __restrict__ total_dst,
-                                                   const uint32_t* __restrict__ n_dev) {
+                                                   const uint32_t* __restrict__ n_dev,
+                                                   const uint32_t* __restrict__ ctl_src = nullptr,
+                                                   uint32_t* __restrict__ ctl_dst = nullptr) {
   __shared__ uint32_t s_w[WG / 64];
   if (n_dev) {
     n = scan_count(n, n_dev);
@@ -213,6 +218,12 @@ __global__ __launch_bounds__(WG) void k_scan_final(const uint32_t* __restrict__ 
     *out_n = carry + tot;
     if (total_dst) *total_dst = carry + tot;
   }
+  // a pass's row scan: its last block also copies the control words to the host mirror (every
+  // kernel that writes them has finished but k_scatter, which mirrors its one word itself);
+  // CTL_TOTAL is this block's own result
+  if (ctl_dst && blockIdx.x == nb - 1)
+    for (uint32_t i = threadIdx.x; i < CTL_N; i += WG)
+      ctl_dst[i] = i == CTL_TOTAL ? carry + tot : ctl_src[i];
 }
 
 #include "gm_tok.inc"
@@ -491,6 +502,17 @@ WalkGeom walk_geometry(int device, uint32_t wg_per_cu) {
 
 uint32_t scan_tmp_words(uint32_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 1; }
 
+hipError_t launch_scan_ctl(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* tmp,
+                           uint32_t* total_dst, const uint32_t* ctl, uint32_t* ctl_host_dev,
+                           hipStream_t s) {
+  const uint32_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+  if (nb == 0) return hipErrorInvalidValue;  // a pass has topics
+  hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(WG), 0, s, in, n, tmp, (const uint32_t*)nullptr);
+  hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(WG), 0, s, in, n, tmp, nb, out, total_dst,
+                     (const uint32_t*)nullptr, ctl, ctl_host_dev);
+  return hipGetLastError();
+}
+
 hipError_t launch_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* tmp,
                        uint32_t* total_dst, hipStream_t s) {
   const uint32_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
@@ -521,9 +543,11 @@ static ExactArgs exact_args(const DevIndex& ix, uint32_t xseq) {
 }
 
 hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
-                      Scratch& sc, hipStream_t s, uint32_t pair_top0, bool zero_rej) {
+                      Scratch& sc, hipStream_t s, uint32_t pair_top0, bool zero_rej,
+                      const uint32_t* claim0) {
   if (n == 0) return hipSuccess;
   TokArgs a;
+  for (uint32_t cs = 0; cs < WALK_SHARDS; ++cs) a.claim0[cs] = claim0 ? claim0[cs] : 0u;
   a.pair_top0 = pair_top0;
   a.rej = zero_rej ? sc.rej : nullptr;
   a.bytes = bytes;
@@ -584,6 +608,31 @@ uint32_t walk_blocks(const WalkGeom& g, uint32_t n, uint32_t level) {
   return blocks;
 }
 
+// Topics per claim: a batch too small to give every wave TBLK topics is spread over all of them
+// (a 100k-topic batch would otherwise keep 3 in 4 waves idle).
+static uint32_t walk_tblk(uint32_t blocks, uint32_t n) {
+  const uint32_t waves = blocks * (WG / 64);
+  const uint32_t per_wave = waves ? (n + waves - 1) / waves : TBLK;
+  return per_wave >= TBLK ? TBLK : ((per_wave + 7) & ~7u) < 8 ? 8 : ((per_wave + 7) & ~7u);
+}
+
+// Static first claims: wave r of shard cs's blocks (block b walks shard b % 8 first) owns the
+// shard's topic block r without an atomic; the shard's counter starts past them (set by k_tok).
+// Every wave claims at the start of a pass, ~500 atomics on each counter at once (r03).
+// claim0[cs] = the counter's start value (0: none).
+void walk_claim_init(const WalkGeom& g, uint32_t n, uint32_t level, uint32_t claim0[WALK_SHARDS]) {
+  const uint32_t blocks = walk_blocks(g, n, level);
+  const uint32_t tblk = walk_tblk(blocks, n);
+  // exactly the walk's condition: claims at all (not static_one), static first ones
+  const bool on = GM_STATIC_CLAIM && !(GM_STATIC_ONE && (uint64_t)n <= (uint64_t)blocks * WG);
+  for (uint32_t cs = 0; cs < WALK_SHARDS; ++cs) {
+    const uint32_t lo = (uint32_t)((uint64_t)n * cs / WALK_SHARDS);
+    const uint32_t hi = (uint32_t)((uint64_t)n * (cs + 1) / WALK_SHARDS);
+    const uint64_t waves = (uint64_t)(blocks > cs ? (blocks - cs + WALK_SHARDS - 1) / WALK_SHARDS : 0) * (WG / 64);
+    claim0[cs] = on ? (uint32_t)std::min<uint64_t>(waves * tblk, hi - lo) : 0u;
+  }
+}
+
 // Staged-pair chunks handed out before the walk starts: wave w of the launch owns chunk w from
 // its first flush on (only later chunks take an atomic on CTL_PAIR_TOP, which k_tok sets to the
 // end of the static ones).  0 when the staging buffer cannot hold one chunk per wave.
@@ -625,13 +674,12 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   const uint32_t blocks = walk_blocks(g, n, level);
   // a batch too small to give every wave TBLK topics is spread over all of them instead
   // (a 100k-topic batch would otherwise keep 3 in 4 waves idle)
-  const uint32_t waves = blocks * (WG / 64);
-  const uint32_t per_wave = waves ? (n + waves - 1) / waves : TBLK;
-  a.tblk = per_wave >= TBLK ? TBLK : ((per_wave + 7) & ~7u) < 8 ? 8 : ((per_wave + 7) & ~7u);
+  a.tblk = walk_tblk(blocks, n);
   // at most one topic per lane of the launched grid: lane gl walks topic gl, no claims (r03:
   // the failed claims of every wave on the exhausted counters dominated small batches)
   a.static_one = GM_STATIC_ONE && (uint64_t)n <= (uint64_t)blocks * WG ? 1u : 0u;
   a.stat_chunks = stat_chunks;
+  a.static_claim = GM_STATIC_CLAIM;
   a.census = census;
   a.leafp_mask = ix.leafp_mask;
   a.root_sig = ix.root_sig;
@@ -686,9 +734,11 @@ hipError_t launch_verify(const uint8_t* bytes, const uint32_t* off, const DevInd
   return hipGetLastError();
 }
 
-hipError_t launch_scatter(Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_t s) {
+hipError_t launch_scatter(Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_t s,
+                          bool mirror_ctl) {
   (void)n;
   ScatterArgs a;
+  a.ctl_host = mirror_ctl ? sc.ctl_host_dev : nullptr;
   a.stg = sc.stg;
   a.chk = sc.chk;
   a.pcap = sc.p_cap;
