@@ -1,17 +1,13 @@
 #!/bin/bash
-# r03: issue / wait mix of the production walk per config (SQ counters, two passes of 8 SQ
-# counters each), every pass its own bounded run.  usage: CFGS="1 2" tools/r03_sq.sh TAG
+# r03: instruction-issue counters of the walk (cfg1 100k, cfg3 64k, cfg3 4M) -- one PMC pass each
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/${1:-r03_sq}
+O=$R/gpurun_out/${1:-r03_sqi}
 mkdir -p $O
-for c in ${CFGS:-1 2 3}; do
-  i=0
-  for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE" \
-             "SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"; do
-    i=$((i+1))
-    timeout -s KILL 300 rocprofv3 --pmc $grp --kernel-include-regex "k_walk|k_scatter" -d $O/sq_cfg$c/p$i -o run --output-format csv -- python3 $R/bench.py --cfg $c --no-cpu-baseline --no-e2e --steps 3 --warmup 1 > $O/sq_cfg${c}_p$i.log 2>&1 || exit 1
-  done
-  python3 $R/tools/pmc_summary.py $O/sq_cfg$c > $O/sq_cfg${c}_summary.txt 2>&1 || exit 1
+G="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVES"
+for c in "1 100000" "3 65536" "3 4000000"; do
+  set -- $c
+  timeout -s KILL 400 rocprofv3 --pmc $G --kernel-include-regex "k_walk" -d $O/sq_$1_$2 -o run --output-format csv -- python3 $R/bench.py --cfg $1 --topics $2 --no-cpu-baseline --no-e2e --steps 3 --warmup 1 > $O/sq_$1_$2.log 2>&1 || exit 1
+  python3 $R/tools/pmc_summary.py $O/sq_$1_$2 > $O/sq_$1_$2_summary.txt 2>&1 || exit 1
 done
