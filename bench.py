@@ -67,6 +67,12 @@ def main():
     ap.add_argument("--windows", default="16384,65536,262144,1048576",
                     help="NIF batcher window sizes (topics) for the operating-point sweep "
                          "('' = skip); rank 0, N=1, with the host-in/host-out timing")
+    ap.add_argument("--nif", default="16:16384,16:65536,64:16384,64:65536",
+                    help="concurrent publish entry load (threads:window, '' = skip): publisher "
+                         "threads each calling emqxgm_async_match one topic at a time; rank 0, "
+                         "N=1")
+    ap.add_argument("--only-nif", action="store_true",
+                    help="build the index and run only the concurrent-entry load (no timed steps)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--inflight", type=int, default=0,
@@ -125,6 +131,12 @@ def main():
     log(f"[rank {rank}] index: {est['n_trie_filters']} trie filters, {est['n_route_keys']} route "
         f"keys, {est['n_nodes']} nodes, {est['device_bytes'] / 2**20:.0f} MiB in "
         f"{time.time() - t0:.1f}s")
+
+    if args.only_nif:
+        out = _nif_concurrent(eng, w, args.nif)
+        print(json.dumps({"config": f"cfg{args.cfg}: {w.nf} filters, {w.nt} topics",
+                          "nif_concurrent": out}), flush=True)
+        return
 
     if args.topic_order != "as-is":
         w = _reorder_topics(w, args.topic_order)
@@ -305,6 +317,10 @@ def main():
                                       "ms_per_batch": round(best * 1e3, 3),
                                       "api": "emqxgm_match_batch (u64 row pointers)"}}
 
+    nif = None
+    if rank == 0 and world == 1 and args.nif:
+        nif = _nif_concurrent(eng, w, args.nif)
+
     windows = None
     if rank == 0 and world == 1 and not args.no_e2e and args.windows:
         from emqx_amd.engine import Batcher
@@ -356,6 +372,7 @@ def main():
             "cpu_baseline": cpu,
             "end_to_end": e2e,
             "nif_windows": windows,
+            "nif_concurrent": nif,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -444,6 +461,38 @@ def _window_sweep(Batcher, eng, w, sizes):
                        "device) in pinned host memory (emqxgm_batcher_*), 3 windows in flight; "
                        "latency = flush -> collected; the caller's reading of the result (the "
                        "NIF's term building) is not included")
+    return out
+
+
+def _nif_concurrent(eng, w, spec):
+    """The NIF's concurrent entry under load: T publisher threads (BEAM
+    schedulers) each run P publisher processes calling emqxgm_async_match one topic at a time --
+    no caller-side batching -- and a call ends when the engine's completer thread reports it
+    (tests/host_harness/async_load.cpp over the engine: emqxgm_async_*).  P = enough calls for
+    the pipes' windows to fill by size (window x (EMQXGM_HOST_PIPES + 1) / T); topics/s and the
+    call -> result latency per call (p50 / p99).  Plus an idle-broker point: one call in flight
+    per thread, windows flushed by the window_us timer."""
+    from workloads import publishers
+    tb = np.ascontiguousarray(w.tbytes)
+    to = w.toff.astype(np.uint64)
+    out = {}
+    runs = [tuple(int(x) for x in item.split(":")) for item in spec.split(",") if item]
+    for T, W in runs:
+        procs = max(1, -(-W * (eng.HOST_PIPES + 1) // T))
+        calls = max(2 * procs, min(4_000_000, 25 * W) // T)
+        publishers.run([eng], tb, to, T, procs, min(calls, 4 * procs), W)  # warm-up
+        r = publishers.run([eng], tb, to, T, procs, calls, W)
+        out[f"T{T}_W{W}"] = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}
+        out[f"T{T}_W{W}"]["processes_per_thread"] = procs
+    if runs:
+        r = publishers.run([eng], tb, to, 16, 1, 2000, 65536)
+        out["idle_T16_P1"] = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}
+    out["includes"] = ("T threads x P processes, one emqxgm_async_match call per topic (the NIF's "
+                       "match_async/3), windows filled lock-free and flushed when full or "
+                       "window_us (50) after their first call, H2D, the device pass, every "
+                       "pair's filter bytes to pinned memory, the callback reporting each call; "
+                       "latency = call -> its report (the NIF's term building and enif_send "
+                       "excluded)")
     return out
 
 
@@ -635,15 +684,19 @@ def _roofline(nt, nbytes, census, pmc, tok_ms, exact_ms, walk_ms, pipe_ms, exact
             src = ("PMC TCP_TCC_READ_REQ per launch (" + str(p.get("source")) + ")" if req else
                    "census edge-bucket loads (no PMC request count committed for this batch: "
                    "L1 hits included, an over-count)")
-            # per topic its 64-B record + 4-B count, 3 x 16-B edge probes per matched
-            # trie state, a 16-B staged pair per match; the pruned walk never loads the states
-            # the depth codes rule out (shown apart)
-            alg = (64 + 4) * nt + 48 * census["states"] + 16 * census["pairs"]
+            # the bytes this design must move per launch: one 64-B bucket line per edge probe the
+            # production walk makes (census), the 64-B topic record and 4-B count per topic, a
+            # 12-B staged pair per match.  SURVEY 8d's model (3 x 16-B probes per matched trie
+            # state, 16-B pairs) is kept beside it, labelled: it counts states the upper levels
+            # serve from the L2 and the fat buckets never probe, so it can pass the HBM peak
+            alg = 64 * census["slot_loads"] + (64 + 4) * nt + 12 * census["pairs"]
+            model = (64 + 4) * nt + 48 * census["states"] + 16 * census["pairs"]
             pruned = 48 * (census["states"] - census.get("states_visited", census["states"]))
         else:
             lines = nt
             src = "one route-key bucket line per name"
             alg = nbytes + 8 * nt + 64 * nt + 4 * nt
+            model = alg
             pruned = 0
         ach = lines / sec
         # the ceiling of this access mix: a request that misses the L2 costs 1 / RANDOM_LINES_PEAK,
@@ -671,9 +724,19 @@ def _roofline(nt, nbytes, census, pmc, tok_ms, exact_ms, walk_ms, pipe_ms, exact
                             "measured dependent random 64-B gather rates (tools/gather_bench.hip, "
                             "profiles/r01/gather_sizes.txt): 53 G/s from beyond the L2, 104 G/s "
                             "from it, weighted by this kernel's L2 miss share (PMC)"),
-            "hbm_algorithmic": {"bytes_per_launch": int(alg), "pruned_state_bytes": int(pruned),
+            "hbm_algorithmic": {"bytes_per_launch": int(alg),
+                                "counts": ("64-B line per edge probe (census) + 68 B per topic "
+                                           "(record, count) + 12 B per staged pair"
+                                           if dom == "k_walk" else
+                                           "topic bytes + offsets + one 64-B bucket line + 4-B "
+                                           "exact id per name"),
                                 "achieved_GBs": round(alg / sec / 1e9, 1),
                                 "frac": round(alg / sec / 1e9 / HBM_PEAK_GBS, 4)},
+            "survey_8d_model": {"bytes_per_launch": int(model), "pruned_state_bytes": int(pruned),
+                                "frac": round(model / sec / 1e9 / HBM_PEAK_GBS, 4),
+                                "note": "SURVEY 8d's per-state model (48 B per matched trie "
+                                        "state), a model of the reference's probes, not of this "
+                                        "design's traffic: may exceed 1"},
         })
         if edge_loads is not None:
             out["edge_loads_per_launch"] = int(edge_loads)
@@ -767,24 +830,57 @@ def _cpu_leg(ref, w, threads, seconds):
     return n / dt, n, reps, dt
 
 
-def _cpu_baseline(w, args, job):
-    """The reference algorithm (C++ restatement of emqx_trie match_compact with an ordered-set
-    index, oracle/ref_trie.cpp) on this host's cores, over a bounded sample of the topics.
-    T = the CPUs this process may run on (os.sched_getaffinity, SURVEY 8d's nproc: one thread
-    per BEAM scheduler), and beside it the 16-CPU share the GPU box gives each GPU."""
+def _cgroup_cpus():
+    """CPUs the cgroup's quota lets this process use (cgroup v2 cpu.max "quota period", v1
+    cpu.cfs_quota_us / cpu.cfs_period_us), or None when unlimited / unknown."""
+    import math
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max":
+            return max(1, math.ceil(int(q) / int(p)))
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            p = int(f.read())
+        return max(1, math.ceil(q / p)) if q > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
+def effective_cpus():
+    """(effective CPUs, affinity CPUs, cgroup quota CPUs or None): SURVEY 8d's "nproc" = the CPUs
+    this process can actually use -- its affinity set, capped by the cgroup's CPU quota (r03's
+    line said 256 from the affinity alone on a lease quota-limited to ~16: 16 and 256 threads
+    gave the same rate)."""
     try:
         aff = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         aff = os.cpu_count() or 1
-    threads = args.cpu_threads or aff
-    share = min(16, aff)
+    quota = _cgroup_cpus()
+    return (min(aff, quota) if quota else aff), aff, quota
+
+
+def _cpu_baseline(w, args, job):
+    """The reference algorithm (C++ restatement of emqx_trie match_compact with an ordered-set
+    index, oracle/ref_trie.cpp) on this host's cores, over a bounded sample of the topics.
+    T = the CPUs this process can use (effective_cpus: affinity capped by the cgroup quota; one
+    thread per BEAM scheduler), and beside it the same leg at the affinity count when that is
+    larger (to show the quota binds)."""
+    eff, aff, quota = effective_cpus()
+    threads = args.cpu_threads or eff
     ref, build_s = job.wait()
     rate, n, reps, dt = _cpu_leg(ref, w, threads, args.cpu_seconds)
-    log(f"cpu baseline: index build {build_s:.1f}s, {n} topics in {dt:.2f}s on {threads} threads")
+    log(f"cpu baseline: index build {build_s:.1f}s, {n} topics in {dt:.2f}s on {threads} threads "
+        f"(affinity {aff}, quota {quota})")
     share_leg = None
-    if share != threads:
-        r2, n2, reps2, dt2 = _cpu_leg(ref, w, share, args.cpu_seconds / 2)
-        share_leg = {"value": round(r2, 1), "cores": share,
+    if aff > threads:
+        r2, n2, reps2, dt2 = _cpu_leg(ref, w, aff, args.cpu_seconds / 2)
+        share_leg = {"value": round(r2, 1), "threads": aff,
                      "sample": f"first {n2} topics" + (f" (x{reps2}, mean)" if reps2 > 1 else "")}
     model = "?"
     try:
@@ -794,7 +890,8 @@ def _cpu_baseline(w, args, job):
         pass
     return {"value": round(rate, 1), "unit": "topics/s", "cores": threads, "kind": "port",
             "cpu_model": model, "host_cpus": os.cpu_count(), "affinity_cpus": aff,
-            "gpu_share_16": share_leg,
+            "cgroup_quota_cpus": quota, "effective_cpus": eff,
+            "at_affinity_threads": share_leg,
             "index_build_s": round(build_s, 1),
             "sample": f"first {n} topics of batch 0" + (f" (x{reps}, mean)" if reps > 1 else "")
                   + f" against the same {w.nf} filters "

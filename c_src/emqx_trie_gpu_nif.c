@@ -2,43 +2,56 @@
  * emqx_trie_gpu_nif.c -- the Erlang NIF over libemqx_gpumatch.so (include/emqx_gpumatch.h).
  *
  * Loaded by src/emqx_trie_gpu_nif.erl.  It replaces the publish-time match path of EMQX
- * 5.0.14: emqx_trie:match/1 (apps/emqx/src/emqx_trie.erl:147-169) as called by
- * emqx_router:match_routes/1 (apps/emqx/src/emqx_router.erl:141-157) from
- * emqx_broker:publish/1 (apps/emqx/src/emqx_broker.erl:218-232).  Topics of concurrent
- * publishers go through one batcher process (src/emqx_trie_gpu_batcher.erl), which calls
- * add/3 per topic, flush/1 per window and collect/2 per completed window here; the writes of
- * committed route changes (src/emqx_trie_gpu_sync.erl) call trie_insert/trie_delete/route_ref/
- * route_unref/commit.
+ * 5.0.14: emqx_trie:match/1 and match_session/1 (apps/emqx/src/emqx_trie.erl:147-169) as called
+ * by emqx_router:match_routes/1 (apps/emqx/src/emqx_router.erl:141-157) and
+ * emqx_session_router:match_routes/1 (emqx_session_router.erl:145-159) from
+ * emqx_broker:publish/1 (apps/emqx/src/emqx_broker.erl:218-232).
  *
- * Compiled only where erl_nif.h exists (c_src/Makefile); this image has no Erlang runtime,
- * so the C-ABI below it is tested through ctypes (tests/test_gpu_batcher.py drives the same
- * emqxgm_batcher_* sequence this file does).
+ * One resource = one index (the route table's trie + route keys, or the session router's) held
+ * by one engine per GPU of broker.perf.gpu_match.devices (every engine the whole index: the
+ * replica layout of DESIGN.md 5) plus the concurrent publish entry over them
+ * (emqxgm_async_*).  Publisher processes call match_async/3 themselves, concurrently, on their
+ * own schedulers; the engine's completer threads send each caller
+ *     {emqx_trie_gpu, Id, [Filter]}  or  {emqx_trie_gpu, Id, {error, Reason}}
+ * (src/emqx_trie_gpu.erl waits for it, and falls back to the reference's own emqx_trie:match/1
+ * on an error or a timeout).  The mirror of the committed route table
+ * (src/emqx_trie_gpu_sync.erl) calls route_set/3, sync_begin/1, sync_end/2 and commit/1.
+ *
+ * Compiled only where erl_nif.h exists (c_src/Makefile); this image has no Erlang runtime, so
+ * the C-ABI below it is tested through ctypes and the C harness of tests/host_harness
+ * (tests/test_gpu_async.py drives emqxgm_async_* from 16 and 64 threads as publishers do).
  */
 #include <erl_nif.h>
 #include <errno.h>
 #include <string.h>
-#include <time.h>
 
 #include "emqx_gpumatch.h"
 
+#define GM_MAX_DEVICES 16
+
 typedef struct {
-  emqxgm_t* h;
-  emqxgm_batcher_t* b;
+  unsigned nh;
+  emqxgm_t* h[GM_MAX_DEVICES];
+  emqxgm_async_t* a;
 } gm_res;
 
 static ErlNifResourceType* RT;
-static ERL_NIF_TERM A_OK, A_ERROR, A_FULL, A_EMPTY, A_TRUE, A_FALSE;
+static ERL_NIF_TERM A_OK, A_ERROR, A_TRUE, A_FALSE, A_MOD;
+
+/* An ErlNifPid is one term word: it travels through the engine as the call's owner. */
+typedef char gm_pid_fits_owner[sizeof(ErlNifPid) <= sizeof(uint64_t) ? 1 : -1];
 
 static void gm_res_dtor(ErlNifEnv* env, void* obj) {
   gm_res* r = (gm_res*)obj;
   (void)env;
-  if (r->b) emqxgm_batcher_destroy(r->b); /* completes windows still in flight */
-  if (r->h) emqxgm_destroy(r->h);
-  r->b = NULL;
-  r->h = NULL;
+  if (r->a) emqxgm_async_destroy(r->a); /* reports every accepted call first */
+  for (unsigned k = 0; k < r->nh; ++k)
+    if (r->h[k]) emqxgm_destroy(r->h[k]);
+  r->a = NULL;
+  r->nh = 0;
 }
 
-static ERL_NIF_TERM err_term(ErlNifEnv* env, int rc) {
+static ERL_NIF_TERM errno_atom(ErlNifEnv* env, int rc) {
   const char* a;
   switch (-rc) {
     case EINVAL: a = "einval"; break;
@@ -47,41 +60,86 @@ static ERL_NIF_TERM err_term(ErlNifEnv* env, int rc) {
     case ENOSPC: a = "enospc"; break;
     case EBUSY: a = "ebusy"; break;
     case ENOENT: a = "enoent"; break;
-    case ENODEV: a = "enodev"; break;
+    case ESTALE: a = "estale"; break;
+    case ESHUTDOWN: a = "eshutdown"; break;
     default: a = "eio"; break;
   }
-  return enif_make_tuple2(env, A_ERROR, enif_make_atom(env, a));
+  return enif_make_atom(env, a);
+}
+
+static ERL_NIF_TERM err_term(ErlNifEnv* env, int rc) {
+  return enif_make_tuple2(env, A_ERROR, errno_atom(env, rc));
 }
 
 static int get_res(ErlNifEnv* env, ERL_NIF_TERM t, gm_res** r) {
-  return enif_get_resource(env, t, RT, (void**)r) && (*r)->h;
+  return enif_get_resource(env, t, RT, (void**)r) && (*r)->nh > 0;
 }
 
-/* open(Device, WindowTopics, WindowBytes, WindowUs) -> {ok, Handle} | {error, Reason}
- * broker.perf.gpu_match.{devices, batch_max, batch_window_us} (src/emqx_trie_gpu_schema.erl) */
+/* The completer thread of one engine handle: every caller of a completed window gets its
+ * message.  One process-independent environment per window (enif_send clears it each time). */
+static void on_window(void* user, const emqxgm_async_window* w) {
+  (void)user;
+  ErlNifEnv* env = enif_alloc_env();
+  if (!env) return;
+  for (uint32_t i = 0; i < w->n; ++i) {
+    if (w->tag[i] == EMQXGM_TAG_CANCELLED) continue; /* the caller timed out and cancelled */
+    ErlNifPid pid;
+    memcpy(&pid, &w->owner[i], sizeof pid);
+    ERL_NIF_TERM res;
+    if (w->status) {
+      res = err_term(env, w->status);
+    } else {
+      res = enif_make_list(env, 0);
+      for (uint32_t j = w->row[i + 1]; j-- > w->row[i];) {
+        const size_t len = (size_t)(w->foff[j + 1] - w->foff[j]);
+        ERL_NIF_TERM b;
+        unsigned char* p = enif_make_new_binary(env, len, &b);
+        if (len) memcpy(p, w->fbytes + w->foff[j], len);
+        res = enif_make_list_cell(env, b, res);
+      }
+    }
+    ERL_NIF_TERM msg = enif_make_tuple3(env, A_MOD, enif_make_uint64(env, w->tag[i]), res);
+    enif_send(NULL, &pid, env, msg);
+  }
+  enif_free_env(env);
+}
+
+/* open(Devices, WindowTopics, WindowBytes, WindowUs, MaxLevels) -> {ok, Res} | {error, Reason}
+ * broker.perf.gpu_match.{devices, batch_max, batch_window_us, max_levels}
+ * (src/emqx_trie_gpu_schema.erl): one engine per device, windows of WindowTopics topics */
 static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
-  int dev;
-  unsigned wt, wb, wus;
+  unsigned ndev, wt, wb, wus, ml;
+  ERL_NIF_TERM list = argv[0], head;
   (void)argc;
-  if (!enif_get_int(env, argv[0], &dev) || !enif_get_uint(env, argv[1], &wt) ||
-      !enif_get_uint(env, argv[2], &wb) || !enif_get_uint(env, argv[3], &wus))
+  if (!enif_get_list_length(env, list, &ndev) || ndev == 0 || ndev > GM_MAX_DEVICES ||
+      !enif_get_uint(env, argv[1], &wt) || !enif_get_uint(env, argv[2], &wb) ||
+      !enif_get_uint(env, argv[3], &wus) || !enif_get_uint(env, argv[4], &ml))
     return enif_make_badarg(env);
-  emqxgm_cfg cfg;
-  memset(&cfg, 0, sizeof cfg);
-  cfg.device = dev;
-  cfg.full_hash_bits = 64;
-  cfg.batch_max = wt; /* one window is one engine batch */
   gm_res* r = enif_alloc_resource(RT, sizeof(gm_res));
-  r->h = NULL;
-  r->b = NULL;
-  int rc = emqxgm_create(&cfg, &r->h);
-  if (rc == 0) {
-    emqxgm_batcher_cfg bc;
-    memset(&bc, 0, sizeof bc);
-    bc.window_topics = wt;
-    bc.window_bytes = wb;
-    bc.window_us = wus;
-    rc = emqxgm_batcher_create(r->h, &bc, &r->b);
+  memset(r, 0, sizeof *r);
+  int rc = 0;
+  for (unsigned k = 0; k < ndev && !rc; ++k) {
+    int dev;
+    if (!enif_get_list_cell(env, list, &head, &list) || !enif_get_int(env, head, &dev)) {
+      enif_release_resource(r);
+      return enif_make_badarg(env);
+    }
+    emqxgm_cfg cfg;
+    memset(&cfg, 0, sizeof cfg);
+    cfg.device = dev;
+    cfg.full_hash_bits = 64;
+    cfg.batch_max = wt; /* one window is one engine batch */
+    rc = emqxgm_create(&cfg, &r->h[k]);
+    if (!rc) r->nh = k + 1;
+  }
+  if (!rc) {
+    emqxgm_async_cfg ac;
+    memset(&ac, 0, sizeof ac);
+    ac.window_topics = wt;
+    ac.window_bytes = wb;
+    ac.window_us = wus;
+    ac.max_levels = ml;
+    rc = emqxgm_async_create(r->h, r->nh, &ac, on_window, NULL, &r->a);
   }
   if (rc) {
     enif_release_resource(r); /* the destructor frees what was made */
@@ -92,125 +150,142 @@ static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
   return enif_make_tuple2(env, A_OK, t);
 }
 
-typedef int (*filter_op)(emqxgm_t*, const uint8_t*, uint32_t);
-
-static int op_insert(emqxgm_t* h, const uint8_t* p, uint32_t n) { return emqxgm_trie_insert(h, p, n, NULL); }
-static int op_route_ref(emqxgm_t* h, const uint8_t* p, uint32_t n) { return emqxgm_route_ref(h, p, n, NULL); }
-
-static ERL_NIF_TERM do_filter_op(ErlNifEnv* env, const ERL_NIF_TERM argv[], filter_op op) {
+/* route_set(Res, Filter, Present) -> ok | {error, Reason}: the route-key / trie membership of
+ * Filter in every engine (emqxgm_route_set: a state, not a count; emqx_router_utils.erl:34-71).
+ * Visible after commit/1. */
+static ERL_NIF_TERM nif_route_set(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   gm_res* r;
   ErlNifBinary bin;
-  if (!get_res(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &bin) || bin.size > 65535)
+  (void)argc;
+  if (!get_res(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &bin) || bin.size > 65535 ||
+      (argv[2] != A_TRUE && argv[2] != A_FALSE))
     return enif_make_badarg(env);
-  const int rc = op(r->h, bin.data, (uint32_t)bin.size);
-  return rc ? err_term(env, rc) : A_OK;
+  for (unsigned k = 0; k < r->nh; ++k) {
+    const int rc = emqxgm_route_set(r->h[k], bin.data, (uint32_t)bin.size, argv[2] == A_TRUE);
+    if (rc) return err_term(env, rc);
+  }
+  return A_OK;
 }
 
-/* emqx_trie:insert/1 / delete/1 (emqx_trie.erl:113-144) of a committed change; route-bag key
- * refcounts (emqx_router_utils.erl:31-71).  Visible after commit/1. */
-static ERL_NIF_TERM nif_trie_insert(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+/* sync_begin(Res) -> {ok, Gen}: a full resync starts (emqxgm_route_sync_begin on every engine;
+ * their generations advance together) */
+static ERL_NIF_TERM nif_sync_begin(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_res* r;
+  uint32_t gen = 0;
   (void)argc;
-  return do_filter_op(env, argv, op_insert);
-}
-static ERL_NIF_TERM nif_trie_delete(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
-  (void)argc;
-  return do_filter_op(env, argv, emqxgm_trie_delete);
-}
-static ERL_NIF_TERM nif_route_ref(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
-  (void)argc;
-  return do_filter_op(env, argv, op_route_ref);
-}
-static ERL_NIF_TERM nif_route_unref(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
-  (void)argc;
-  return do_filter_op(env, argv, emqxgm_route_unref);
+  if (!get_res(env, argv[0], &r)) return enif_make_badarg(env);
+  for (unsigned k = 0; k < r->nh; ++k) {
+    uint32_t g;
+    const int rc = emqxgm_route_sync_begin(r->h[k], &g);
+    if (rc) return err_term(env, rc);
+    if (k == 0) gen = g;
+    else if (g != gen) return err_term(env, -ESTALE);
+  }
+  return enif_make_tuple2(env, A_OK, enif_make_uint(env, gen));
 }
 
-/* commit(H) -> {ok, Epoch}: the atomic epoch swap (a delta patch or a full build; dirty CPU) */
+/* sync_end(Res, Gen) -> {ok, Removed}: every route key not set present since sync_begin goes
+ * (dirty CPU: one pass over the registry) */
+static ERL_NIF_TERM nif_sync_end(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_res* r;
+  unsigned gen;
+  uint64_t removed = 0;
+  (void)argc;
+  if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &gen)) return enif_make_badarg(env);
+  for (unsigned k = 0; k < r->nh; ++k) {
+    uint64_t n = 0;
+    const int rc = emqxgm_route_sync_end(r->h[k], gen, &n);
+    if (rc) return err_term(env, rc);
+    if (k == 0) removed = n;
+  }
+  return enif_make_tuple2(env, A_OK, enif_make_uint64(env, removed));
+}
+
+/* commit(Res) -> {ok, Epoch}: the atomic epoch swap on every engine (a delta patch or a full
+ * build; dirty CPU) */
 static ERL_NIF_TERM nif_commit(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   gm_res* r;
   uint64_t epoch = 0;
   (void)argc;
   if (!get_res(env, argv[0], &r)) return enif_make_badarg(env);
-  const int rc = emqxgm_commit(r->h, &epoch);
-  return rc ? err_term(env, rc) : enif_make_tuple2(env, A_OK, enif_make_uint64(env, epoch));
+  for (unsigned k = 0; k < r->nh; ++k) {
+    uint64_t e = 0;
+    const int rc = emqxgm_commit(r->h[k], &e);
+    if (rc) return err_term(env, rc);
+    if (k == 0) epoch = e;
+  }
+  return enif_make_tuple2(env, A_OK, enif_make_uint64(env, epoch));
 }
 
-/* empty(H) -> boolean(): emqx_trie:empty/0 (emqx_trie.erl:172-178) of the committed index */
+/* empty(Res) -> boolean(): emqx_trie:empty/0 (emqx_trie.erl:172-178) of the committed index
+ * (an atomic read: never waits for a commit) */
 static ERL_NIF_TERM nif_empty(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   gm_res* r;
   (void)argc;
   if (!get_res(env, argv[0], &r)) return enif_make_badarg(env);
-  const int rc = emqxgm_trie_empty(r->h);
+  const int rc = emqxgm_trie_empty(r->h[0]);
   return rc < 0 ? err_term(env, rc) : (rc ? A_TRUE : A_FALSE);
 }
 
-/* add(H, Topic, Tag) -> ok | full | {error, enospc | e2big}: the topic joins the open window;
- * full = flush it before the next add */
-static ERL_NIF_TERM nif_add(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+typedef int (*member_fn)(emqxgm_t*, const uint8_t*, uint32_t);
+
+static ERL_NIF_TERM do_member(ErlNifEnv* env, const ERL_NIF_TERM argv[], member_fn f) {
   gm_res* r;
   ErlNifBinary bin;
-  ErlNifUInt64 tag;
-  uint32_t slot;
+  if (!get_res(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &bin) || bin.size > 65535)
+    return enif_make_badarg(env);
+  const int rc = f(r->h[0], bin.data, (uint32_t)bin.size);
+  return rc < 0 ? err_term(env, rc) : (rc ? A_TRUE : A_FALSE);
+}
+
+/* trie_member(Res, Filter) -> boolean(): emqx_trie:lookup_topic/2 (emqx_trie.erl:267-271) */
+static ERL_NIF_TERM nif_trie_member(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  return do_member(env, argv, emqxgm_trie_member);
+}
+
+/* route_member(Res, Filter) -> boolean(): whether Filter is a committed route key */
+static ERL_NIF_TERM nif_route_member(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  return do_member(env, argv, emqxgm_route_member);
+}
+
+/* match_async(Res, Topic, Id) -> ok | {error, e2big | ebusy | eshutdown}: Topic joins the open
+ * window; the caller (self()) later receives {emqx_trie_gpu, Id, Result}.  Id: a unique
+ * non-negative integer (erlang:unique_integer([positive])).  Runs on the caller's own scheduler
+ * (a copy into pinned memory under a short lock). */
+static ERL_NIF_TERM nif_match_async(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_res* r;
+  ErlNifBinary bin;
+  ErlNifUInt64 id;
+  ErlNifPid self;
+  uint64_t owner = 0;
   (void)argc;
   if (!get_res(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &bin) ||
-      !enif_get_uint64(env, argv[2], &tag) || bin.size > 65535)
+      !enif_get_uint64(env, argv[2], &id) || id == EMQXGM_TAG_CANCELLED || bin.size > 65535 ||
+      !enif_self(env, &self))
     return enif_make_badarg(env);
-  const int rc = emqxgm_batcher_add(r->b, bin.data, (uint32_t)bin.size, tag, &slot);
-  return rc < 0 ? err_term(env, rc) : (rc ? A_FULL : A_OK);
+  memcpy(&owner, &self, sizeof self);
+  const int rc = emqxgm_async_match(r->a, bin.data, (uint32_t)bin.size, id, owner);
+  return rc ? err_term(env, rc) : A_OK;
 }
 
-/* due(H) -> boolean(): the open window's first topic is batch_window_us old */
-static ERL_NIF_TERM nif_due(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+/* cancel(Res, Id) -> true | false: true = the call will never be answered; false = its answer
+ * is already in the caller's mailbox.  Dirty IO: may wait while the call's window is reported. */
+static ERL_NIF_TERM nif_cancel(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   gm_res* r;
-  struct timespec ts;
+  ErlNifUInt64 id;
+  ErlNifPid self;
+  uint64_t owner = 0;
   (void)argc;
-  if (!get_res(env, argv[0], &r)) return enif_make_badarg(env);
-  clock_gettime(CLOCK_MONOTONIC, &ts);
-  const uint64_t now = (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
-  return emqxgm_batcher_due(r->b, now) == 1 ? A_TRUE : A_FALSE;
-}
-
-/* flush(H) -> {ok, WindowId} | empty | {error, ebusy} */
-static ERL_NIF_TERM nif_flush(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
-  gm_res* r;
-  uint64_t w = 0;
-  (void)argc;
-  if (!get_res(env, argv[0], &r)) return enif_make_badarg(env);
-  const int rc = emqxgm_batcher_flush(r->b, &w);
-  if (rc) return err_term(env, rc);
-  return w ? enif_make_tuple2(env, A_OK, enif_make_uint64(env, w)) : A_EMPTY;
-}
-
-/* collect(H, WindowId) -> {ok, [{Tag, [Filter], ExactHit}]} in add order (dirty IO: waits for
- * the window's pass).  [Filter] is emqx_trie:match(Topic) -- a set, [] for a wildcard name;
- * ExactHit = whether the topic itself is a route key (emqx_router.erl:143-144). */
-static ERL_NIF_TERM nif_collect(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
-  gm_res* r;
-  ErlNifUInt64 wid;
-  emqxgm_window_out o;
-  (void)argc;
-  if (!get_res(env, argv[0], &r) || !enif_get_uint64(env, argv[1], &wid))
+  if (!get_res(env, argv[0], &r) || !enif_get_uint64(env, argv[1], &id) || !enif_self(env, &self))
     return enif_make_badarg(env);
-  const int rc = emqxgm_batcher_collect(r->b, wid, &o);
-  if (rc) return err_term(env, rc);
-  ERL_NIF_TERM list = enif_make_list(env, 0);
-  for (uint32_t i = o.n; i-- > 0;) {
-    ERL_NIF_TERM row = enif_make_list(env, 0);
-    for (uint32_t j = o.row[i + 1]; j-- > o.row[i];) {
-      const size_t len = (size_t)(o.foff[j + 1] - o.foff[j]);
-      ERL_NIF_TERM b;
-      unsigned char* p = enif_make_new_binary(env, len, &b);
-      if (len) memcpy(p, o.fbytes + o.foff[j], len);
-      row = enif_make_list_cell(env, b, row);
-    }
-    ERL_NIF_TERM ent = enif_make_tuple3(env, enif_make_uint64(env, o.tag[i]), row,
-                                        o.exact_id[i] == EMQXGM_NONE ? A_FALSE : A_TRUE);
-    list = enif_make_list_cell(env, ent, list);
-  }
-  return enif_make_tuple2(env, A_OK, list);
+  memcpy(&owner, &self, sizeof self);
+  const int rc = emqxgm_async_cancel(r->a, id, owner);
+  return rc < 0 ? err_term(env, rc) : (rc ? A_TRUE : A_FALSE);
 }
 
-/* tune(H, Key, Value) -> ok | {error, einval}: emqxgm_tune knobs */
+/* tune(Res, Key, Value) -> ok | {error, einval}: emqxgm_tune knobs on every engine */
 static ERL_NIF_TERM nif_tune(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   gm_res* r;
   char key[64];
@@ -219,8 +294,27 @@ static ERL_NIF_TERM nif_tune(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
   if (!get_res(env, argv[0], &r) || enif_get_atom(env, argv[1], key, sizeof key, ERL_NIF_LATIN1) <= 0 ||
       !enif_get_int64(env, argv[2], &v))
     return enif_make_badarg(env);
-  const int rc = emqxgm_tune(r->h, key, v);
-  return rc ? err_term(env, rc) : A_OK;
+  for (unsigned k = 0; k < r->nh; ++k) {
+    const int rc = emqxgm_tune(r->h[k], key, v);
+    if (rc) return err_term(env, rc);
+  }
+  return A_OK;
+}
+
+/* stats(Res) -> #{calls, windows, reported, busy, cancelled, too_deep, failed, outstanding} */
+static ERL_NIF_TERM nif_stats(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  static const char* keys[8] = {"calls", "windows", "reported", "busy",
+                                "cancelled", "too_deep", "failed", "outstanding"};
+  gm_res* r;
+  uint64_t v[8];
+  (void)argc;
+  if (!get_res(env, argv[0], &r)) return enif_make_badarg(env);
+  const int rc = emqxgm_async_stats(r->a, v);
+  if (rc) return err_term(env, rc);
+  ERL_NIF_TERM m = enif_make_new_map(env);
+  for (int i = 0; i < 8; ++i)
+    enif_make_map_put(env, m, enif_make_atom(env, keys[i]), enif_make_uint64(env, v[i]), &m);
+  return m;
 }
 
 static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
@@ -230,26 +324,25 @@ static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   if (!RT || emqxgm_abi_version() != EMQXGM_ABI_VERSION) return -1;
   A_OK = enif_make_atom(env, "ok");
   A_ERROR = enif_make_atom(env, "error");
-  A_FULL = enif_make_atom(env, "full");
-  A_EMPTY = enif_make_atom(env, "empty");
   A_TRUE = enif_make_atom(env, "true");
   A_FALSE = enif_make_atom(env, "false");
+  A_MOD = enif_make_atom(env, "emqx_trie_gpu");
   return 0;
 }
 
 static ErlNifFunc funcs[] = {
-    {"open", 4, nif_open, ERL_NIF_DIRTY_JOB_IO_BOUND},
-    {"trie_insert", 2, nif_trie_insert, 0},
-    {"trie_delete", 2, nif_trie_delete, 0},
-    {"route_ref", 2, nif_route_ref, 0},
-    {"route_unref", 2, nif_route_unref, 0},
+    {"open", 5, nif_open, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"route_set", 3, nif_route_set, 0},
+    {"sync_begin", 1, nif_sync_begin, 0},
+    {"sync_end", 2, nif_sync_end, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"commit", 1, nif_commit, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"empty", 1, nif_empty, 0},
-    {"add", 3, nif_add, 0},
-    {"due", 1, nif_due, 0},
-    {"flush", 1, nif_flush, 0},
-    {"collect", 2, nif_collect, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"trie_member", 2, nif_trie_member, 0},
+    {"route_member", 2, nif_route_member, 0},
+    {"match_async", 3, nif_match_async, 0},
+    {"cancel", 2, nif_cancel, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"tune", 3, nif_tune, 0},
+    {"stats", 1, nif_stats, 0},
 };
 
 ERL_NIF_INIT(emqx_trie_gpu_nif, funcs, load, NULL, NULL, NULL)

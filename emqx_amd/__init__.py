@@ -7,11 +7,12 @@ The product is ``libemqx_gpumatch.so`` (gfx950 HIP kernels + host index builder 
     from emqx_amd import Trie, Router, Broker, Engine
 """
 from .broker import Broker  # noqa: F401
-from .engine import NONE, Batcher, DeviceResult, Engine, EngineError, MatchResult, PublishResult, Window  # noqa: F401
+from .engine import NONE, AsyncMatcher, AsyncResult, Batcher, DeviceResult, Engine, EngineError, MatchResult, PublishResult, Window  # noqa: F401
 from .router import Router, SessionRouter  # noqa: F401
 from .retainer import Retainer  # noqa: F401
 from .rules import TopicRules  # noqa: F401
 from .trie import Trie  # noqa: F401
 
 __all__ = ["Engine", "EngineError", "MatchResult", "DeviceResult", "PublishResult", "Trie",
-           "Router", "SessionRouter", "Broker", "TopicRules", "Retainer", "Batcher", "Window", "NONE"]
+           "Router", "SessionRouter", "Broker", "TopicRules", "Retainer", "Batcher", "Window",
+           "AsyncMatcher", "AsyncResult", "NONE"]

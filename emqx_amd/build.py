@@ -5,6 +5,9 @@
 * ``oracle/build/libemqx_ref.so`` -- the C++ restatement of the reference (test checker and
   CPU baseline only; g++).
 * ``workloads/libemqx_workload.so`` -- deterministic synthetic workload generator (g++).
+* ``tests/host_harness/lib/libasync_load.so`` -- publisher threads driving the engine's concurrent
+  entry (tests/host_harness/async_load.cpp; test and bench infrastructure, linked against the
+  engine).
 
 Outputs are git-ignored and travel to the GPU box with the tree.
 """
@@ -20,8 +23,9 @@ CSRC = os.path.join(ROOT, "emqx_amd", "csrc")
 ENGINE_SO = os.path.join(ROOT, "emqx_amd", "libemqx_gpumatch.so")
 ORACLE_SO = os.path.join(ROOT, "oracle", "build", "libemqx_ref.so")
 WORKLOAD_SO = os.path.join(ROOT, "workloads", "libemqx_workload.so")
+LOAD_SO = os.path.join(ROOT, "tests", "host_harness", "lib", "libasync_load.so")
 
-ENGINE_SRCS = ["gm_kernels.hip", "gm_engine.cpp", "gm_retain.cpp", "gm_batcher.cpp"]
+ENGINE_SRCS = ["gm_kernels.hip", "gm_engine.cpp", "gm_retain.cpp", "gm_batcher.cpp", "gm_async.cpp"]
 ENGINE_DEPS = sorted(set(ENGINE_SRCS) | {f for f in os.listdir(CSRC) if f.endswith((".h", ".inc"))})
 
 
@@ -52,7 +56,7 @@ def build_engine(force: bool = False) -> str:
         os.path.join(ROOT, "include", "emqx_gpumatch.h")]
     if force or _stale(ENGINE_SO, deps):
         _run([_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-Wall", "-Wno-unused-function", "-Wno-unused-result"]
+              "-Wall", "-Wno-unused-function", "-Wno-unused-result", "-pthread"]
              + [os.path.join(CSRC, s) for s in ENGINE_SRCS] + ["-o", ENGINE_SO])
     return ENGINE_SO
 
@@ -73,8 +77,20 @@ def build_workloads(force: bool = False) -> str:
     return WORKLOAD_SO
 
 
+def build_load_harness(force: bool = False) -> str:
+    src = os.path.join(ROOT, "tests", "host_harness", "async_load.cpp")
+    deps = [src, ENGINE_SO, os.path.join(ROOT, "include", "emqx_gpumatch.h")]
+    if force or _stale(LOAD_SO, deps):
+        os.makedirs(os.path.dirname(LOAD_SO), exist_ok=True)
+        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wall", src,
+              "-L", os.path.dirname(ENGINE_SO), "-l:libemqx_gpumatch.so",
+              "-Wl,-rpath,$ORIGIN/../../../emqx_amd", "-o", LOAD_SO])
+    return LOAD_SO
+
+
 def build_all(force: bool = False):
-    return build_engine(force), build_oracle(force), build_workloads(force)
+    return (build_engine(force), build_oracle(force), build_workloads(force),
+            build_load_harness(force))
 
 
 if __name__ == "__main__":

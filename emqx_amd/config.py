@@ -3,18 +3,25 @@ reference's ``broker.perf.route_lock_type`` / ``trie_compaction`` (apps/emqx/src
 1259-1273; SURVEY 5 "Config / flags"), and how each field reaches the engine.  The same table as
 ``src/emqx_trie_gpu_schema.erl`` (the HOCON fields a maintainer adds to ``fields("broker_perf")``):
 
-============== ======================= ==========================================================
-field          default                 engine
-============== ======================= ==========================================================
-enable         false                   the device answers ``emqx_trie:match/1`` at all
-devices        [0]                     ``emqxgm_cfg.device`` (the first; one index per node)
-batch_max      65536                   ``emqxgm_cfg.batch_max`` = ``emqxgm_batcher_cfg.window_topics``
-                                       (``window_bytes`` = 64 x batch_max)
-batch_window_us 50                     ``emqxgm_batcher_cfg.window_us``
-max_levels     128                     deeper topics take the reference's ``emqx_trie:match/1``
-                                       (``mqtt.max_topic_levels``, emqx_schema.erl:405-412)
-delta_commit   small                   ``emqxgm_tune("delta_commit", never 0 / small 1 / always 2)``
-============== ======================= ==========================================================
+================== ================== ======================================================
+field              default            engine
+================== ================== ======================================================
+enable             false              the device answers ``emqx_trie:match/1`` at all
+devices            [0]                one engine per device (``emqxgm_cfg.device``), each with
+                                      the whole index; windows round robin over them
+                                      (``emqxgm_async_create``)
+batch_max          65536              ``emqxgm_cfg.batch_max`` = ``emqxgm_async_cfg.window_topics``
+                                      (``window_bytes`` = 64 x batch_max)
+batch_window_us    50                 ``emqxgm_async_cfg.window_us``
+max_levels         128                ``emqxgm_async_cfg.max_levels``: deeper topics take the
+                                      reference's ``emqx_trie:match/1`` (``mqtt.max_topic_levels``,
+                                      emqx_schema.erl:405-412)
+delta_commit       small              ``emqxgm_tune("delta_commit", never 0 / small 1 / always 2)``
+timeout_ms         5000               a publisher's wait before it cancels and takes the
+                                      reference's match (src/emqx_trie_gpu.erl)
+resync_interval_ms 30000              period of the mirror's full resync
+                                      (``emqxgm_route_sync_begin`` / ``_end``)
+================== ================== ======================================================
 """
 from __future__ import annotations
 
@@ -32,6 +39,8 @@ class GpuMatchConfig:
     batch_window_us: int = 50
     max_levels: int = 128
     delta_commit: str = "small"
+    timeout_ms: int = 5000
+    resync_interval_ms: int = 30000
 
     @classmethod
     def from_map(cls, conf: Mapping) -> "GpuMatchConfig":
@@ -58,15 +67,23 @@ class GpuMatchConfig:
         rng("batch_max", self.batch_max, 1, 4 << 20)
         rng("batch_window_us", self.batch_window_us, 1, 1_000_000)
         rng("max_levels", self.max_levels, 1, 65535)
+        rng("timeout_ms", self.timeout_ms, 1, 600_000)
+        rng("resync_interval_ms", self.resync_interval_ms, 100, 86_400_000)
         if self.delta_commit not in DELTA_COMMIT:
             raise ValueError(f"broker.perf.gpu_match.delta_commit: one of {sorted(DELTA_COMMIT)}")
 
-    def engine_kwargs(self) -> Dict[str, int]:
-        """``emqxgm_cfg`` fields (emqx_amd.Engine keywords)."""
-        return {"device": self.devices[0], "batch_max": self.batch_max}
+    def engine_kwargs(self) -> List[Dict[str, int]]:
+        """``emqxgm_cfg`` fields (emqx_amd.Engine keywords), one engine per device."""
+        return [{"device": d, "batch_max": self.batch_max} for d in self.devices]
+
+    def async_kwargs(self) -> Dict[str, int]:
+        """``emqxgm_async_cfg`` fields (emqx_amd.AsyncMatcher keywords)."""
+        return {"window_topics": self.batch_max, "window_bytes": 64 * self.batch_max,
+                "window_us": self.batch_window_us, "max_levels": self.max_levels}
 
     def batcher_kwargs(self) -> Dict[str, int]:
-        """``emqxgm_batcher_cfg`` fields (emqx_amd.Batcher keywords)."""
+        """``emqxgm_batcher_cfg`` fields (emqx_amd.Batcher keywords: the single-driver batcher
+        core the bench's window sweep uses)."""
         return {"window_topics": self.batch_max, "window_bytes": 64 * self.batch_max,
                 "window_us": self.batch_window_us}
 
@@ -74,10 +91,13 @@ class GpuMatchConfig:
         """``emqxgm_tune`` knobs."""
         return {"delta_commit": DELTA_COMMIT[self.delta_commit]}
 
-    def open(self):
-        """An Engine and its Batcher as the NIF's open/4 makes them (emqx_trie_gpu:start_link)."""
-        from .engine import Batcher, Engine
-        eng = Engine(**self.engine_kwargs())
-        for k, v in self.tunes().items():
-            eng.tune(k, v)
-        return eng, Batcher(eng, **self.batcher_kwargs())
+    def open(self, callback):
+        """The engines and their concurrent entry as the NIF's open/5 makes them
+        (emqx_trie_gpu_sync:init/1): one Engine per device, tuned, and an AsyncMatcher over them
+        reporting completed windows to `callback`."""
+        from .engine import AsyncMatcher, Engine
+        engines = [Engine(**kw) for kw in self.engine_kwargs()]
+        for eng in engines:
+            for k, v in self.tunes().items():
+                eng.tune(k, v)
+        return engines, AsyncMatcher(engines, callback, **self.async_kwargs())

@@ -39,7 +39,7 @@ struct Window {
   uint32_t n = 0;
   uint64_t first_ns = 0;
   uint64_t id = 0, ticket = 0;
-  int state = 0;  // 0 open / free, 1 in flight, 2 collected
+  int state = 0;  // 0 open / free, 1 in flight, 2 collected, 3 being collected
   uint64_t flush_ns = 0, done_ns = 0;
   // the collected result: tags copied (the slot's tag list is refilled when it reopens), the
   // rest read in place from the host pipe's pinned buffers, valid until EMQXGM_HOST_PIPES more
@@ -181,12 +181,15 @@ int emqxgm_batcher_flush(emqxgm_batcher_t* b, uint64_t* window) {
   // the next open window: a slot not in flight (SLOTS = HOST_PIPES + 1 guarantees one)
   for (uint32_t k = 1; k <= SLOTS; ++k) {
     const uint32_t s = (b->open + k) % SLOTS;
-    if (b->w[s].state != 1) {
+    if (b->w[s].state != 1 && b->w[s].state != 3) {
       b->open = s;
       Window& nw = b->w[s];
       nw.n = 0;
       nw.off[0] = 0;
       nw.tag.clear();
+      // a collected window reopened: its old id no longer names a result (-ENOENT)
+      nw.state = 0;
+      nw.id = 0;
       break;
     }
   }
@@ -195,21 +198,39 @@ int emqxgm_batcher_flush(emqxgm_batcher_t* b, uint64_t* window) {
 
 int emqxgm_batcher_collect(emqxgm_batcher_t* b, uint64_t window, emqxgm_window_out* out) {
   if (!b || !out || !window) return -EINVAL;
-  std::lock_guard<std::mutex> g(b->mu);
+  std::unique_lock<std::mutex> g(b->mu);
   Window* wp = nullptr;
   for (Window& w : b->w)
     if (w.id == window && w.state != 0) wp = &w;
   if (!wp) return -ENOENT;
   Window& w = *wp;
+  if (w.state == 3) return -EBUSY;  // another thread is collecting it right now
   if (w.state == 1) {
+    // the stream wait runs without the batcher lock (adds of other threads go on); state 3
+    // keeps the slot from being reopened or collected twice meanwhile
+    w.state = 3;
+    const uint64_t tk = w.ticket;
+    g.unlock();
+    emqxgm_batch_out r{};
+    const uint32_t* foff = nullptr;
+    const uint8_t* fb = nullptr;
     // every pair's filter bytes gathered on the device from its copy of the string pool (the
     // host registry per pair costs two random DRAM reads: ~250 ns per cfg3 topic, r03)
-    int rc = emqxgm_match_batch_wait_filters(b->h, w.ticket, &w.r, &w.r_foff, &w.r_fb);
-    if (rc) return rc;
+    const int rc = emqxgm_match_batch_wait_filters(b->h, tk, &r, &foff, &fb);
+    g.lock();
+    b->in_flight -= 1;
+    if (rc) {
+      // the window is gone (its callers are answered some other way): free its slot
+      w.state = 0;
+      w.id = 0;
+      return rc;
+    }
+    w.r = r;
+    w.r_foff = foff;
+    w.r_fb = fb;
     w.r_tag = w.tag;
     w.state = 2;
     w.done_ns = mono_ns();
-    b->in_flight -= 1;
   }
   out->n = w.r.n;
   out->n_pairs = w.r.n_pairs;

@@ -147,6 +147,7 @@ struct Filter {
   uint8_t trie_committed;
   uint8_t route_committed;
   uint32_t route_refs;
+  uint32_t sync_gen;  // emqxgm_route_set: the resync generation that last set it present
 };
 
 struct DevBuf {
@@ -386,6 +387,8 @@ struct emqxgm {
   uint64_t slot_mask = 0;
   uint64_t n_trie_pending = 0, n_route_pending = 0;
   bool dirty = false;
+  // emqxgm_route_sync_begin/_end: generation of the resync in progress (0: none)
+  uint32_t sync_gen = 0, sync_next = 1;
 
   // ---- the writer's working copy of the committed index (published as epochs) ----
   uint64_t epoch = 0;
@@ -398,6 +401,8 @@ struct emqxgm {
 
   // ---- what readers see ----
   EpochP cur;                      // current epoch (emu)
+  std::atomic<int> cur_trie_empty{1};  // cur->ix.trie_empty, readable without emu (which a
+                                       // commit holds across its patch wait)
   std::vector<EpochP> graveyard;   // retired epochs a reader may still hold (swept by writers)
 
   // ---- reader side (mmu) ----
@@ -476,6 +481,9 @@ struct emqxgm {
     Pinned h_blk;                                   // the packed block (FbLayout)
     bool fb_fast = false;                           // the last completion came from the block
     double fb_ppt = 0, fb_bpp = 0;                  // pairs per topic, bytes per pair (decaying max)
+    // recorded behind everything a submit enqueued: a waiter blocks on it without holding mmu,
+    // so other threads keep submitting (and waiting for other tickets) meanwhile
+    hipEvent_t fin = nullptr;
   } hpipes[EMQXGM_HOST_PIPES];
   uint64_t next_hticket = 1;
   hipStream_t pipe_streams[EMQXGM_HOST_PIPES] = {};  // pipe_stream(): shared by both pipe kinds
@@ -587,6 +595,7 @@ uint32_t find_id(emqxgm* h, const uint8_t* p, uint32_t len, bool create) {
   f.route_committed = 0;
   f.wild = is_wild(p, len) ? 1 : 0;
   f.route_refs = 0;
+  f.sync_gen = 0;
   h->pool.insert(h->pool.end(), p, p + len);
   h->filters.push_back(f);
   h->slots[i] = id + 1;
@@ -1421,6 +1430,7 @@ int publish_epoch(emqxgm* h, bool delta) {
   HIPCHK(h, hipEventRecord(E->ready, h->wstream));
   if (h->cur) h->graveyard.push_back(std::move(h->cur));
   h->cur = std::move(E);
+  h->cur_trie_empty.store(h->cur->ix.trie_empty ? 1 : 0);
   h->epoch += 1;
   return 0;
 }
@@ -1613,12 +1623,6 @@ int pass_prepare(emqxgm* h, PassCtx& c, uint32_t n, uint64_t bytes_len) {
   return 0;
 }
 
-#ifndef GM_CTL_KERNEL  // A/B builds may override it: the control words to the host by a kernel
-#define GM_CTL_KERNEL 1
-#endif
-#ifndef GM_CTL_IN_SCAN  // A/B builds may override it: ... by the row scan's last block
-#define GM_CTL_IN_SCAN 1
-#endif
 // Every launch of one pass against epoch E on the context's stream (caller holds emu).
 int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
                  const uint32_t* d_off, uint32_t n, bool legacy, bool census) {
@@ -1663,13 +1667,9 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
       roctx_mark(h->roctx && ix.needs_verify, "k_verify");
       if (ix.needs_verify) HIPCHK(h, launch_verify(d_bytes, d_off, ix, s, n, h->geom, st));
       roctx_mark(h->roctx, "k_scan");
-#if GM_CTL_IN_SCAN
       // the scan's last block mirrors the control words to the host (no launch of its own)
       HIPCHK(h, launch_scan_ctl(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, s.ctl, s.ctl_host_dev, st));
       ctl_sent = true;
-#else
-      HIPCHK(h, launch_scan(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, st));
-#endif
       roctx_mark(h->roctx, "k_scatter");
       HIPCHK(h, launch_scatter(s, n, h->geom, st, ctl_sent));
     } else {
@@ -1679,11 +1679,7 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
   }
   if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[3], st));
   if (!ctl_sent) {
-#if GM_CTL_KERNEL
     HIPCHK(h, launch_ctl_out(s.ctl, s.ctl_host_dev, st));
-#else
-    HIPCHK(h, hipMemcpyAsync(s.ctl_host, s.ctl, CTL_N * 4, hipMemcpyDeviceToHost, st));
-#endif
   }
   return 0;
 }
@@ -1691,12 +1687,7 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
 // Marks the end of the table reads a context enqueued (caller holds emu): a later delta commit
 // orders its patches behind this point.
 int mark_done(emqxgm* h, PassCtx& c) {
-#ifdef GM_AB_PASS_EVENT  // A/B builds: an event per pass, as until r03
-  HIPCHK(h, hipEventRecord(c.done, c.stream));
-  c.done_rec = true;
-#else
-  (void)h, (void)c;
-#endif
+  (void)h, (void)c;  // (until r03 an event per pass; a commit now records them itself)
   return 0;
 }
 
@@ -2158,6 +2149,7 @@ int grow_dev(emqxgm* h, DevBuf& b, uint64_t bytes, hipStream_t s) {
 
 void host_pipe_free(emqxgm::HostPipe& p) {
   ctx_free(p.c);
+  if (p.fin) (void)hipEventDestroy(p.fin);
   if (p.d_fb.p) (void)hipFree(p.d_fb.p);
   for (void* q : {p.h_fboff.p, p.h_fb.p})
     if (q) (void)hipHostFree(q);
@@ -2314,6 +2306,89 @@ int emqxgm_route_unref(emqxgm_t* h, const uint8_t* filter, uint32_t len) {
   return 0;
 }
 
+// Level-triggered route-key membership (emqx_router_utils.erl:34-39, 57-71 as a state): the
+// route key exists, and a wildcard filter is in the trie, exactly when `present`.  Overrides the
+// refcount route_ref/route_unref keep (a mirror that calls this never counts).
+static void route_set_locked(emqxgm* h, uint32_t i, bool present) {
+  Filter& f = h->filters[i];
+  const bool was = f.route_refs > 0;
+  if (present) f.sync_gen = h->sync_gen;
+  if (present == was && (!f.wild || (bool)f.in_trie == present)) return;
+  if (present != was) {
+    f.route_refs = present ? 1 : 0;
+    if (present) ++h->n_route_pending; else --h->n_route_pending;
+  }
+  if (f.wild && (bool)f.in_trie != present) {
+    f.in_trie = present ? 1 : 0;
+    if (present) ++h->n_trie_pending; else --h->n_trie_pending;
+  }
+  h->changed.push_back(i);
+  h->dirty = true;
+}
+
+int emqxgm_route_set(emqxgm_t* h, const uint8_t* filter, uint32_t len, int present) {
+  if (!h || (!filter && len) || len > 65535) return -EINVAL;
+  WriterLock g(h);
+  if (!present) {
+    const uint32_t i = find_id(h, filter, len, false);
+    if (i != NONE) route_set_locked(h, i, false);
+    return 0;
+  }
+  if (h->filters.size() >= 0x7FFFFFFFu) return -E2BIG;
+  route_set_locked(h, find_id(h, filter, len, true), true);
+  return 0;
+}
+
+int emqxgm_route_set_many(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                          int present) {
+  if (!h || !offsets || (!bytes && n)) return -EINVAL;
+  for (uint64_t i = 0; i < n; ++i)
+    if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > 65535) return -EINVAL;
+  WriterLock g(h);
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint8_t* p = bytes + offsets[i];
+    const uint32_t len = (uint32_t)(offsets[i + 1] - offsets[i]);
+    const uint32_t id = find_id(h, p, len, present != 0);
+    if (id == NONE) continue;
+    if (h->filters.size() >= 0x7FFFFFFFu) return -E2BIG;
+    route_set_locked(h, id, present != 0);
+  }
+  return 0;
+}
+
+int emqxgm_route_sync_begin(emqxgm_t* h, uint32_t* gen) {
+  if (!h) return -EINVAL;
+  WriterLock g(h);
+  h->sync_gen = h->sync_next++;
+  if (h->sync_next == 0) h->sync_next = 1;  // 0 means "no resync"
+  if (gen) *gen = h->sync_gen;
+  return 0;
+}
+
+int emqxgm_route_sync_end(emqxgm_t* h, uint32_t gen, uint64_t* removed) {
+  if (!h) return -EINVAL;
+  WriterLock g(h);
+  if (gen == 0 || gen != h->sync_gen) return -ESTALE;
+  uint64_t k = 0;
+  for (uint32_t i = 0; i < (uint32_t)h->filters.size(); ++i) {
+    const Filter& f = h->filters[i];
+    if (f.route_refs > 0 && f.sync_gen != gen) {
+      route_set_locked(h, i, false);
+      ++k;
+    }
+  }
+  h->sync_gen = 0;
+  if (removed) *removed = k;
+  return 0;
+}
+
+int emqxgm_route_member(emqxgm_t* h, const uint8_t* filter, uint32_t len) {
+  if (!h || (!filter && len)) return -EINVAL;
+  std::shared_lock<std::shared_mutex> g(h->pmu);
+  const uint32_t i = find_id(h, filter, len, false);
+  return (i != NONE && h->filters[i].route_committed) ? 1 : 0;
+}
+
 // ---- publish fan-out registry ----
 
 int emqxgm_route_add(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t node,
@@ -2452,7 +2527,7 @@ int emqxgm_commit(emqxgm_t* h, uint64_t* epoch) {
 namespace {
 
 constexpr uint64_t SNAP_MAGIC = 0x31534d47584d45ull;  // "EMXGMS1"
-constexpr uint32_t SNAP_VERSION = 2;  // 2: fat buckets (TrieModel fchild / half)
+constexpr uint32_t SNAP_VERSION = 3;  // 2: fat buckets (TrieModel fchild / half), 3: Filter::sync_gen
 
 struct SnapOut {
   FILE* f;
@@ -2763,8 +2838,7 @@ int emqxgm_snapshot_load(emqxgm_t* h, const char* path) {
 
 int emqxgm_trie_empty(emqxgm_t* h) {
   if (!h) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->emu);
-  return h->cur->ix.trie_empty ? 1 : 0;
+  return h->cur_trie_empty.load();
 }
 
 int emqxgm_trie_member(emqxgm_t* h, const uint8_t* filter, uint32_t len) {
@@ -2951,6 +3025,8 @@ int batch_submit(emqxgm* h, const uint8_t* bytes, const uint32_t* offsets, uint3
     if ((rc = pass_submit(h, p.c, p.d_bytes, p.d_off, n, false, false)) ||
         (rc = host_pipe_copy_out(h, p)) || (want_fb && (rc = host_pipe_enqueue_gather(h, p))))
       return rc;
+    if (!p.fin) HIPCHK(h, hipEventCreateWithFlags(&p.fin, hipEventDisableTiming));
+    HIPCHK(h, hipEventRecord(p.fin, p.c.stream));
     p.state = 1;
   }
   p.ticket = tk;
@@ -3011,8 +3087,26 @@ int emqxgm_match_batch_submit_filters(emqxgm_t* h, const uint8_t* bytes, const u
   return batch_submit(h, bytes, offsets, n, ticket, true);
 }
 
+// Blocks until everything ticket's submit enqueued has run, without holding mmu (the stream
+// wait of host_pipe_complete is then immediate).  Only the waiter of a ticket changes its pipe's
+// state while it is in flight (a resubmit of the pipe needs the ticket waited: -EBUSY).
+static int host_pipe_prewait(emqxgm* h, uint64_t ticket) {
+  hipEvent_t ev = nullptr;
+  {
+    std::lock_guard<std::mutex> g(h->mmu);
+    const emqxgm::HostPipe& p = h->hpipes[ticket % EMQXGM_HOST_PIPES];
+    if (ticket != 0 && p.ticket == ticket && p.state == 1) ev = p.fin;
+  }
+  if (ev && (hipSetDevice(h->cfg.device) != hipSuccess || hipEventSynchronize(ev) != hipSuccess)) {
+    set_err(h, "hipEventSynchronize failed");
+    return -EIO;
+  }
+  return 0;
+}
+
 int emqxgm_match_batch_wait(emqxgm_t* h, uint64_t ticket, emqxgm_batch_out* out) {
   if (!h || !out) return -EINVAL;
+  if (int rc = host_pipe_prewait(h, ticket)) return rc;
   std::lock_guard<std::mutex> g(h->mmu);
   RoctxRange rr(h->roctx, "emqxgm.host_wait");
   if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
@@ -3035,6 +3129,7 @@ int emqxgm_match_batch_wait(emqxgm_t* h, uint64_t ticket, emqxgm_batch_out* out)
 int emqxgm_match_batch_wait_filters(emqxgm_t* h, uint64_t ticket, emqxgm_batch_out* out,
                                     const uint32_t** foff, const uint8_t** fbytes) {
   if (!h || !out || !foff || !fbytes) return -EINVAL;
+  if (int rc = host_pipe_prewait(h, ticket)) return rc;
   std::lock_guard<std::mutex> g(h->mmu);
   if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
   RoctxRange rr(h->roctx, "emqxgm.host_wait_filters");
@@ -3137,7 +3232,7 @@ void* emqxgm_host_alloc(emqxgm_t* h, uint64_t bytes) {
   if (!h) return nullptr;
   void* p = nullptr;
   if (hipSetDevice(h->cfg.device) != hipSuccess ||
-      hipHostMalloc(&p, std::max<uint64_t>(bytes, 1), hipHostMallocDefault) != hipSuccess)
+      hipHostMalloc(&p, std::max<uint64_t>(bytes, 1), hipHostMallocPortable) != hipSuccess)
     return nullptr;
   return p;
 }

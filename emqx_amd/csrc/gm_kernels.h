@@ -118,16 +118,11 @@ constexpr uint32_t REJ_SCAN_MAX = 4096;  // rejects the deferred scatter handles
 // (2 blocks per CU); cfg3 never leaves the shallow stack (an 8-deep one cost it ~1.5%).
 // Walk item stacks per variant level: SHALLOW and DEEP keep compact 32-bit items in LDS (12 at
 // four blocks per CU, 24 at three: gm_walk.inc CPT), SPILL keeps 12 {node, level} pairs in LDS
-// and continues in global memory.  GM_WALK_CPT=0 (A/B builds): 8-B items, 6 / 12 / 12 + spill.
-#ifndef GM_WALK_CPT
-#define GM_WALK_CPT 1
-#endif
-constexpr bool WALK_CPT = GM_WALK_CPT != 0;
-constexpr uint32_t WALK_STK_SHALLOW = WALK_CPT ? 12 : 6;
-#ifndef GM_WALK_STK_DEEP_CPT  // A/B builds may override it
-#define GM_WALK_STK_DEEP_CPT 24
-#endif
-constexpr uint32_t WALK_STK_DEEP = WALK_CPT ? GM_WALK_STK_DEEP_CPT : 12;
+// and continues in global memory (r03: compact items made cfg2's walk 1.274 -> 1.229 ms;
+// an 18-item deep stack made its pipelined step slower, profiles/r03/results/ab_*).
+constexpr bool WALK_CPT = true;
+constexpr uint32_t WALK_STK_SHALLOW = 12;
+constexpr uint32_t WALK_STK_DEEP = 24;
 constexpr uint32_t WALK_STK_SPILL = 12;
 enum WalkLevel : uint32_t { WALK_SHALLOW = 0, WALK_DEEP = 1, WALK_SPILL = 2 };
 constexpr uint32_t WALK_SPILL_MIN = 32;  // initial spill items per lane (grown on overflow)

@@ -20,25 +20,7 @@ namespace {
 
 constexpr uint32_t WG = 256;
 constexpr uint32_t CH = STAGE_CHUNK;  // staged-pair slots reserved per wave per atomic
-#ifndef GM_STATIC_ONE  // A/B builds may override it
-#define GM_STATIC_ONE 1
-#endif
-#ifndef GM_SMALL_WS  // A/B builds may override it: probe slots of the one-topic-per-lane walk
-#define GM_SMALL_WS 2  // r03: 4 slots (158 VGPRs) cost cfg3 64k-topic walks 0.019 -> 0.023 ms
-#endif
-#ifndef GM_STATIC_CLAIM  // A/B builds may override it
-#define GM_STATIC_CLAIM 1
-#endif
-#ifndef GM_STATIC_CHUNK  // A/B builds may override it
-#define GM_STATIC_CHUNK 1
-#endif
-#ifndef GM_SMALL_GRID  // A/B builds may override it
-#define GM_SMALL_GRID 1
-#endif
-#ifndef GM_TBLK  // A/B builds may override it
-#define GM_TBLK 128
-#endif
-constexpr uint32_t TBLK = GM_TBLK;  // topics claimed per wave per atomic
+constexpr uint32_t TBLK = 128;  // topics claimed per wave per atomic (r02: 64 / 256 no better)
 constexpr uint32_t SCAN_ITEMS = 16;
 constexpr uint32_t SCAN_TILE = WG * SCAN_ITEMS;
 constexpr uint32_t TILE_BYTES = 16384;  // tokenizer LDS tile (256 topics)
@@ -602,10 +584,7 @@ uint32_t walk_blocks(const WalkGeom& g, uint32_t n, uint32_t level) {
                        : level == WALK_DEEP ? walk_lds_bytes(WALK_STK_DEEP, WALK_CPT)
                                             : walk_lds_bytes(WALK_STK_SHALLOW, WALK_CPT);
   uint32_t blocks = std::min<uint32_t>(g.blocks, g.cus * (LDS_CU / lds));
-#if GM_SMALL_GRID
-  blocks = std::min<uint32_t>(blocks, std::max<uint32_t>((n + WG - 1) / WG, g.cus));
-#endif
-  return blocks;
+  return std::min<uint32_t>(blocks, std::max<uint32_t>((n + WG - 1) / WG, g.cus));
 }
 
 // Topics per claim: a batch too small to give every wave TBLK topics is spread over all of them
@@ -624,7 +603,7 @@ void walk_claim_init(const WalkGeom& g, uint32_t n, uint32_t level, uint32_t cla
   const uint32_t blocks = walk_blocks(g, n, level);
   const uint32_t tblk = walk_tblk(blocks, n);
   // exactly the walk's condition: claims at all (not static_one), static first ones
-  const bool on = GM_STATIC_CLAIM && !(GM_STATIC_ONE && (uint64_t)n <= (uint64_t)blocks * WG);
+  const bool on = (uint64_t)n > (uint64_t)blocks * WG;
   for (uint32_t cs = 0; cs < WALK_SHARDS; ++cs) {
     const uint32_t lo = (uint32_t)((uint64_t)n * cs / WALK_SHARDS);
     const uint32_t hi = (uint32_t)((uint64_t)n * (cs + 1) / WALK_SHARDS);
@@ -637,13 +616,8 @@ void walk_claim_init(const WalkGeom& g, uint32_t n, uint32_t level, uint32_t cla
 // its first flush on (only later chunks take an atomic on CTL_PAIR_TOP, which k_tok sets to the
 // end of the static ones).  0 when the staging buffer cannot hold one chunk per wave.
 uint32_t walk_static_chunks(const WalkGeom& g, uint32_t n, uint32_t level, uint32_t pcap) {
-#if GM_STATIC_CHUNK
   const uint64_t waves = (uint64_t)walk_blocks(g, n, level) * (WG / 64);
   return waves * CH <= pcap ? (uint32_t)waves : 0u;
-#else
-  (void)g, (void)n, (void)level, (void)pcap;
-  return 0u;
-#endif
 }
 
 hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGeom& g,
@@ -677,9 +651,9 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   a.tblk = walk_tblk(blocks, n);
   // at most one topic per lane of the launched grid: lane gl walks topic gl, no claims (r03:
   // the failed claims of every wave on the exhausted counters dominated small batches)
-  a.static_one = GM_STATIC_ONE && (uint64_t)n <= (uint64_t)blocks * WG ? 1u : 0u;
+  a.static_one = (uint64_t)n <= (uint64_t)blocks * WG ? 1u : 0u;
   a.stat_chunks = stat_chunks;
-  a.static_claim = GM_STATIC_CLAIM;
+  a.static_claim = 1;
   a.census = census;
   a.leafp_mask = ix.leafp_mask;
   a.root_sig = ix.root_sig;
@@ -693,12 +667,6 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
       hipLaunchKernelGGL((k_walk<true, false, DP, C>), grid, dim3(WG), 0, s, a);
     else
       hipLaunchKernelGGL((k_walk<true, false, SH, C>), grid, dim3(WG), 0, s, a);
-  } else if (a.static_one && GM_SMALL_WS != WSLOTS && level < WALK_SPILL && blocks <= 3 * g.cus) {
-    // one topic per lane: the 4-slot variants (fewer, wider iterations; three blocks per CU)
-    if (level == WALK_DEEP)
-      hipLaunchKernelGGL((k_walk<false, false, DP, C, GM_SMALL_WS>), grid, dim3(WG), 0, s, a);
-    else
-      hipLaunchKernelGGL((k_walk<false, false, SH, C, GM_SMALL_WS>), grid, dim3(WG), 0, s, a);
   } else {
     if (level >= WALK_SPILL)
       hipLaunchKernelGGL((k_walk<false, true, SP>), grid, dim3(WG), 0, s, a);

@@ -17,7 +17,8 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libemqx_gpumatch.so")
 NONE = 0xFFFFFFFF
-ABI_VERSION = 2  # include/emqx_gpumatch.h EMQXGM_ABI_VERSION
+ABI_VERSION = 3  # include/emqx_gpumatch.h EMQXGM_ABI_VERSION
+TAG_CANCELLED = 0xFFFFFFFFFFFFFFFF  # EMQXGM_TAG_CANCELLED
 
 
 class EngineError(RuntimeError):
@@ -68,6 +69,24 @@ class _WindowOut(C.Structure):
                 ("done_ns", C.c_uint64)]
 
 
+class _AsyncCfg(C.Structure):
+    _fields_ = [("window_topics", C.c_uint32), ("window_bytes", C.c_uint32),
+                ("window_us", C.c_uint32), ("max_levels", C.c_uint32),
+                ("queued_windows", C.c_uint32), ("reserved", C.c_uint32 * 3)]
+
+
+class _AsyncWindow(C.Structure):
+    _fields_ = [("status", C.c_int), ("n", C.c_uint32), ("n_pairs", C.c_uint32),
+                ("device_index", C.c_uint32), ("tag", C.POINTER(C.c_uint64)),
+                ("owner", C.POINTER(C.c_uint64)), ("row", C.POINTER(C.c_uint32)),
+                ("filter_id", C.POINTER(C.c_uint32)), ("foff", C.POINTER(C.c_uint32)),
+                ("fbytes", C.POINTER(C.c_uint8)), ("exact_id", C.POINTER(C.c_uint32)),
+                ("first_ns", C.c_uint64), ("flush_ns", C.c_uint64), ("done_ns", C.c_uint64)]
+
+
+ASYNC_CB = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(_AsyncWindow))
+
+
 class _RetOut(C.Structure):
     _fields_ = [("n", C.c_uint32), ("n_ids", C.c_uint64), ("ptr", C.POINTER(C.c_uint64)),
                 ("id", C.POINTER(C.c_uint32))]
@@ -102,6 +121,11 @@ SYMBOLS = {
     "emqxgm_route_unref": (C.c_int, [_P, C.c_char_p, C.c_uint32]),
     "emqxgm_trie_insert_many": (C.c_int, [_P, _P, _P, C.c_uint64, _P]),
     "emqxgm_route_ref_many": (C.c_int, [_P, _P, _P, C.c_uint64, _P]),
+    "emqxgm_route_set": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_int]),
+    "emqxgm_route_set_many": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_int]),
+    "emqxgm_route_sync_begin": (C.c_int, [_P, _U32P]),
+    "emqxgm_route_sync_end": (C.c_int, [_P, C.c_uint32, _U64P]),
+    "emqxgm_route_member": (C.c_int, [_P, C.c_char_p, C.c_uint32]),
     "emqxgm_commit": (C.c_int, [_P, _U64P]),
     "emqxgm_trie_empty": (C.c_int, [_P]),
     "emqxgm_snapshot_save": (C.c_int, [_P, C.c_char_p]),
@@ -157,6 +181,12 @@ SYMBOLS = {
     "emqxgm_batcher_add_many": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64]),
     "emqxgm_batcher_flush": (C.c_int, [_P, _U64P]),
     "emqxgm_batcher_collect": (C.c_int, [_P, C.c_uint64, C.POINTER(_WindowOut)]),
+    "emqxgm_async_create": (C.c_int, [_P, C.c_uint32, C.POINTER(_AsyncCfg), ASYNC_CB, _P,
+                                      C.POINTER(_P)]),
+    "emqxgm_async_destroy": (None, [_P]),
+    "emqxgm_async_match": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint64, C.c_uint64]),
+    "emqxgm_async_cancel": (C.c_int, [_P, C.c_uint64, C.c_uint64]),
+    "emqxgm_async_stats": (C.c_int, [_P, _U64P]),
     "emqxgm_set_profiling": (C.c_int, [_P, C.c_int]),
     "emqxgm_tune": (C.c_int, [_P, C.c_char_p, C.c_int64]),
     "emqxgm_get_stats": (C.c_int, [_P, C.POINTER(_Stats)]),
@@ -164,13 +194,17 @@ SYMBOLS = {
 }
 
 
-def load_library(path: str = LIB_PATH) -> C.CDLL:
+def load_library(path: str = LIB_PATH, allow_missing: bool = False) -> C.CDLL:
+    """The engine library with every SYMBOLS signature set.  allow_missing: skip entry points
+    the library lacks (tests/host_harness's CPU build of the host code has no retainer)."""
     if not os.path.exists(path):
         raise ImportError(
             f"{path} is missing: build the HIP engine first (python -m emqx_amd.build); "
             "there is no CPU fallback")
     lib = C.CDLL(path)
     for name, (res, args) in SYMBOLS.items():
+        if allow_missing and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -253,8 +287,10 @@ class Engine:
     """One engine instance = one device index (one emqx_trie + route-key set) on one GPU."""
 
     def __init__(self, device: int = 0, word_hash_bits: int = 0, full_hash_bits: int = 64,
-                 batch_max: int = 0, walk_wg_per_cu: int = 0, reject_cap: int = 0):
-        self._lib = lib()
+                 batch_max: int = 0, walk_wg_per_cu: int = 0, reject_cap: int = 0,
+                 library: Optional[C.CDLL] = None):
+        # library: another build of the C-ABI (tests: the host code on a fake HIP runtime)
+        self._lib = library or lib()
         self.device = device
         cfg = _Cfg(device, word_hash_bits, full_hash_bits, batch_max, walk_wg_per_cu, reject_cap)
         h = C.c_void_p()
@@ -300,6 +336,30 @@ class Engine:
 
     def route_unref(self, f: bytes) -> None:
         self._check(self._lib.emqxgm_route_unref(self._h, f, len(f)), "route_unref")
+
+    # ---- the level-triggered mirror (emqxgm_route_set: the NIF's sync process) ----
+    def route_set(self, f: bytes, present: bool) -> None:
+        self._check(self._lib.emqxgm_route_set(self._h, f, len(f), 1 if present else 0), "route_set")
+
+    def route_set_many(self, buf: np.ndarray, off: np.ndarray, present: bool) -> None:
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        self._check(self._lib.emqxgm_route_set_many(self._h, _ptr(buf), _ptr(off), len(off) - 1,
+                                                     1 if present else 0), "route_set_many")
+
+    def sync_begin(self) -> int:
+        g = C.c_uint32()
+        self._check(self._lib.emqxgm_route_sync_begin(self._h, C.byref(g)), "route_sync_begin")
+        return int(g.value)
+
+    def sync_end(self, gen: int) -> int:
+        """Ends a resync: route keys not set present since sync_begin are removed; how many."""
+        k = C.c_uint64()
+        self._check(self._lib.emqxgm_route_sync_end(self._h, gen, C.byref(k)), "route_sync_end")
+        return int(k.value)
+
+    def route_member(self, f: bytes) -> bool:
+        return bool(self._check(self._lib.emqxgm_route_member(self._h, f, len(f)), "route_member"))
 
     # ---- publish fan-out registry (emqx_router do_add_route/do_delete_route, subscribers) ----
     def route_add(self, f: bytes, node: int, group: int = NONE) -> None:
@@ -684,3 +744,102 @@ class Batcher:
                       arr(o.filter_id, m, np.uint32), arr(o.foff, m + 1, np.uint32),
                       C.string_at(o.fbytes, nb) if nb else b"", arr(o.exact_id, n, np.uint32),
                       int(o.done_ns - o.flush_ns))
+
+
+@dataclass
+class AsyncResult:
+    """One reported call of the concurrent entry: its trie filters' bytes (None: the window
+    failed, status < 0) and its exact route key id."""
+    tag: int
+    owner: int
+    status: int
+    filters: Optional[List[bytes]]
+    exact_id: int
+    device_index: int
+    latency_ns: int  # first call of its window -> its window's result complete
+
+
+class AsyncMatcher:
+    """emqxgm_async_*: the concurrent publish entry (what the NIF's match_async/3 calls) over
+    one or more engines (one per GPU, each holding the whole index).  `callback(results)` gets
+    the reported calls of each completed window (a list of AsyncResult), from an engine
+    completer thread; the default callback stores them in ``self.results`` by (tag, owner)."""
+
+    def __init__(self, engines: Sequence[Engine], callback=None, window_topics: int = 0,
+                 window_bytes: int = 0, window_us: int = 0, max_levels: int = 0,
+                 queued_windows: int = 0):
+        import threading
+        self._engines = list(engines)  # kept alive: the layer uses their handles
+        self._lib = self._engines[0]._lib
+        self.results = {}
+        self._cv = threading.Condition()
+        self._user_cb = callback
+
+        def on_window(_user, wp):
+            w = wp.contents
+            out = []
+            for i in range(w.n):
+                tag = w.tag[i]
+                if tag == TAG_CANCELLED:
+                    continue
+                if w.status:
+                    fl, ex = None, NONE
+                else:
+                    fl = [C.string_at(C.addressof(w.fbytes.contents) + w.foff[j],
+                                      w.foff[j + 1] - w.foff[j]) if w.foff[j + 1] > w.foff[j] else b""
+                          for j in range(w.row[i], w.row[i + 1])]
+                    ex = w.exact_id[i]
+                out.append(AsyncResult(tag, w.owner[i], w.status, fl, ex, w.device_index,
+                                       w.done_ns - w.first_ns))
+            if self._user_cb is not None:
+                self._user_cb(out)
+            else:
+                with self._cv:
+                    for r in out:
+                        self.results[(r.tag, r.owner)] = r
+                    self._cv.notify_all()
+        self._cb = ASYNC_CB(on_window)  # kept alive as long as the layer
+        cfg = _AsyncCfg(window_topics, window_bytes, window_us, max_levels, queued_windows)
+        arr = (C.c_void_p * len(self._engines))(*[e._h for e in self._engines])
+        a = C.c_void_p()
+        self._engines[0]._check(self._lib.emqxgm_async_create(arr, len(self._engines), C.byref(cfg),
+                                                              self._cb, None, C.byref(a)),
+                                "async_create")
+        self._a = a
+
+    def match(self, topic: bytes, tag: int, owner: int = 0) -> int:
+        """0: accepted (reported later); -E2BIG / -EBUSY / -EINVAL: the caller answers it."""
+        return self._lib.emqxgm_async_match(self._a, topic, len(topic), tag, owner)
+
+    def cancel(self, tag: int, owner: int = 0) -> bool:
+        return bool(self._engines[0]._check(self._lib.emqxgm_async_cancel(self._a, tag, owner),
+                                            "async_cancel"))
+
+    def wait(self, keys, timeout: float = 30.0) -> bool:
+        """Default callback only: until every (tag, owner) in keys was reported."""
+        import time
+        end = time.time() + timeout
+        with self._cv:
+            while not all(k in self.results for k in keys):
+                left = end - time.time()
+                if left <= 0:
+                    return False
+                self._cv.wait(left)
+        return True
+
+    def stats(self) -> dict:
+        v = (C.c_uint64 * 8)()
+        self._engines[0]._check(self._lib.emqxgm_async_stats(self._a, v), "async_stats")
+        return dict(zip(("calls", "windows", "reported", "busy", "cancelled", "too_deep",
+                         "failed", "outstanding"), list(v)))
+
+    def close(self):
+        if getattr(self, "_a", None):
+            self._lib.emqxgm_async_destroy(self._a)  # reports every accepted call first
+            self._a = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -11,6 +11,11 @@
  *   emqxgm_trie_member   <- emqx_trie:lookup_topic/2  apps/emqx/src/emqx_trie.erl:267-271
  *   emqxgm_route_ref     <- route-bag key insert      apps/emqx/src/emqx_router_utils.erl:31-39
  *   emqxgm_route_unref   <- route-bag key delete      apps/emqx/src/emqx_router_utils.erl:48-71
+ *   emqxgm_route_set     <- the same membership rule as a state, for a mirror of the committed
+ *                           route table (emqx_router_utils.erl:34-39, 57-71; emqx_router.erl:72-92)
+ *   emqxgm_async_match   <- emqx_trie:match/1 called from every publisher process at once
+ *                           (emqx_broker.erl:218-232 -> emqx_router.erl:141-153, read_concurrency
+ *                           tables emqx_trie.erl:70-75): the NIF's match_async/3
  *   emqxgm_commit        <- mnesia/mria commit point  (snapshot swap; readers never see partial
  *                           state; emqx_router_utils.erl:74-135 is where writes commit)
  *   emqxgm_match_batch   <- emqx_trie:match/1 + emqx_router:match_routes/1 over a batch of
@@ -71,7 +76,7 @@ extern "C" {
 #define EMQXGM_DEST_GROUP 0x80000000u /* dest handle bit: a shared-subscription group */
 #define EMQXGM_RULE_EQ 1u    /* rule flag: {eq, Filter} -- the name must equal the filter */
 #define EMQXGM_RULE_WORDS 2u /* rule flag: match/2 on word lists (no '$' clauses) */
-#define EMQXGM_ABI_VERSION 2
+#define EMQXGM_ABI_VERSION 3
 
 typedef struct emqxgm emqxgm_t;
 
@@ -153,6 +158,25 @@ int emqxgm_commit(emqxgm_t* h, uint64_t* epoch /* nullable */);
  * -EBUSY: the handle is not fresh; -EINVAL: not a snapshot of this configuration. */
 int emqxgm_snapshot_save(emqxgm_t* h, const char* path);
 int emqxgm_snapshot_load(emqxgm_t* h, const char* path);
+/* Level-triggered route-key membership, for a mirror of the committed route table (the NIF's sync
+ * process): present != 0 makes `filter` a route key and, when it is a wildcard filter
+ * (emqx_topic:wildcard/1), a trie member; present == 0 removes both -- the state
+ * emqx_router_utils.erl:34-39, 57-71 keeps (a route key exists while its filter has a route, a
+ * wildcard filter is in the trie while it has one).  Idempotent: the index converges to the
+ * route table's state whatever the number and order of the calls that told it so.  It overrides
+ * the refcount emqxgm_route_ref / _unref keep: a mirror uses this call alone.  Visible after
+ * emqxgm_commit. */
+int emqxgm_route_set(emqxgm_t* h, const uint8_t* filter, uint32_t len, int present);
+int emqxgm_route_set_many(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                          int present);
+/* A full resync (the mirror's start and its periodic anti-entropy pass): _begin starts generation
+ * *gen; every emqxgm_route_set(.., 1) until _end marks its filter; _end(gen) sets every route key
+ * that was not marked absent (*removed of them).  -ESTALE if another _begin came in between. */
+int emqxgm_route_sync_begin(emqxgm_t* h, uint32_t* gen);
+int emqxgm_route_sync_end(emqxgm_t* h, uint32_t gen, uint64_t* removed /* nullable */);
+/* 1 if `filter` is a committed route key (emqx_router:has_routes/1 of the committed index), 0 if
+ * not. */
+int emqxgm_route_member(emqxgm_t* h, const uint8_t* filter, uint32_t len);
 /* 1 if the committed trie holds no filter, 0 otherwise (emqx_trie:empty/0). */
 int emqxgm_trie_empty(emqxgm_t* h);
 /* 1 if the committed trie holds exactly this filter key (emqx_trie:lookup_topic/2,
@@ -390,6 +414,58 @@ int emqxgm_batcher_flush(emqxgm_batcher_t* b, uint64_t* window);
  * read in place from the host pipe's pinned buffers: valid until EMQXGM_HOST_PIPES more windows
  * are flushed (collecting it again before that returns the same result). */
 int emqxgm_batcher_collect(emqxgm_batcher_t* b, uint64_t window, emqxgm_window_out* out);
+
+/* ---- concurrent publish entry: one topic per call from any number of threads ------------------
+ * The reference matches every publish in the publisher's own process, on every scheduler at once
+ * (emqx_broker:publish/1 -> emqx_router:match_routes/1 -> emqx_trie:match/1,
+ * emqx_broker.erl:218-232, emqx_router.erl:141-153, read_concurrency ETS emqx_trie.erl:70-75).
+ * emqxgm_async_match is what those processes call through the NIF (match_async/3): it appends the
+ * topic to the open window in pinned memory and returns at once; a flusher thread submits a
+ * window when it is full or window_us after its first topic, over the handles' host pipes (round
+ * robin over the handles with a pipe free: one handle per GPU, each holding the whole index), and
+ * one completer thread per handle waits for its windows in order and calls `cb` once per window
+ * (from that thread; the windows of different handles concurrently).  The window passed to `cb`
+ * is valid during the call only.  Every accepted call is reported exactly once, unless cancelled
+ * first.  Errors of emqxgm_async_match: -E2BIG (longer than a window, or more than max_levels
+ * levels), -EBUSY (every window full or in flight), -EINVAL: the caller answers those itself. */
+#define EMQXGM_TAG_CANCELLED 0xFFFFFFFFFFFFFFFFull /* never a caller's tag */
+typedef struct emqxgm_async emqxgm_async_t;
+typedef struct emqxgm_async_cfg {
+  uint32_t window_topics;  /* topics per window (0 = 65,536; <= every handle's batch_max) */
+  uint32_t window_bytes;   /* topic bytes per window (0 = 64 x window_topics) */
+  uint32_t window_us;      /* a window is submitted at most this long after its first topic (0 = 50) */
+  uint32_t max_levels;     /* calls for topics with more levels: -E2BIG (0 = no limit) */
+  uint32_t queued_windows; /* full windows that may wait for a pipe (0 = 2) */
+  uint32_t reserved[3];
+} emqxgm_async_cfg;
+typedef struct emqxgm_async_window {
+  int status;               /* 0, or the negative errno the window's pass failed with (no result) */
+  uint32_t n;               /* calls in the window, in the order they were made */
+  uint32_t n_pairs;
+  uint32_t device_index;    /* the handle that matched it */
+  const uint64_t* tag;      /* [n] each call's tag (EMQXGM_TAG_CANCELLED: cancelled, skip it) */
+  const uint64_t* owner;    /* [n] each call's owner (e.g. the calling process) */
+  const uint32_t* row;      /* [n+1] call i's trie filters are pairs row[i] .. row[i+1] */
+  const uint32_t* filter_id;/* [n_pairs] */
+  const uint32_t* foff;     /* [n_pairs + 1] pair j's filter bytes: fbytes[foff[j] .. foff[j+1]) */
+  const uint8_t* fbytes;
+  const uint32_t* exact_id; /* [n] route key equal to the topic, or EMQXGM_NONE */
+  uint64_t first_ns, flush_ns, done_ns; /* CLOCK_MONOTONIC: first call, submit, result complete */
+} emqxgm_async_window;
+typedef void (*emqxgm_async_cb)(void* user, const emqxgm_async_window* w);
+int emqxgm_async_create(emqxgm_t* const* hs, uint32_t n_handles, const emqxgm_async_cfg* cfg,
+                        emqxgm_async_cb cb, void* user, emqxgm_async_t** out);
+/* Stops taking calls, submits and reports every accepted one, then frees the layer. */
+void emqxgm_async_destroy(emqxgm_async_t* a);
+int emqxgm_async_match(emqxgm_async_t* a, const uint8_t* topic, uint32_t len, uint64_t tag,
+                       uint64_t owner);
+/* 1: the call (tag, owner) was still pending and will never be reported; 0: it was reported
+ * already (when its window is being reported right now, this waits until that is done) or is
+ * unknown.  A caller that timed out cancels, and on 0 finds the report delivered. */
+int emqxgm_async_cancel(emqxgm_async_t* a, uint64_t tag, uint64_t owner);
+/* out = {calls accepted, windows submitted, calls reported, -EBUSY refusals, cancelled, -E2BIG
+ * refusals (levels), windows failed, windows outstanding} */
+int emqxgm_async_stats(emqxgm_async_t* a, uint64_t out[8]);
 
 /* ---- filter-sharded layout over several GPUs (the subscription set partitioned by
  * filter, the topic batch broadcast, the per-GPU match lists gathered to one GPU) ----

@@ -1,74 +1,111 @@
 %%--------------------------------------------------------------------
-%% emqx_trie_gpu -- emqx_trie:match/1 and emqx_router:match_routes/1 on the MI355X engine.
+%% emqx_trie_gpu -- emqx_trie:match/1, match_session/1 and emqx_router:match_routes/1 on the
+%% MI355X engine.
 %%
-%%   emqx_trie:match/1        apps/emqx/src/emqx_trie.erl:147-169
-%%   emqx_router:match_trie/1 apps/emqx/src/emqx_router.erl:149-153
-%%   emqx_router:match_routes/1                      :141-146
+%%   emqx_trie:match/1, match_session/1        apps/emqx/src/emqx_trie.erl:147-169
+%%   emqx_trie:empty/0, empty_session/0                                  :172-178
+%%   emqx_router:match_trie/1, match_routes/1  apps/emqx/src/emqx_router.erl:141-153
 %%
-%% The route bag (emqx_route) and the mnesia trie stay the source of truth; the device index
-%% mirrors their committed state (emqx_trie_gpu_sync) and answers the match through the
-%% batcher (emqx_trie_gpu_batcher).  Configuration: broker.perf.gpu_match
-%% (emqx_trie_gpu_schema); with enable = false every call is the reference's own.
+%% Every publisher process calls in itself, concurrently, as it calls emqx_trie:match/1 in the
+%% reference (emqx_broker.erl:218-232): match_async/3 hands the topic to the engine's open window
+%% on the caller's own scheduler and the caller waits for {emqx_trie_gpu, Id, Result}, which an
+%% engine completer thread sends once the window's device pass is done.  No process sits between
+%% the publishers and the device.
+%%
+%% The route tables (emqx_route; the session router's when persistent sessions are enabled) stay
+%% the source of truth: emqx_trie_gpu_sync mirrors their committed state into the device indexes
+%% and publishes an index only once its first full sync has been committed.  With enable = false,
+%% before that, and whenever the device cannot answer (a topic deeper than max_levels, every
+%% window busy, a device error, a timeout) the call is the reference's own.
 %%--------------------------------------------------------------------
 -module(emqx_trie_gpu).
 
 -include_lib("emqx/include/emqx.hrl").
 
--export([start_link/0, child_specs/0, enabled/0, handle/0]).
--export([match/1, match_trie/1, match_routes/1, empty/0]).
+-export([child_specs/0, enabled/0, handle/1, publish/2]).
+-export([match/1, match_session/1, match_trie/1, match_routes/1, empty/0, empty_session/0]).
 
--define(HANDLE_KEY, {?MODULE, handle}).
+-define(KEY(Index), {?MODULE, Index}).
+-define(CONF(K, D), emqx_config:get([broker, perf, gpu_match, K], D)).
 
-enabled() ->
-    emqx_config:get([broker, perf, gpu_match, enable], false) andalso
-        persistent_term:get(?HANDLE_KEY, undefined) =/= undefined.
-
-handle() ->
-    persistent_term:get(?HANDLE_KEY).
-
-%% opens the device index (broker.perf.gpu_match) and publishes its handle
-start_link() ->
-    Conf = emqx_config:get([broker, perf, gpu_match]),
-    #{devices := [Device | _], batch_max := Max, batch_window_us := Us} = Conf,
-    case emqx_trie_gpu_nif:open(Device, Max, 64 * Max, Us) of
-        {ok, H} ->
-            persistent_term:put(?HANDLE_KEY, H),
-            ignore;
-        {error, Reason} ->
-            {error, {gpu_match_open, Reason}}
-    end.
-
+%% the supervisor's children (a maintainer adds them to emqx_broker_sup, INTEGRATION.md 4): one
+%% mirror per index; each opens its engines in init/1
+-spec child_specs() -> [supervisor:child_spec()].
 child_specs() ->
+    Indexes =
+        case emqx_persistent_session:is_store_enabled() of
+            true -> [route, session];
+            false -> [route]
+        end,
     [
-        #{id => emqx_trie_gpu, start => {?MODULE, start_link, []}, restart => transient},
         #{
-            id => emqx_trie_gpu_batcher,
-            start => {emqx_trie_gpu_batcher, start_link, [handle()]},
+            id => {emqx_trie_gpu_sync, I},
+            start => {emqx_trie_gpu_sync, start_link, [I]},
             restart => permanent
-        },
-        #{id => emqx_trie_gpu_sync, start => {emqx_trie_gpu_sync, start_link, [handle()]}}
+        }
+     || I <- Indexes
     ].
 
-%% emqx_trie:match/1: the wildcard filters of the trie matching Topic (a set; [] for a
-%% wildcard topic name, emqx_trie.erl:157-166).  Topics deeper than max_levels (the zone's
-%% mqtt.max_topic_levels, emqx_mqtt_caps.erl:94-97, bypassed by internal publishes) take the
-%% reference's path.
+%% the published engines of index route | session, or undefined (not synced yet)
+handle(Index) ->
+    persistent_term:get(?KEY(Index), undefined).
+
+%% called by emqx_trie_gpu_sync once the index's first full sync is committed
+publish(Index, H) ->
+    persistent_term:put(?KEY(Index), H).
+
+enabled() ->
+    device(route) =/= undefined.
+
+device(Index) ->
+    case ?CONF(enable, false) of
+        true -> handle(Index);
+        false -> undefined
+    end.
+
+%% emqx_trie:match/1: the wildcard filters of the trie matching Topic (a set; [] for a wildcard
+%% topic name, emqx_trie.erl:157-166 -- the device applies that rule itself)
 -spec match(emqx_types:topic()) -> [emqx_types:topic()].
 match(Topic) when is_binary(Topic) ->
-    case enabled() of
-        false ->
-            emqx_trie:match(Topic);
-        true ->
-            Words = emqx_topic:words(Topic),
-            case emqx_topic:wildcard(Words) of
-                true ->
-                    [];
-                false ->
-                    case length(Words) > emqx_config:get([broker, perf, gpu_match, max_levels]) of
-                        true -> emqx_trie:match(Topic);
-                        false -> emqx_trie_gpu_batcher:match(Topic)
-                    end
-            end
+    match(route, Topic).
+
+%% emqx_trie:match_session/1 (emqx_session_router:match_trie/1, emqx_session_router.erl:154-159)
+-spec match_session(emqx_types:topic()) -> [emqx_types:topic()].
+match_session(Topic) when is_binary(Topic) ->
+    match(session, Topic).
+
+match(Index, Topic) ->
+    case device(Index) of
+        undefined -> ref_match(Index, Topic);
+        H -> device_match(Index, H, Topic)
+    end.
+
+ref_match(route, Topic) -> emqx_trie:match(Topic);
+ref_match(session, Topic) -> emqx_trie:match_session(Topic).
+
+device_match(Index, H, Topic) ->
+    Id = erlang:unique_integer([positive]),
+    case emqx_trie_gpu_nif:match_async(H, Topic, Id) of
+        ok ->
+            receive
+                {emqx_trie_gpu, Id, Filters} when is_list(Filters) -> Filters;
+                {emqx_trie_gpu, Id, {error, _}} -> ref_match(Index, Topic)
+            after ?CONF(timeout_ms, 5000) ->
+                case emqx_trie_gpu_nif:cancel(H, Id) of
+                    true ->
+                        ref_match(Index, Topic);
+                    false ->
+                        %% reported while we gave up: the answer is in the mailbox already
+                        receive
+                            {emqx_trie_gpu, Id, Filters} when is_list(Filters) -> Filters;
+                            {emqx_trie_gpu, Id, _} -> ref_match(Index, Topic)
+                        after 0 -> ref_match(Index, Topic)
+                        end
+                end
+            end;
+        {error, _} ->
+            %% deeper than max_levels, every window busy, or shutting down
+            ref_match(Index, Topic)
     end.
 
 %% emqx_router:match_trie/1
@@ -87,9 +124,15 @@ match_routes(Topic) when is_binary(Topic) ->
         Matched -> lists:append([emqx_router:lookup_routes(To) || To <- [Topic | Matched]])
     end.
 
-%% emqx_trie:empty/0 of the committed device index
+%% emqx_trie:empty/0, empty_session/0 of the committed device index
 empty() ->
-    case enabled() of
-        false -> emqx_trie:empty();
-        true -> emqx_trie_gpu_nif:empty(handle())
+    case device(route) of
+        undefined -> emqx_trie:empty();
+        H -> emqx_trie_gpu_nif:empty(H)
+    end.
+
+empty_session() ->
+    case device(session) of
+        undefined -> emqx_trie:empty_session();
+        H -> emqx_trie_gpu_nif:empty(H)
     end.

@@ -5,18 +5,18 @@
 -module(emqx_trie_gpu_nif).
 
 -export([
-    open/4,
-    trie_insert/2,
-    trie_delete/2,
-    route_ref/2,
-    route_unref/2,
+    open/5,
+    route_set/3,
+    sync_begin/1,
+    sync_end/2,
     commit/1,
     empty/1,
-    add/3,
-    due/1,
-    flush/1,
-    collect/2,
-    tune/3
+    trie_member/2,
+    route_member/2,
+    match_async/3,
+    cancel/2,
+    tune/3,
+    stats/1
 ]).
 
 -on_load(init/0).
@@ -31,20 +31,23 @@ init() ->
 
 -define(NOT_LOADED, erlang:nif_error(nif_not_loaded)).
 
-%% open(Device, WindowTopics, WindowBytes, WindowUs) -> {ok, Handle} | {error, Reason}
-open(_Device, _WindowTopics, _WindowBytes, _WindowUs) -> ?NOT_LOADED.
-trie_insert(_H, _Filter) -> ?NOT_LOADED.
-trie_delete(_H, _Filter) -> ?NOT_LOADED.
-route_ref(_H, _Filter) -> ?NOT_LOADED.
-route_unref(_H, _Filter) -> ?NOT_LOADED.
-%% commit(H) -> {ok, Epoch}
-commit(_H) -> ?NOT_LOADED.
-empty(_H) -> ?NOT_LOADED.
-%% add(H, Topic, Tag) -> ok | full | {error, enospc | e2big}
-add(_H, _Topic, _Tag) -> ?NOT_LOADED.
-due(_H) -> ?NOT_LOADED.
-%% flush(H) -> {ok, WindowId} | empty | {error, ebusy}
-flush(_H) -> ?NOT_LOADED.
-%% collect(H, WindowId) -> {ok, [{Tag, [Filter], ExactHit}]}
-collect(_H, _WindowId) -> ?NOT_LOADED.
-tune(_H, _Key, _Value) -> ?NOT_LOADED.
+%% open(Devices, WindowTopics, WindowBytes, WindowUs, MaxLevels) -> {ok, Res} | {error, Reason}
+open(_Devices, _WindowTopics, _WindowBytes, _WindowUs, _MaxLevels) -> ?NOT_LOADED.
+%% route_set(Res, Filter, Present :: boolean()) -> ok | {error, Reason}
+route_set(_Res, _Filter, _Present) -> ?NOT_LOADED.
+%% sync_begin(Res) -> {ok, Gen}
+sync_begin(_Res) -> ?NOT_LOADED.
+%% sync_end(Res, Gen) -> {ok, Removed}
+sync_end(_Res, _Gen) -> ?NOT_LOADED.
+%% commit(Res) -> {ok, Epoch}
+commit(_Res) -> ?NOT_LOADED.
+empty(_Res) -> ?NOT_LOADED.
+trie_member(_Res, _Filter) -> ?NOT_LOADED.
+route_member(_Res, _Filter) -> ?NOT_LOADED.
+%% match_async(Res, Topic, Id) -> ok | {error, e2big | ebusy | eshutdown}; later the caller gets
+%% {emqx_trie_gpu, Id, [Filter] | {error, Reason}}
+match_async(_Res, _Topic, _Id) -> ?NOT_LOADED.
+%% cancel(Res, Id) -> true (never answered) | false (the answer is in the mailbox)
+cancel(_Res, _Id) -> ?NOT_LOADED.
+tune(_Res, _Key, _Value) -> ?NOT_LOADED.
+stats(_Res) -> ?NOT_LOADED.

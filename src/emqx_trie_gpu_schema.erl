@@ -4,14 +4,19 @@
 %% {"gpu_match", sc(ref(emqx_trie_gpu_schema, "gpu_match"), #{})} to fields("broker_perf").
 %%
 %% How each field reaches the engine (include/emqx_gpumatch.h):
-%%   enable          -> whether emqx_trie_gpu answers emqx_trie:match/1 at all
-%%   devices         -> emqxgm_cfg.device (the first; one index per node)
-%%   batch_max       -> emqxgm_batcher_cfg.window_topics = emqxgm_cfg.batch_max
-%%                      (window_bytes = 64 x batch_max)
-%%   batch_window_us -> emqxgm_batcher_cfg.window_us
-%%   max_levels      -> topics deeper than this take emqx_trie:match/1 (the zone's
-%%                      mqtt.max_topic_levels, emqx_schema.erl:405-412, default 128)
-%%   delta_commit    -> emqxgm_tune(h, "delta_commit", V)
+%%   enable              -> whether emqx_trie_gpu answers emqx_trie:match/1 at all
+%%   devices             -> one engine per device (emqxgm_cfg.device), each holding the whole
+%%                          index; windows go round robin to the engines (emqxgm_async_create)
+%%   batch_max           -> emqxgm_async_cfg.window_topics = emqxgm_cfg.batch_max
+%%                          (window_bytes = 64 x batch_max)
+%%   batch_window_us     -> emqxgm_async_cfg.window_us: a window is submitted at most this long
+%%                          after its first topic
+%%   max_levels          -> emqxgm_async_cfg.max_levels: deeper topics take emqx_trie:match/1
+%%                          (the zone's mqtt.max_topic_levels, emqx_schema.erl:405-412)
+%%   delta_commit        -> emqxgm_tune(h, "delta_commit", never 0 | small 1 | always 2)
+%%   timeout_ms          -> how long a publisher waits for the device before it cancels and takes
+%%                          emqx_trie:match/1
+%%   resync_interval_ms  -> period of emqx_trie_gpu_sync's full resync (emqxgm_route_sync_*)
 %% emqx_amd/config.py is the same table for the Python mirror (tests/test_config.py).
 %%--------------------------------------------------------------------
 -module(emqx_trie_gpu_schema).
@@ -29,5 +34,7 @@ fields("gpu_match") ->
             hoconsc:mk(range(1, 4194304), #{default => 65536})},
         {"batch_window_us", hoconsc:mk(range(1, 1000000), #{default => 50})},
         {"max_levels", hoconsc:mk(range(1, 65535), #{default => 128})},
-        {"delta_commit", hoconsc:mk(hoconsc:enum([never, small, always]), #{default => small})}
+        {"delta_commit", hoconsc:mk(hoconsc:enum([never, small, always]), #{default => small})},
+        {"timeout_ms", hoconsc:mk(range(1, 600000), #{default => 5000})},
+        {"resync_interval_ms", hoconsc:mk(range(100, 86400000), #{default => 30000})}
     ].

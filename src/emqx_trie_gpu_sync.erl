@@ -1,38 +1,93 @@
 %%--------------------------------------------------------------------
-%% emqx_trie_gpu_sync -- mirrors the committed route table into the device index.
+%% emqx_trie_gpu_sync -- mirrors one committed route table into its device index.
+%%
+%% Index route   : the route table emqx_route (emqx_router.erl:72-92) -> emqx_trie's trie;
+%% Index session : the session router's table (emqx_session_router.erl:64-65, 312-316) -> the
+%%                 session trie (emqx_trie.erl:117-119, 135-137, 151-153).
 %%
 %% emqx_trie:insert/delete run inside mria transactions that may abort and retry
-%% (emqx_router_utils.erl:74-135), so the device only ever follows committed state: this process
-%% subscribes to the route table's events, as emqx_router_helper does for its own table
-%% (emqx_router_helper.erl:107), and applies the membership rule of emqx_router_utils.erl:34-39,
-%% 57-71 -- a route key exists while its filter has a route, a wildcard filter is in the trie
-%% while it has one.  Changes are committed (one atomic epoch swap) on a short tick; matches
+%% (emqx_router_utils.erl:74-135), so the device follows committed state only.  The mirror is
+%% LEVEL-triggered: whatever event arrives for a topic T, it reads the table as it is now and
+%% sets T's membership to match it (emqxgm_route_set: a route key while T has a route, a trie
+%% member while a wildcard T has one -- the rule of emqx_router_utils.erl:34-39, 57-71).  The
+%% number and order of events therefore never matter: two dests added before the first event is
+%% handled, paired deletes, events queued while init/1 scans the table, a restart -- each ends in
+%% the table's state.  Changes are committed (one atomic epoch swap) on a short tick; matches
 %% never wait for it.
+%%
+%% Full resyncs (init/1, then every resync_interval_ms): sync_begin, every topic of the table set
+%% present, sync_end -- which removes every route key the scan did not see.  Events that arrive
+%% during a scan are handled after it, against the table as it is then, so they win.  The
+%% periodic resync is what keeps a node that never sees the table's mnesia events in step: on a
+%% mria replicant the route shard is replayed from the core nodes' rlog (emqx_router.erl:78-92)
+%% and mnesia table events may not fire there, so such a node lags by at most one interval.
 %%--------------------------------------------------------------------
 -module(emqx_trie_gpu_sync).
 
 -behaviour(gen_server).
 
--include_lib("emqx/include/emqx.hrl").
-
 -export([start_link/1]).
 -export([init/1, handle_call/3, handle_cast/2, handle_info/2]).
 
--define(ROUTE_TAB, emqx_route).
 -define(TICK_MS, 2).
+-define(CONF(K, D), emqx_config:get([broker, perf, gpu_match, K], D)).
 
-start_link(Handle) ->
-    gen_server:start_link({local, ?MODULE}, ?MODULE, Handle, []).
+start_link(Index) ->
+    gen_server:start_link({local, name(Index)}, ?MODULE, Index, []).
 
-init(H) ->
-    {ok, _} = mnesia:subscribe({table, ?ROUTE_TAB, simple}),
-    %% the routes that exist already: one full build
-    lists:foreach(
-        fun(Topic) -> first_route(H, Topic) end,
-        lists:usort([T || #route{topic = T} <- ets:tab2list(?ROUTE_TAB)])
-    ),
-    {ok, _Epoch} = emqx_trie_gpu_nif:commit(H),
-    {ok, #{h => H, dirty => false}}.
+name(route) -> emqx_trie_gpu_sync_route;
+name(session) -> emqx_trie_gpu_sync_session.
+
+%% emqx_session_router:route_tab/0 (emqx_session_router.erl:312-316)
+table(route) ->
+    emqx_route;
+table(session) ->
+    case emqx_persistent_session:storage_type() of
+        disc -> emqx_session_route_disc;
+        ram -> emqx_session_route_ram
+    end.
+
+init(Index) ->
+    Tab = table(Index),
+    case open(Index) of
+        {ok, H} ->
+            {ok, _} = mnesia:subscribe({table, Tab, simple}),
+            ok = tune(H),
+            S = #{index => Index, h => H, tab => Tab, dirty => false},
+            ok = resync(S),
+            {ok, _Epoch} = emqx_trie_gpu_nif:commit(H),
+            %% only now may publishers use it (before, they take the reference's path)
+            emqx_trie_gpu:publish(Index, H),
+            schedule_resync(),
+            {ok, S};
+        {error, Reason} ->
+            {stop, {gpu_match_open, Reason}}
+    end.
+
+%% a restart keeps the engines (and their index) it published: the resync repairs whatever
+%% changed meanwhile
+open(Index) ->
+    case emqx_trie_gpu:handle(Index) of
+        undefined ->
+            emqx_trie_gpu_nif:open(
+                ?CONF(devices, [0]),
+                ?CONF(batch_max, 65536),
+                64 * ?CONF(batch_max, 65536),
+                ?CONF(batch_window_us, 50),
+                ?CONF(max_levels, 128)
+            );
+        H ->
+            {ok, H}
+    end.
+
+tune(H) ->
+    Delta =
+        case ?CONF(delta_commit, small) of
+            never -> 0;
+            small -> 1;
+            always -> 2
+        end,
+    emqx_trie_gpu_nif:tune(H, delta_commit, Delta).
 
 handle_call(_Req, _From, S) ->
     {reply, ignored, S}.
@@ -40,36 +95,46 @@ handle_call(_Req, _From, S) ->
 handle_cast(_Msg, S) ->
     {noreply, S}.
 
-handle_info({mnesia_table_event, {write, #route{topic = T}, _}}, S = #{h := H}) ->
-    case emqx_router:lookup_routes(T) of
-        [_] -> first_route(H, T);
-        _ -> ok
-    end,
-    {noreply, tick(S)};
-handle_info({mnesia_table_event, {delete_object, #route{topic = T}, _}}, S = #{h := H}) ->
-    case emqx_router:lookup_routes(T) of
-        [] -> last_route(H, T);
-        _ -> ok
-    end,
-    {noreply, tick(S)};
-handle_info({mnesia_table_event, {delete, {?ROUTE_TAB, T}, _}}, S = #{h := H}) ->
-    last_route(H, T),
-    {noreply, tick(S)};
+%% simple table events: the record's first field is the topic, whatever its tag
+handle_info({mnesia_table_event, {write, Route, _}}, S) ->
+    {noreply, set(element(2, Route), S)};
+handle_info({mnesia_table_event, {delete_object, Route, _}}, S) ->
+    {noreply, set(element(2, Route), S)};
+handle_info({mnesia_table_event, {delete, {_Tab, Topic}, _}}, S) ->
+    {noreply, set(Topic, S)};
 handle_info(commit, S = #{h := H}) ->
     {ok, _Epoch} = emqx_trie_gpu_nif:commit(H),
     {noreply, S#{dirty := false}};
+handle_info(resync, S) ->
+    ok = resync(S),
+    schedule_resync(),
+    {noreply, tick(S)};
 handle_info(_Info, S) ->
     {noreply, S}.
 
-first_route(H, Topic) ->
-    ok = emqx_trie_gpu_nif:route_ref(H, Topic),
-    emqx_topic:wildcard(Topic) andalso (ok = emqx_trie_gpu_nif:trie_insert(H, Topic)),
+%% T's membership := whether the table holds a route for T now
+set(Topic, S = #{h := H, tab := Tab}) ->
+    case emqx_trie_gpu_nif:route_set(H, Topic, ets:member(Tab, Topic)) of
+        ok ->
+            tick(S);
+        {error, _} ->
+            %% the engine refused (out of memory): a full resync retries every key
+            self() ! resync,
+            S
+    end.
+
+resync(#{h := H, tab := Tab}) ->
+    {ok, Gen} = emqx_trie_gpu_nif:sync_begin(H),
+    ets:foldl(
+        fun(Route, ok) -> emqx_trie_gpu_nif:route_set(H, element(2, Route), true) end,
+        ok,
+        Tab
+    ),
+    {ok, _Removed} = emqx_trie_gpu_nif:sync_end(H, Gen),
     ok.
 
-last_route(H, Topic) ->
-    ok = emqx_trie_gpu_nif:route_unref(H, Topic),
-    emqx_topic:wildcard(Topic) andalso (ok = emqx_trie_gpu_nif:trie_delete(H, Topic)),
-    ok.
+schedule_resync() ->
+    erlang:send_after(?CONF(resync_interval_ms, 30000), self(), resync).
 
 tick(S = #{dirty := true}) ->
     S;

@@ -1,0 +1,322 @@
+// async_harness.cpp -- TEST INFRASTRUCTURE: the concurrent publish entry (emqx_amd/csrc/
+// gm_async.cpp) under ThreadSanitizer / AddressSanitizer on the CPU.
+//
+// gm_async.cpp is a layer over four engine entry points (emqxgm_host_alloc / _free,
+// emqxgm_match_batch_submit_filters / _wait_filters).  Here they are a mock engine whose
+// "device pass" is the oracle's C++ restatement of emqx_trie:match/1 + the route-key lookup
+// (oracle/ref_trie.cpp, emqx_trie.erl:282-348, emqx_router.erl:141-146), with the real engine's
+// contract enforced: at most EMQXGM_HOST_PIPES tickets in flight per handle (-EBUSY beyond), a
+// result's buffers valid only until ticket + EMQXGM_HOST_PIPES is submitted (the mock then
+// poisons them, so a layer that reads a released result reports garbage and fails the check),
+// and waits that take a random while.
+//
+// T publisher threads call emqxgm_async_match one topic at a time with a bounded number of
+// calls outstanding each (their "processes"), cancel some of them, and check in the callback:
+// every reported call's filter set and exact hit equal the oracle's for its topic; every accepted
+// call is reported exactly once unless its cancel returned 1, and never after a cancel that
+// returned 1.  Prints "OK <calls> <windows> <cancelled> <busy>".
+#include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/emqx_gpumatch.h"
+
+extern "C" {
+void* ref_create(int compact);
+void ref_destroy(void* h);
+int ref_add_many(void* h, const uint8_t* bytes, const uint64_t* off, uint64_t n, const uint8_t* kind);
+int ref_match_batch(void* h, const uint8_t* tb, const uint32_t* toff, uint64_t n, int threads,
+                    uint64_t* row, uint32_t** ids_out, uint64_t* n_ids, uint32_t* exact);
+void ref_free(void* p);
+}
+
+#define CHECK(c, ...)                                             \
+  do {                                                            \
+    if (!(c)) {                                                   \
+      fprintf(stderr, "FAIL %s:%d: %s: ", __FILE__, __LINE__, #c); \
+      fprintf(stderr, __VA_ARGS__);                               \
+      fprintf(stderr, "\n");                                      \
+      abort();                                                    \
+    }                                                             \
+  } while (0)
+
+namespace {
+
+std::vector<std::string> g_filters;  // oracle ids = registration order
+void* g_ref = nullptr;
+std::mutex g_ref_mu;  // ref_match_batch is a reader, but keep the oracle single-threaded
+
+struct MockPipe {
+  uint64_t ticket = 0;
+  int state = 0;  // 0 free / taken, 1 in flight
+  std::vector<uint32_t> row, fid, exact, foff;
+  std::vector<uint8_t> fb;
+};
+
+}  // namespace
+
+struct emqxgm {
+  std::mutex mu;
+  MockPipe p[EMQXGM_HOST_PIPES];
+  uint64_t next = 1;
+  std::atomic<uint64_t> busy{0};
+};
+
+extern "C" {
+
+void* emqxgm_host_alloc(emqxgm_t*, uint64_t bytes) { return malloc(bytes ? bytes : 1); }
+void emqxgm_host_free(emqxgm_t*, void* p) { free(p); }
+
+int emqxgm_match_batch_submit_filters(emqxgm_t* h, const uint8_t* bytes, const uint32_t* off,
+                                      uint32_t n, uint64_t* ticket) {
+  std::lock_guard<std::mutex> g(h->mu);
+  const uint64_t tk = h->next;
+  MockPipe& p = h->p[tk % EMQXGM_HOST_PIPES];
+  if (p.state == 1) {
+    h->busy++;
+    return -EBUSY;
+  }
+  // the previous result of this pipe is overwritten now: poison it first (a reader of a released
+  // result then sees garbage)
+  std::fill(p.row.begin(), p.row.end(), 0xDEADBEEFu);
+  std::fill(p.fid.begin(), p.fid.end(), 0xDEADBEEFu);
+  std::fill(p.foff.begin(), p.foff.end(), 0xDEADBEEFu);
+  std::fill(p.fb.begin(), p.fb.end(), (uint8_t)0xEE);
+  CHECK(off[0] == 0, "offsets[0]");
+  std::vector<uint64_t> row(n + 1);
+  uint32_t* ids = nullptr;
+  uint64_t nid = 0;
+  p.exact.assign(n, 0);
+  {
+    std::lock_guard<std::mutex> r(g_ref_mu);
+    ref_match_batch(g_ref, bytes, off, n, 1, row.data(), &ids, &nid, p.exact.data());
+  }
+  p.row.assign(row.begin(), row.end());
+  p.fid.assign(ids, ids + nid);
+  ref_free(ids);
+  p.foff.assign(1, 0);
+  p.fb.clear();
+  for (uint32_t id : p.fid) {
+    p.fb.insert(p.fb.end(), g_filters[id].begin(), g_filters[id].end());
+    p.foff.push_back((uint32_t)p.fb.size());
+  }
+  p.ticket = tk;
+  p.state = 1;
+  h->next += 1;
+  *ticket = tk;
+  return 0;
+}
+
+int emqxgm_match_batch_wait_filters(emqxgm_t* h, uint64_t ticket, emqxgm_batch_out* out,
+                                    const uint32_t** foff, const uint8_t** fbytes) {
+  // the "device" takes a while; the layer must not hold its own lock meanwhile
+  thread_local std::mt19937 rng(std::hash<std::thread::id>()(std::this_thread::get_id()));
+  std::this_thread::sleep_for(std::chrono::microseconds(rng() % 300));
+  std::lock_guard<std::mutex> g(h->mu);
+  MockPipe& p = h->p[ticket % EMQXGM_HOST_PIPES];
+  if (ticket == 0 || p.ticket != ticket || p.state != 1) return -ENOENT;
+  p.state = 0;
+  out->n = (uint32_t)p.exact.size();
+  out->n_pairs = (uint32_t)p.fid.size();
+  out->row_ptr = p.row.data();
+  out->filter_id = p.fid.data();
+  out->exact_id = p.exact.data();
+  *foff = p.foff.data();
+  *fbytes = p.fb.data();
+  return 0;
+}
+
+}  // extern "C"
+
+namespace {
+
+// per call: its topic index; reported / cancelled flags
+struct CallState {
+  std::atomic<int> reported{0};
+  std::atomic<int> cancelled{0};
+  uint32_t topic = 0;
+};
+
+std::vector<std::string> g_topics;
+std::vector<std::vector<std::string>> g_want;  // sorted filter strings per topic
+std::vector<uint32_t> g_want_exact;
+std::vector<CallState>* g_calls = nullptr;
+std::atomic<uint64_t> g_reported{0};
+std::atomic<int64_t>* g_outstanding = nullptr;  // per thread
+
+void on_window(void* user, const emqxgm_async_window* w) {
+  (void)user;
+  CHECK(w->status == 0, "window status %d", w->status);
+  for (uint32_t i = 0; i < w->n; ++i) {
+    if (w->tag[i] == EMQXGM_TAG_CANCELLED) continue;
+    CallState& c = (*g_calls)[w->tag[i]];
+    CHECK(c.cancelled.load() == 0, "call %llu reported after a successful cancel",
+          (unsigned long long)w->tag[i]);
+    CHECK(c.reported.fetch_add(1) == 0, "call %llu reported twice", (unsigned long long)w->tag[i]);
+    std::vector<std::string> got;
+    for (uint32_t j = w->row[i]; j < w->row[i + 1]; ++j)
+      got.emplace_back((const char*)w->fbytes + w->foff[j], w->foff[j + 1] - w->foff[j]);
+    std::sort(got.begin(), got.end());
+    CHECK(got == g_want[c.topic], "call %llu topic %u: %zu filters vs %zu",
+          (unsigned long long)w->tag[i], c.topic, got.size(), g_want[c.topic].size());
+    CHECK((w->exact_id[i] == EMQXGM_NONE) == (g_want_exact[c.topic] == EMQXGM_NONE),
+          "exact hit of topic %u", c.topic);
+    g_outstanding[w->owner[i]].fetch_sub(1);
+    g_reported++;
+  }
+}
+
+std::string rand_topic(std::mt19937& rng, bool filter) {
+  static const char* W[] = {"a", "b", "c", "dd", "eeeeeeeee", "", "$s"};
+  const int n = 1 + rng() % 5;
+  std::string t;
+  for (int i = 0; i < n; ++i) {
+    if (i) t += '/';
+    const uint32_t r = rng() % (filter ? 9 : 7);
+    if (filter && r == 7) t += '+';
+    else if (filter && r == 8) {
+      t += '#';
+      break;
+    } else t += W[r == 6 && i ? 0 : r];
+  }
+  return t;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const unsigned seed = argc > 1 ? atoi(argv[1]) : 1;
+  const int threads = argc > 2 ? atoi(argv[2]) : 16;
+  const int handles = argc > 3 ? atoi(argv[3]) : 2;
+  const uint32_t window = argc > 4 ? atoi(argv[4]) : 64;
+  const uint64_t calls_per_thread = argc > 5 ? atoll(argv[5]) : 3000;
+  std::mt19937 rng(seed);
+  // the index: random filters (trie + route keys) and some exact keys
+  std::vector<uint8_t> fb;
+  std::vector<uint64_t> fo{0};
+  std::vector<uint8_t> kind;
+  std::unordered_map<std::string, int> seen;
+  for (int i = 0; i < 400; ++i) {
+    std::string f = rand_topic(rng, true);
+    if (seen.count(f)) continue;
+    seen[f] = 1;
+    const bool wild = f.find('+') != std::string::npos || f.find('#') != std::string::npos;
+    g_filters.push_back(f);
+    fb.insert(fb.end(), f.begin(), f.end());
+    fo.push_back(fb.size());
+    kind.push_back(wild ? 3 : 2);
+  }
+  g_ref = ref_create(1);
+  ref_add_many(g_ref, fb.data(), fo.data(), g_filters.size(), kind.data());
+  for (int i = 0; i < 300; ++i) g_topics.push_back(rand_topic(rng, false));
+  {  // expected answers, one oracle call per topic
+    std::vector<uint8_t> tb;
+    std::vector<uint32_t> to{0};
+    for (auto& t : g_topics) {
+      tb.insert(tb.end(), t.begin(), t.end());
+      to.push_back((uint32_t)tb.size());
+    }
+    std::vector<uint64_t> row(g_topics.size() + 1);
+    uint32_t* ids = nullptr;
+    uint64_t nid = 0;
+    g_want_exact.assign(g_topics.size(), 0);
+    ref_match_batch(g_ref, tb.data(), to.data(), g_topics.size(), 1, row.data(), &ids, &nid,
+                    g_want_exact.data());
+    for (size_t t = 0; t < g_topics.size(); ++t) {
+      std::vector<std::string> v;
+      for (uint64_t j = row[t]; j < row[t + 1]; ++j) v.push_back(g_filters[ids[j]]);
+      std::sort(v.begin(), v.end());
+      g_want.push_back(v);
+    }
+    ref_free(ids);
+  }
+  std::vector<emqxgm> engines(handles);
+  std::vector<emqxgm_t*> hs;
+  for (auto& e : engines) hs.push_back(&e);
+  std::vector<CallState> calls(threads * calls_per_thread);
+  g_calls = &calls;
+  std::vector<std::atomic<int64_t>> outstanding(threads);
+  g_outstanding = outstanding.data();
+  emqxgm_async_cfg cfg{};
+  cfg.window_topics = window;
+  cfg.window_bytes = 64 * window;
+  cfg.window_us = 20 + seed % 100;
+  cfg.max_levels = 4;
+  emqxgm_async_t* a = nullptr;
+  CHECK(emqxgm_async_create(hs.data(), handles, &cfg, on_window, nullptr, &a) == 0, "create");
+  std::atomic<uint64_t> accepted{0}, cancelled{0}, busy{0}, too_deep{0};
+  std::vector<std::thread> th;
+  for (int k = 0; k < threads; ++k) {
+    th.emplace_back([&, k] {
+      std::mt19937 r(seed * 7919 + k);
+      const int64_t procs = 1 + r() % 48;  // this "scheduler"'s publisher processes
+      for (uint64_t i = 0; i < calls_per_thread; ++i) {
+        const uint64_t tag = k * calls_per_thread + i;
+        CallState& c = calls[tag];
+        c.topic = r() % g_topics.size();
+        while (outstanding[k].load() >= procs) std::this_thread::yield();
+        outstanding[k].fetch_add(1);
+        const std::string& t = g_topics[c.topic];
+        const int rc = emqxgm_async_match(a, (const uint8_t*)t.data(), (uint32_t)t.size(), tag, k);
+        if (rc == -EBUSY || rc == -E2BIG) {
+          outstanding[k].fetch_sub(1);
+          c.cancelled.store(2);  // never accepted
+          (rc == -EBUSY ? busy : too_deep)++;
+          if (rc == -E2BIG) {
+            const long levels = std::count(t.begin(), t.end(), '/') + 1;
+            CHECK(levels > 4, "E2BIG for a %ld-level topic", levels);
+          }
+          continue;
+        }
+        CHECK(rc == 0, "async_match %d", rc);
+        accepted++;
+        if (r() % 17 == 0) {  // a caller that gives up at once
+          // mark first: the callback must not report it once the cancel succeeds
+          const int cr = emqxgm_async_cancel(a, tag, k);
+          CHECK(cr == 0 || cr == 1, "cancel %d", cr);
+          if (cr == 1) {
+            c.cancelled.store(1);
+            cancelled++;
+            outstanding[k].fetch_sub(1);
+          } else {
+            CHECK(c.reported.load() == 1, "cancel returned 0 but call %llu not reported",
+                  (unsigned long long)tag);
+          }
+        }
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  emqxgm_async_destroy(a);  // reports every accepted call
+  uint64_t never = 0;
+  for (auto& c : calls) {
+    if (c.cancelled.load() == 2) continue;
+    if (c.cancelled.load() == 1) {
+      CHECK(c.reported.load() == 0, "cancelled call reported");
+      continue;
+    }
+    if (c.reported.load() != 1) ++never;
+  }
+  CHECK(never == 0, "%llu accepted calls never reported", (unsigned long long)never);
+  CHECK(g_reported.load() + cancelled.load() == accepted.load(), "report count");
+  uint64_t eb = 0;
+  for (auto& e : engines) eb += e.busy.load();
+  CHECK(eb == 0, "the layer overran a handle's pipes (%llu -EBUSY)", (unsigned long long)eb);
+  ref_destroy(g_ref);
+  printf("OK %llu %llu %llu %llu %llu\n", (unsigned long long)accepted.load(),
+         (unsigned long long)g_reported.load(), (unsigned long long)cancelled.load(),
+         (unsigned long long)busy.load(), (unsigned long long)too_deep.load());
+  return 0;
+}

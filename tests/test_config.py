@@ -8,20 +8,22 @@ from emqx_amd.config import GpuMatchConfig
 def test_defaults_map_onto_the_engine():
     c = GpuMatchConfig.from_map({})
     assert not c.enable and c.devices == [0] and c.max_levels == 128
-    assert c.engine_kwargs() == {"device": 0, "batch_max": 65536}
-    assert c.batcher_kwargs() == {"window_topics": 65536, "window_bytes": 64 * 65536,
-                                  "window_us": 50}
+    assert c.engine_kwargs() == [{"device": 0, "batch_max": 65536}]
+    assert c.async_kwargs() == {"window_topics": 65536, "window_bytes": 64 * 65536,
+                                "window_us": 50, "max_levels": 128}
+    assert c.timeout_ms == 5000 and c.resync_interval_ms == 30000
     assert c.tunes() == {"delta_commit": 1}
 
 
 def test_values_and_ranges():
     c = GpuMatchConfig.from_map({"enable": True, "devices": [3, 1], "batch_max": 16384,
                                  "batch_window_us": 200, "delta_commit": "always"})
-    assert c.engine_kwargs() == {"device": 3, "batch_max": 16384}
-    assert c.batcher_kwargs()["window_us"] == 200 and c.tunes()["delta_commit"] == 2
+    assert c.engine_kwargs() == [{"device": 3, "batch_max": 16384}, {"device": 1, "batch_max": 16384}]
+    assert c.async_kwargs()["window_us"] == 200 and c.tunes()["delta_commit"] == 2
     for bad in ({"batch_max": 0}, {"batch_max": 5 << 20}, {"batch_window_us": 0},
                 {"max_levels": 0}, {"devices": []}, {"devices": [-1]}, {"enable": 1},
-                {"delta_commit": "sometimes"}, {"batch_size": 3}, {"batch_max": True}):
+                {"delta_commit": "sometimes"}, {"batch_size": 3}, {"batch_max": True},
+                {"timeout_ms": 0}, {"resync_interval_ms": 10}):
         with pytest.raises(ValueError):
             GpuMatchConfig.from_map(bad)
 

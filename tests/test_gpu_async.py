@@ -1,0 +1,254 @@
+"""The NIF's publish path on the device.
+
+* The level-triggered mirror (src/emqx_trie_gpu_sync.erl, emqx_amd/mirror.py) after the
+  adversarial event orders -- two dests before either event, paired deletes, events queued while
+  init scans, a restart on the same engines -- and random churn: every topic's
+  match_routes over the device's answer (exact route key + trie row, emqx_router.erl:141-146)
+  equals oracle.emqx_ref.Router.match_routes.
+* The concurrent entry (emqxgm_async_*, the NIF's match_async/3): calls from Python one at a
+  time (cancel, max_levels, wildcard names, empty topics), and the C load harness
+  (tests/host_harness/async_load.cpp) with 16 and 64 publisher threads calling one topic at a
+  time: EVERY call's answer (trie filter set, as count + order-independent hash of the filter
+  bytes, and the exact-hit flag) equals the oracle's (oracle/ref_trie.cpp) for its topic -- on
+  cfg1, on a 1M-filter cfg3 slice, and with two engines (replicas) taking windows round robin.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from emqx_amd.mirror import RouteTableMirror
+from oracle import emqx_ref as R
+from oracle.cref import RefIndex
+
+pytestmark = pytest.mark.gpu
+NONE = 0xFFFFFFFF
+
+
+@pytest.fixture(scope="module")
+def emqx():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need the MI355X"
+    import emqx_amd
+    return emqx_amd
+
+
+def _routes_device(eng, rt, topics):
+    """match_routes(T) from the device's answer: routes of the exact key, then of every trie
+    filter (emqx_router.erl:141-146), with the route bag's dests."""
+    res = eng.match(topics)
+    out = []
+    for i, t in enumerate(topics):
+        keys = []
+        if res.exact_id[i] != NONE:
+            keys.append(eng.filter_bytes(int(res.exact_id[i])))
+        keys += [eng.filter_bytes(int(f)) for f in res.row(i)]
+        if not res.row(i).size:  # match_trie [] -> lookup_routes(Topic) only
+            keys = [t] if t in rt.bag else []
+        out.append(sorted((k, str(d)) for k in keys for _, d in rt.lookup_routes(k)))
+    return out
+
+
+def _check_routes(eng, rt, topics):
+    got = _routes_device(eng, rt, topics)
+    for t, g in zip(topics, got):
+        want = sorted((k, str(d)) for k, d in rt.match_routes(t))
+        assert g == want, (t, g, want)
+
+
+def test_mirror_adversarial_orders_match_routes(emqx):
+    eng, rt = emqx.Engine(), R.Router()
+    m = RouteTableMirror([eng], rt)
+    m.init()
+    probe = [b"a/b/c", b"a/x/c", b"x/y", b"x", b"s/1", b"k1", b"k2", b"z/q/z", b"a/+/c"]
+    # two dests before either event
+    for d in ("n1", "n2"):
+        rt.add_route(b"a/+/c", d)
+        m.event("write", b"a/+/c")
+    m.handle_events()
+    m.commit()
+    _check_routes(eng, rt, probe)
+    # paired deletes
+    for d in ("n1", "n2"):
+        rt.add_route(b"x/#", d)
+    m.event("write", b"x/#")
+    m.handle_events()
+    m.commit()
+    for d in ("n1", "n2"):
+        rt.delete_route(b"x/#", d)
+        m.event("delete_object", b"x/#")
+    m.handle_events()
+    m.commit()
+    _check_routes(eng, rt, probe)
+    # events queued while init scans (a second mirror on the same engines = a restart), with
+    # changes nobody handled while "down"
+    for t in (b"s/+", b"k1", b"k2"):
+        rt.add_route(t, "n1")
+    rt.delete_route(b"a/+/c", "n1")
+    m2 = RouteTableMirror([eng], rt)
+    for t in (b"s/+", b"k1"):
+        m2.event("write", t)
+    m2.init()
+    _check_routes(eng, rt, probe)
+    m2.handle_events()
+    m2.commit()
+    rt.add_route(b"z/+/z", "n3")
+    rt.delete_route(b"k1", "n1")
+    m2.event("write", b"z/+/z")
+    m2.event("delete_object", b"k1")
+    m2.handle_events()
+    m2.commit()
+    _check_routes(eng, rt, probe)
+
+
+def test_mirror_random_churn_match_routes(emqx):
+    rng = random.Random(7)
+    engs = [emqx.Engine(), emqx.Engine()]  # the NIF's resource: one engine per GPU
+    rt = R.Router()
+    words = [b"a", b"b", b"c", b"+", b"#", b"", b"longword_x"]
+
+    def topic(filt):
+        n = rng.randint(1, 4)
+        ws = [rng.choice(words if filt else [w for w in words if w not in (b"+", b"#")])
+              for _ in range(n)]
+        if b"#" in ws:
+            ws = ws[:ws.index(b"#") + 1]
+        return b"/".join(ws)
+    m = RouteTableMirror(engs, rt)
+    m.init()
+    probes = list({topic(False) for _ in range(300)}) + [b"$SYS/a", b""]
+    for step in range(400):
+        r = rng.random()
+        if r < 0.55:
+            t = topic(True)
+            d = rng.choice(["n1", "n2", ("g", "n1")])
+            if rng.random() < 0.6:
+                rt.add_route(t, d)
+                m.event("write", t)
+            else:
+                if rt.has_routes(t):
+                    d = rng.choice([x for _, x in rt.lookup_routes(t)])
+                rt.delete_route(t, d)
+                m.event(rng.choice(["delete_object", "delete"]), t)
+        elif r < 0.85:
+            m.handle_events(limit=rng.randint(0, 5))
+        elif r < 0.9:
+            m.resync()
+        else:
+            m.handle_events()
+            m.commit()
+            for e in engs:
+                _check_routes(e, rt, probes)
+    m.handle_events()
+    m.commit()
+    for e in engs:
+        _check_routes(e, rt, probes)
+
+
+def _cfg1(emqx, nf=None, nt=30_000, engines=1):
+    import workloads
+    w = workloads.generate(1, nf, nt)
+    engs = []
+    for _ in range(engines):
+        e = emqx.Engine()
+        e.route_ref_many(w.fbytes, w.foff)
+        wi = np.nonzero(w.fwild)[0]
+        for i in wi:
+            e.trie_insert(w.filter(int(i)))
+        e.commit()
+        engs.append(e)
+    return w, engs
+
+
+def test_async_matcher_calls_one_at_a_time(emqx):
+    w, (eng,) = _cfg1(emqx, nt=20_000)
+    ref = RefIndex(True)
+    ref.add_many(w.fbytes, w.foff, 2 + w.fwild.astype(np.uint8))
+    row, ids, ex = ref.match(w.tbytes, w.toff)
+    flt = [w.filter(i) for i in range(w.nf)]
+    am = emqx.AsyncMatcher([eng], window_topics=4096, window_us=100, max_levels=8)
+    keys = []
+    for i in range(w.nt):
+        assert am.match(w.topic(i), i, owner=1) == 0
+        keys.append((i, 1))
+    # edge calls: a wildcard name (trie [] but its exact key), an empty topic, too deep
+    eng2_topics = [b"l0w1/+", b"", b"a/b/c/d/e/f/g/h/i"]
+    assert am.match(eng2_topics[0], 10**9, owner=2) == 0
+    assert am.match(eng2_topics[1], 10**9 + 1, owner=2) == 0
+    assert am.match(eng2_topics[2], 10**9 + 2, owner=2) == -7  # -E2BIG: 9 levels > 8
+    assert am.wait(keys + [(10**9, 2), (10**9 + 1, 2)], timeout=60)
+    for i in range(w.nt):
+        r = am.results[(i, 1)]
+        assert r.status == 0
+        assert sorted(r.filters) == sorted(flt[j] for j in ids[row[i]:row[i + 1]]), i
+        assert (r.exact_id != NONE) == (ex[i] != NONE), i
+    assert am.results[(10**9, 2)].filters == []
+    pyr = R.Trie()
+    for f in flt:
+        if R.wildcard(f):
+            pyr.insert(f)
+    assert sorted(am.results[(10**9 + 1, 2)].filters) == sorted(pyr.match(b""))
+    # cancel: either never reported (True) or already reported (False), never both
+    outcomes = []
+    for k in range(200):
+        tag = 2 * 10**9 + k
+        assert am.match(w.topic(k), tag, owner=3) == 0
+        outcomes.append((tag, am.cancel(tag, owner=3)))
+    am.close()  # reports every accepted call
+    for tag, cancelled in outcomes:
+        assert ((tag, 3) in am.results) != cancelled, tag
+    st = am.stats()
+    assert st["too_deep"] == 1 and st["failed"] == 0
+
+
+def _oracle_rows(w):
+    from workloads import publishers
+    ref = RefIndex(True)
+    ref.add_many(w.fbytes, w.foff, 2 + w.fwild.astype(np.uint8))
+    row, ids, ex = ref.match(w.tbytes, w.toff, threads=8)
+    fh = publishers.string_hashes(w.fbytes, w.foff)
+    return np.diff(row).astype(np.uint32), publishers.row_hashes(row, ids, fh), ex != NONE
+
+
+def _check_load(r, want):
+    cnt, hsh, exact = want
+    t = r["topic"]
+    assert r["calls"] == len(t) and r["failed"] == 0
+    bad = np.nonzero((r["count"] != cnt[t]) | (r["hash"] != hsh[t]) |
+                     (r["exact"].astype(bool) != exact[t]))[0]
+    assert bad.size == 0, (bad[:10], t[bad[:10]])
+
+
+@pytest.mark.parametrize("threads,window", [(16, 4096), (64, 16384)])
+def test_async_load_cfg1_every_call(emqx, threads, window):
+    from workloads import publishers
+    w, (eng,) = _cfg1(emqx, nt=100_000)
+    want = _oracle_rows(w)
+    procs = max(1, window * 4 // threads)
+    r = publishers.run([eng], w.tbytes, w.toff.astype(np.uint64), threads, procs,
+                       max(2 * procs, 300_000 // threads), window, record=True)
+    _check_load(r, want)
+    assert r["windows"] > 0 and r["calls_per_window"] > 1
+
+
+def test_async_load_two_replicas(emqx):
+    from workloads import publishers
+    w, engs = _cfg1(emqx, nt=50_000, engines=2)
+    want = _oracle_rows(w)
+    r = publishers.run(engs, w.tbytes, w.toff.astype(np.uint64), 16, 512, 10_000, 2048,
+                       record=True)
+    _check_load(r, want)
+
+
+def test_async_load_cfg3_slice_every_call(emqx):
+    import workloads
+    from workloads import publishers
+    w = workloads.generate(3, 1_000_000, 200_000)
+    eng = emqx.Engine()
+    eng.route_ref_many(w.fbytes, w.foff)
+    eng.trie_insert_many(w.fbytes, w.foff)  # every cfg3 filter is a wildcard
+    eng.commit()
+    want = _oracle_rows(w)
+    r = publishers.run([eng], w.tbytes, w.toff.astype(np.uint64), 64, 4096, 6_000, 65536,
+                       record=True)
+    _check_load(r, want)

@@ -137,7 +137,9 @@ def test_batcher_protocol_edges(emqx):
     assert sorted(w0.filters(2)) == [b"#"] and w0.exact_id[2] == emqx.NONE
     assert w0.latency_ns > 0
     assert b.collect(ws[0]).tag.tolist() == [7, 8, 8, 8]  # collected results stay readable
-    ws.append(b.flush())
+    ws.append(b.flush())  # reopens ws[0]'s slot as the open window
+    with pytest.raises(emqx.EngineError, match="ENOENT"):
+        b.collect(ws[0])  # its id no longer names a result (it used to read in place)
     for wid in ws[1:]:
         assert len(b.collect(wid).tag) == 1
     with pytest.raises(emqx.EngineError, match="ENOENT"):

@@ -1,0 +1,139 @@
+#!/bin/bash
+# The one GPU-box job runner (replaces r01-r03's one-off lease scripts).  Runs its steps in
+# order, each under its own time limit, and stops at the first failure.  Output under
+# gpurun_out/TAG/.
+#
+#   tools/job.sh TAG STEP [STEP ...]
+#
+# steps:
+#   tests[=PYTEST_ARGS]     python -m pytest tests -m gpu (default: the whole GPU suite)
+#   smoke                   __graft_entry__.smoke()
+#   bench=CFG[:TOPICS[:ARGS]]  bench.py --cfg CFG (default bench line, or --topics TOPICS);
+#                           ARGS: extra bench arguments, commas for spaces
+#   onepass=CFG             rocprofv3 --kernel-trace --stats over bench.py --no-pipeline (the
+#                           roofline's kernel time: one pass at a time)
+#   prof=CFG                rocprofv3 kernel stats + the PMC passes (one counter group per
+#                           run: FETCH_SIZE; WRITE_SIZE + L2 hit/miss; TCP->TCC requests), then
+#                           tools/pmc_summary.py
+#   sq=CFG[:TOPICS]         PMC issue counters of k_walk (SQ_* groups)
+#   ab=SPECS/VARIANTS       A/B of engine builds build/lib_<V>.so (tools/ab_build.sh) against
+#                           the in-tree one, base first and last; SPECS "cfg:topics,..." (0 =
+#                           default topics), VARIANTS "v1,v2"
+#   load=CFG[:FILTERS]      the concurrent publish entry's load (bench.py --only-nif)
+#   dist[=filters]          bench.py's N=2 path with two ranks sharing this box's one GPU over
+#                           gloo (RCCL refuses two ranks on one device): the control flow at full
+#                           size, not a timing; "filters" makes the filter-sharded layout the
+#                           headline
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+TAG=${1:?usage: tools/job.sh TAG STEP...}
+shift
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+KRE="k_walk|k_tok|k_exact|k_scatter|k_verify|k_scan"
+NOCPU="--no-cpu-baseline --no-e2e"
+
+step_tests() {
+  local args=${1:-tests -m gpu}
+  (cd $R && timeout -k 10 1000 python -u -m pytest $args -x -v --timeout 300 --timeout-method thread) \
+    > $O/pytest.log 2>&1
+  local rc=$?
+  tail -3 $O/pytest.log
+  return $rc
+}
+
+step_smoke() {
+  (cd $R && timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()') > $O/smoke.log 2>&1
+}
+
+step_bench() {
+  local cfg=${1%%:*} rest= topics= extra=
+  [ "$1" != "$cfg" ] && rest=${1#*:}
+  topics=${rest%%:*}
+  [ "$rest" != "$topics" ] && extra=${rest#*:}
+  local T=""; [ -n "$topics" ] && [ "$topics" != 0 ] && T="--topics $topics"
+  local name=bench_c${cfg}_${topics:-0}
+  (cd $R && timeout -k 10 900 python -u bench.py --cfg $cfg $T ${extra//,/ }) > $O/$name.json 2> $O/$name.log
+}
+
+step_onepass() {
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/onepass_c$1 -o run --output-format csv \
+    -- python3 $R/bench.py --cfg $1 --no-pipeline $NOCPU --steps 20 --warmup 3 \
+    > $O/onepass_c$1.json 2> $O/onepass_c$1.log
+}
+
+step_prof() {
+  local c=$1 steps=5
+  [ $c = 3 ] && steps=10
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/stats_cfg$c -o run --output-format csv \
+    -- python3 $R/bench.py --cfg $c $NOCPU --steps $steps --warmup 2 \
+    > $O/stats_cfg$c.json 2> $O/stats_cfg$c.log || return 1
+  local i=0 grp
+  for grp in "FETCH_SIZE" "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" \
+             "TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TOTAL_CACHE_ACCESSES_sum"; do
+    i=$((i+1))
+    timeout -s KILL 400 rocprofv3 --pmc $grp --kernel-include-regex "$KRE" -d $O/pmc_cfg$c/p$i -o run \
+      --output-format csv -- python3 $R/bench.py --cfg $c $NOCPU --steps 3 --warmup 1 \
+      > $O/pmc_cfg${c}_p$i.log 2>&1 || return 1
+  done
+  python3 $R/tools/pmc_summary.py $O/pmc_cfg$c > $O/pmc_cfg${c}_summary.txt 2>&1
+}
+
+step_sq() {
+  local c=${1%%:*} topics=
+  [ "$1" != "$c" ] && topics="--topics ${1#*:}"
+  local i=0 grp
+  for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU" \
+             "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE"; do
+    i=$((i+1))
+    timeout -s KILL 300 rocprofv3 --pmc $grp --kernel-include-regex "k_walk" -d $O/sq_cfg$c/p$i -o run \
+      --output-format csv -- python3 $R/bench.py --cfg $c $topics $NOCPU --steps 3 --warmup 1 \
+      > $O/sq_cfg${c}_p$i.log 2>&1 || return 1
+  done
+  python3 $R/tools/pmc_summary.py $O/sq_cfg$c > $O/sq_cfg${c}_summary.txt 2>&1
+}
+
+step_ab() {
+  local specs=${1%%/*} variants=${1#*/} V spec
+  cp $R/emqx_amd/libemqx_gpumatch.so $R/build/lib_base.so || return 1
+  for V in base ${variants//,/ } base; do
+    cp $R/build/lib_$V.so $R/emqx_amd/libemqx_gpumatch.so || return 1
+    for spec in ${specs//,/ }; do
+      local c=${spec%%:*} t=${spec##*:} T=""
+      [ "$t" != 0 ] && T="--topics $t"
+      (cd $R && timeout -k 10 300 python -u bench.py --cfg $c $T $NOCPU --steps 50 --warmup 5) \
+        > $O/${V}_c${c}_${t}.json 2> $O/${V}_c${c}_${t}.log || { cp $R/build/lib_base.so $R/emqx_amd/libemqx_gpumatch.so; return 1; }
+    done
+  done
+  cp $R/build/lib_base.so $R/emqx_amd/libemqx_gpumatch.so
+  python3 $R/tools/ab_lib_summary.py $O > $O/ab_summary.txt 2>&1
+}
+
+step_load() {
+  local c=${1%%:*} f=
+  [ "$1" != "$c" ] && f="--filters ${1#*:}"
+  (cd $R && timeout -k 10 600 python -u bench.py --cfg $c $f --only-nif) > $O/load_c$c.json 2> $O/load_c$c.log
+}
+
+step_dist() {
+  local extra=""
+  [ "$1" = filters ] && extra="--shard filters"
+  (cd $R && EMQXGM_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
+    --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 $extra \
+    --steps 5 --warmup 1) > $O/dist_n2${1:+_$1}.json 2> $O/dist_n2${1:+_$1}.log
+}
+
+for s in "$@"; do
+  name=${s%%=*}
+  arg=
+  [ "$s" != "$name" ] && arg=${s#*=}
+  echo "[job] $name $arg"
+  step_$name "$arg"
+  rc=$?
+  if [ $rc != 0 ]; then
+    echo "[job] step $s failed: $rc"
+    exit $rc
+  fi
+done
+echo "[job] done"
