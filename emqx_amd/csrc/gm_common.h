@@ -144,6 +144,18 @@ constexpr uint32_t LIST_MULTI = 0x80000000u;  // tw/tn value is a multi[] index
 GM_HD uint64_t edge_slot(uint32_t parent, uint64_t tok, uint64_t mask) {
   return fmix64(tok ^ ((uint64_t)parent * 0x9e3779b97f4a7c15ull)) & mask;
 }
+// Token-keyed parents.  The home bucket of a child edge (P, t) is edge_slot(P, t) -- or, when P
+// is KEYED and t a literal word (not '+'), a hash of t alone, so the edges of the parents that share a child token share a
+// line: on cfg3 site/S/device/D and site/+/device/D (D a global device id, one site's) sit in
+// one bucket, and the walk's second probe of D is an L1/L2 hit instead of an HBM miss (r04).
+// A full build keys the parents with many literal children whose every child token is the child
+// of at most EBUCKET keyed parents (tune "keyed"); a node reached by a '+' edge or the root is
+// never keyed (the walk creates those states without their slot).  The flag travels in the
+// parent's slot as an impossible signature: CF_LIT with sig 0 (every literal child of an
+// unkeyed node sets its class bit), so a keyed node's children are never filtered by class.
+GM_HD uint64_t edge_home(uint32_t parent, uint64_t tok, uint64_t mask, bool keyed) {
+  return keyed ? (fmix64(tok + 0x5851f42d4c957f2dull) & mask) : edge_slot(parent, tok, mask);
+}
 // Exact route-key table: 64-B buckets (one line) of XBUCKET 32-B entries, filled in order
 // (linear probing over buckets); exact_slot gives the home bucket.  An entry carries the key's
 // first XINL bytes, so a probe for a key of up to XINL bytes is decided by the one line it loads

@@ -253,6 +253,7 @@ struct TrieModel {
   // node is such a child
   std::vector<uint32_t> fchild;
   std::vector<uint8_t> half;
+  std::vector<uint8_t> keyed;  // the node's children are placed by token (gm_common.h edge_home)
   std::vector<uint64_t> occ, tomb;  // bitmaps over edge slots: used (live or TOMB), TOMB
   uint64_t nbk = 0, ecap = 0, n_occ = 0, n_edges = 0, tn_cap = 0, fv_cap = 0;
   std::vector<uint32_t> fvbits;
@@ -291,7 +292,8 @@ struct TrieModel {
   void node_slot(uint32_t c, uint4* sl) const {  // the 2 x uint4 of c's incoming edge
     const uint32_t p = pchild[c];
     sl[0] = make_uint4((uint32_t)tok[c], (uint32_t)(tok[c] >> 32),
-                       (half[c] ? FAT_ID : parent[c]) | ((uint32_t)sig[c] << SIG_SHIFT), cf(c));
+                       (half[c] ? FAT_ID : parent[c]) | ((keyed[c] ? 0u : (uint32_t)sig[c]) << SIG_SHIFT),
+                       cf(c));
     sl[1] = make_uint4(hfd(c), tw[c], p ? pcf(p) : 0u, p ? phf(p) : NONE);
   }
   // the carried copy of '+' child p (gm_common.h CF_PTW): its '#' filter, or -- when it has
@@ -314,7 +316,13 @@ struct TrieModel {
     slot.push_back(DEAD);
     fchild.push_back(0);
     half.push_back(0);
+    keyed.push_back(0);
     return c;
+  }
+  // home bucket of the edge (par, t): a keyed parent's literal children by token, its '+' child
+  // (probed by IT_PLUS items, never keyed) like every other edge
+  uint64_t home(uint32_t par, uint64_t t) const {
+    return edge_home(par, t, nbk - 1, keyed[par] != 0 && t != PLUS_TOK);
   }
   // the root's fat half as the walk's arguments carry it (rh0.z = NONE: none)
   void root_half(DevIndex& x) const {
@@ -509,6 +517,7 @@ struct emqxgm {
   hipEvent_t patch_ev = nullptr;    // the last patch upload + launch
   uint32_t delta_mode = 1;        // 0: always rebuild, 1: delta when small, 2: delta if possible
   uint32_t fat_mode = 1;          // 1: fat buckets at full builds (gm_common.h FAT_ID), 0: none
+  uint32_t keyed_mode = 1;        // token-keyed parents at full builds (select_keyed): 0 / 1 / 2
   bool roctx = false;             // roctx ranges / launch markers (gm_roctx.h)
 };
 
@@ -934,6 +943,46 @@ int upload_model(emqxgm* h, TrieModel& m) {
   return 0;
 }
 
+// Token-keyed parents (gm_common.h edge_home) of a full build.  mode 1: parents with at least
+// KEYED_MIN_FANOUT literal children, every child token of which is the child of at most
+// EBUCKET such parents (their edges then share one bucket per token); mode 2 (tests): every
+// eligible parent; 0: none.  Never the root or a node reached by a '+' edge.
+constexpr uint32_t KEYED_MIN_FANOUT = 16;
+void select_keyed(TrieModel& m, uint32_t mode) {
+  const size_t nn = m.parent.size();
+  m.keyed.assign(nn, 0u);
+  if (mode == 0) return;
+  auto eligible = [&](uint32_t x) {
+    return x != 0 && m.tok[x] != PLUS_TOK && m.nlit[x] > 0 &&
+           (mode == 2 || m.nlit[x] >= KEYED_MIN_FANOUT);
+  };
+  if (mode == 2) {
+    for (uint32_t x = 1; x < nn; ++x) m.keyed[x] = eligible(x) ? 1 : 0;
+    return;
+  }
+  // child tokens of the candidates, counted by sorting
+  std::vector<uint64_t> toks;
+  for (uint32_t c = 1; c < nn; ++c)
+    if (m.tok[c] != PLUS_TOK && eligible(m.parent[c])) toks.push_back(m.tok[c]);
+  if (toks.empty()) return;
+  std::sort(toks.begin(), toks.end());
+  std::vector<uint64_t> crowded;  // tokens under more than EBUCKET candidates
+  for (size_t i = 0; i < toks.size();) {
+    size_t j = i;
+    while (j < toks.size() && toks[j] == toks[i]) ++j;
+    if (j - i > EBUCKET) crowded.push_back(toks[i]);
+    i = j;
+  }
+  std::vector<uint8_t> ok(nn, 0);
+  for (uint32_t x = 1; x < nn; ++x) ok[x] = eligible(x) ? 1 : 0;
+  for (uint32_t c = 1; c < nn; ++c) {
+    const uint32_t p = m.parent[c];
+    if (ok[p] && m.tok[c] != PLUS_TOK && std::binary_search(crowded.begin(), crowded.end(), m.tok[c]))
+      ok[p] = 0;
+  }
+  for (uint32_t x = 1; x < nn; ++x) m.keyed[x] = ok[x];
+}
+
 // Full build of the device index from the pending registry; swaps it in and rebuilds the host
 // model (TrieModel) that later delta commits patch.
 int commit_full(emqxgm* h) {
@@ -1038,6 +1087,7 @@ int commit_full(emqxgm* h) {
   // that still has a free slot (r03 A/B: TOMBing passed buckets lengthened cfg2's miss chains).
   m.fchild.assign(n_nodes, 0u);
   m.half.assign(n_nodes, 0u);
+  select_keyed(m, h->keyed_mode);
   if (h->fat_mode) {
     std::vector<uint8_t> depth(n_nodes, 0);
     std::vector<uint32_t> lit(n_nodes, 0);
@@ -1054,7 +1104,7 @@ int commit_full(emqxgm* h) {
   }
   for (uint32_t c = 1; c < n_nodes; ++c) {
     if (!m.fchild[c]) continue;
-    const uint64_t q = edge_slot(m.parent[c], m.tok[c], m.nbk - 1) * EBUCKET;
+    const uint64_t q = m.home(m.parent[c], m.tok[c]) * EBUCKET;
     if (bit(m.occ, q) || bit(m.occ, q + 1)) {  // home bucket taken: thin
       m.half[m.fchild[c]] = 0;
       m.fchild[c] = 0;
@@ -1066,22 +1116,25 @@ int commit_full(emqxgm* h) {
     m.slot[m.fchild[c]] = q + 1;
   }
   if (m.fchild[0]) m.slot[m.fchild[0]] = ROOTH;
-  for (uint32_t c = 1; c < n_nodes; ++c) {
-    if (m.fchild[c] || m.half[c]) continue;
-    uint64_t b = edge_slot(m.parent[c], m.tok[c], m.nbk - 1), i;
-    for (;;) {
-      uint32_t j = 0;
-      while (j < EBUCKET && bit(m.occ, b * EBUCKET + j) && !bit(m.tomb, b * EBUCKET + j)) ++j;
-      if (j < EBUCKET) {
-        i = b * EBUCKET + j;
-        break;
+  // the children of keyed parents before the other thin edges, so that the edges sharing a token
+  // find their home bucket free and share its line
+  for (int pass = 0; pass < 2; ++pass)
+    for (uint32_t c = 1; c < n_nodes; ++c) {
+      if (m.fchild[c] || m.half[c] || (m.keyed[m.parent[c]] != 0) != (pass == 0)) continue;
+      uint64_t b = m.home(m.parent[c], m.tok[c]), i;
+      for (;;) {
+        uint32_t j = 0;
+        while (j < EBUCKET && bit(m.occ, b * EBUCKET + j) && !bit(m.tomb, b * EBUCKET + j)) ++j;
+        if (j < EBUCKET) {
+          i = b * EBUCKET + j;
+          break;
+        }
+        b = (b + 1) & (m.nbk - 1);
       }
-      b = (b + 1) & (m.nbk - 1);
+      bset(m.occ, i);
+      bclr(m.tomb, i);
+      m.slot[c] = i;
     }
-    bset(m.occ, i);
-    bclr(m.tomb, i);
-    m.slot[c] = i;
-  }
   m.n_occ = 0;
   for (uint64_t w : m.occ) m.n_occ += (uint64_t)__builtin_popcountll(w);
   // node side array with headroom for delta-commit growth
@@ -1217,7 +1270,7 @@ int commit_delta(emqxgm* h) {
 
   // ---- trie inserts: new nodes take the first free or TOMB slot of their bucket chain ----
   auto alloc_slot = [&](uint32_t par, uint64_t tok) {
-    uint64_t b = edge_slot(par, tok, m.nbk - 1), i = DEAD;
+    uint64_t b = m.home(par, tok), i = DEAD;
     while (i == DEAD) {
       for (uint32_t j = 0; j < EBUCKET && i == DEAD; ++j) {
         const uint64_t q = b * EBUCKET + j;
@@ -2527,7 +2580,7 @@ int emqxgm_commit(emqxgm_t* h, uint64_t* epoch) {
 namespace {
 
 constexpr uint64_t SNAP_MAGIC = 0x31534d47584d45ull;  // "EMXGMS1"
-constexpr uint32_t SNAP_VERSION = 3;  // 2: fat buckets (TrieModel fchild / half), 3: Filter::sync_gen
+constexpr uint32_t SNAP_VERSION = 3;  // 2: fat buckets (TrieModel fchild / half), 3: Filter::sync_gen, keyed
 
 struct SnapOut {
   FILE* f;
@@ -2578,6 +2631,7 @@ void snap_model(IO& io, M& m) {
   io.vec(m.tok);
   io.vec(m.slot);
   io.vec(m.fchild);
+  io.vec(m.keyed);
   io.vec(m.half);
   io.vec(m.occ);
   io.vec(m.tomb);
@@ -2620,7 +2674,7 @@ bool model_consistent(const TrieModel& m, uint64_t n_filters, std::string& why) 
   for (const auto* v : {&m.ref, &m.nlit, &m.pchild, &m.hf, &m.tw, &m.tn})
     if (v->size() != n) return bad("per-node array size");
   if (m.sig.size() != n || m.hcode.size() != n || m.tok.size() != n || m.slot.size() != n ||
-      m.fchild.size() != n || m.half.size() != n)
+      m.fchild.size() != n || m.half.size() != n || m.keyed.size() != n)
     return bad("per-node array size");
   if (!pow2(m.nbk) || m.ecap != m.nbk * EBUCKET || m.ecap > (1ull << 40)) return bad("edge capacity");
   if (m.occ.size() < m.ecap / 64 + 1 || m.tomb.size() < m.ecap / 64 + 1) return bad("edge bitmaps");
@@ -2644,6 +2698,7 @@ bool model_consistent(const TrieModel& m, uint64_t n_filters, std::string& why) 
   for (uint64_t c = 0; c < n; ++c) {
     if (c && m.slot[c] != DEAD && m.slot[c] != ROOTH && m.slot[c] >= m.ecap) return bad("slot position");
     if (m.slot[c] == ROOTH && (!m.half[c] || m.parent[c] != 0)) return bad("root half");
+    if (m.keyed[c] && (c == 0 || m.tok[c] == PLUS_TOK)) return bad("keyed node");
     if (const uint32_t g = m.fchild[c]) {  // the half sits right after its fat parent's slot
       if (g >= n || !m.half[g] || m.parent[g] != c) return bad("fat child");
       if (c ? (m.slot[c] == DEAD || m.slot[c] % EBUCKET != 0 || m.slot[g] != m.slot[c] + 1)
@@ -3544,6 +3599,16 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
   if (strcmp(key, "roctx") == 0) {  // 1: roctx ranges / launch markers (gm_roctx.h)
     if (value < 0 || value > 1) return -EINVAL;
     h->roctx = value != 0;
+    return 0;
+  }
+  if (strcmp(key, "keyed") == 0) {  // token-keyed parents (select_keyed), next full build on
+    if (value < 0 || value > 2) return -EINVAL;
+    std::lock_guard<std::mutex> g(h->wmu);
+    if (h->keyed_mode != (uint32_t)value && !h->filters.empty()) {
+      h->tm.valid = false;  // the next commit is a full build
+      h->dirty = true;
+    }
+    h->keyed_mode = (uint32_t)value;
     return 0;
   }
   if (strcmp(key, "fat_buckets") == 0) {  // 1 (default) / 0: from the next full build on

@@ -363,17 +363,15 @@ typedef struct emqxgm_retain_out { /* host-resident, valid until the next call o
 int emqxgm_retain_match(emqxgm_retain_t* r, const uint8_t* bytes, const uint32_t* offsets,
                         uint32_t n, uint64_t now_ms, emqxgm_retain_out* out);
 
-/* ---- NIF batcher core: publish windows over the host pipes ----------------------------------
- * What the emqx_trie_gpu NIF (c_src/emqx_trie_gpu_nif.c) calls per published topic.  The
- * reference answers every publish in its own process (emqx_broker:publish/1 ->
- * emqx_router:match_routes/1 -> emqx_trie:match/1, emqx_broker.erl:218-232,
- * emqx_router.erl:141-157, emqx_trie.erl:147-169); the batcher packs the topics of concurrent
- * publishers into a window in pinned host memory, submits a full window (or one that is due)
- * with emqxgm_match_batch_submit, and on collection expands every topic's trie row into its
- * filter bytes with one emqxgm_filters_copy per window, so the NIF builds each caller's filter
- * list from one arena.  Up to EMQXGM_HOST_PIPES windows are in flight; a window's result stays
- * valid until that many more windows are flushed.  One thread drives a batcher (the NIF's
- * batcher process); the handle's other calls stay thread-safe around it. */
+/* ---- single-driver batcher core: publish windows over the host pipes ---------------------
+ * A caller that batches topics itself (one thread adding, flushing and collecting; bench.py's
+ * window sweep) packs them into a window in pinned host memory, submits a full window (or one
+ * that is due) with emqxgm_match_batch_submit_filters, and on collection reads every topic's trie
+ * row with its filter bytes (gathered on the device).  Up to EMQXGM_HOST_PIPES windows are in
+ * flight; a window's result stays valid until that many more windows are flushed.  Collect waits
+ * without the batcher's lock.  The NIF uses the concurrent entry below (emqxgm_async_*), which
+ * any number of threads call one topic at a time (emqx_broker.erl:218-232,
+ * emqx_trie.erl:147-169). */
 typedef struct emqxgm_batcher emqxgm_batcher_t;
 typedef struct emqxgm_batcher_cfg {
   uint32_t window_topics; /* topics per window (0 = 65,536; <= the engine's batch_max) */

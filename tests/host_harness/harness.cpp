@@ -87,6 +87,7 @@ struct CpuWalk {
   std::vector<uint32_t> out;
   std::vector<std::pair<uint32_t, uint32_t>> stk;  // (node | item kind, level)
   static constexpr uint32_t IT_PLUS = 0x80000000u, IT_TN = 0x40000000u;
+  static constexpr uint32_t IT_KEYED = IT_PLUS | IT_TN, IT_KIND = IT_PLUS | IT_TN;
 
   explicit CpuWalk(const DevIndex& x) : ix(x) {}
   void em(uint32_t v) {
@@ -102,25 +103,26 @@ struct CpuWalk {
     const uint32_t h = cf_depth_code(cf & ix.leafp_mask);
     return (h != 0u && (int)(n - d) > (int)h) ? (cf & ~(CF_LIT | CF_PLUS)) : cf;
   }
-  void visit(uint32_t cf, uint32_t hf, uint32_t tw, uint32_t d, bool lit) {
+  void visit(uint32_t cf, uint32_t hf, uint32_t tw, uint32_t d, bool lit, uint32_t kind = 0) {
     if (hf != NONE) em(hf);
     if (d == n) {
       if (cf & CF_TW) em(tw);
       if (lit && (cf & CF_TN) && dollar && n == 1) stk.push_back({IT_TN | (cf & CF_ID_MASK), d});
     } else if (cf & CF_LIT) {
-      stk.push_back({cf & CF_ID_MASK, d});
+      stk.push_back({(cf & CF_ID_MASK) | kind, d});
     }
   }
   // fat: the state's only literal child comes with it in {h0, h1} (gm_common.h FAT_ID)
   void create(uint32_t cf, uint32_t hf, uint32_t tw, uint32_t sig, uint32_t pcf, uint32_t phf,
               uint32_t d, bool plus_ok, bool lit, bool fat = false, const uint4* h = nullptr) {
+    const bool keyed = sig == 0u && (cf & CF_LIT);  // gm_common.h edge_home
     cf = strip(cf, d);
     const uint64_t wtok = d < REC_TOKS ? (d < n ? toks[d] : 0ull) : 0ull;
     const bool fat_go = fat && (cf & CF_LIT) && d < n && d < REC_TOKS &&
                         (uint32_t)wtok == h[0].x && (uint32_t)(wtok >> 32) == h[0].y;
-    if (fat || (d < REC_TOKS && !(sig & sig_bit(wtok)))) cf &= ~CF_LIT;
+    if (fat || (!keyed && d < REC_TOKS && !(sig & sig_bit(wtok)))) cf &= ~CF_LIT;
     pcf = strip(pcf, d + 1);
-    visit(cf, hf, tw, d, lit);
+    visit(cf, hf, tw, d, lit, keyed ? IT_KEYED : 0u);
     if (fat_go)
       create(h[0].w, h[1].x, h[1].y, h[0].z >> SIG_SHIFT, h[1].z, h[1].w, d + 1, true, true);
     if (!plus_ok || d >= n || !(cf & CF_PLUS)) return;
@@ -134,8 +136,8 @@ struct CpuWalk {
   }
   // the edge slot of (node, key): probes buckets like k_walk (a bucket with an empty slot ends)
   // fat: the hit is a bucket's first slot and the second holds its fat half (copied to h)
-  bool probe(uint32_t node, uint64_t key, uint4 s[2], bool& fat, uint4 h[2]) const {
-    for (uint64_t b = edge_slot(node, key, ix.emask);; b = (b + 1) & ix.emask) {
+  bool probe(uint32_t node, uint64_t key, bool keyed, uint4 s[2], bool& fat, uint4 h[2]) const {
+    for (uint64_t b = edge_home(node, key, ix.emask, keyed);; b = (b + 1) & ix.emask) {
       bool empty = false;
       for (uint32_t j = 0; j < EBUCKET; ++j) {
         const uint4* q = ix.edges + SLOT_U4 * (EBUCKET * b + j);
@@ -172,19 +174,20 @@ struct CpuWalk {
     while (!stk.empty()) {
       const auto it = stk.back();
       stk.pop_back();
-      if (it.first & IT_TN) {
+      const uint32_t kind = it.first & IT_KIND;
+      if (kind == IT_TN) {
         em(ix.tn_of[it.first & CF_ID_MASK]);
         continue;
       }
       const uint32_t node = it.first & CF_ID_MASK, k = it.second;
-      const uint64_t key = (it.first & IT_PLUS) ? PLUS_TOK : toks[k];
+      const uint64_t key = kind == IT_PLUS ? PLUS_TOK : toks[k];
       uint4 s[2], hh[2];
       bool fat = false;
-      const bool hit = probe(node, key, s, fat, hh);
+      const bool hit = probe(node, key, kind == IT_KEYED, s, fat, hh);
       if (getenv("HH_TRACE")) fprintf(stderr, "probe node %u k %u plus %d -> %d fat %d\n", node, k, (it.first & IT_PLUS) ? 1 : 0, hit ? 1 : 0, fat ? 1 : 0);
       if (hit)
         create(s[0].w, s[1].x, s[1].y, s[0].z >> SIG_SHIFT, s[1].z, s[1].w, k + 1, true,
-               !(it.first & IT_PLUS), fat, hh);
+               kind != IT_PLUS, fat, hh);
     }
     return out;
   }
@@ -235,6 +238,7 @@ int main(int argc, char** argv) {
   const uint64_t seed = argc > 1 ? strtoull(argv[1], nullptr, 10) : 1;
   const int rounds = argc > 2 ? atoi(argv[2]) : 30;
   const uint32_t hash_bits = argc > 3 ? (uint32_t)atoi(argv[3]) : 0;
+  const int keyed_mode = argc > 5 ? atoi(argv[5]) : 1;  // emqxgm_tune "keyed" (2: every eligible node)
   std::mt19937_64 rng(seed);
   auto rnd = [&](uint64_t k) { return (uint64_t)(rng() % k); };
 
@@ -267,6 +271,7 @@ int main(int argc, char** argv) {
   CHECK(emqxgm_create(&cfg, &hd) == 0, "create");
   CHECK(emqxgm_create(&cfg, &hf) == 0, "create");
   CHECK(emqxgm_tune(hf, "delta_commit", 0) == 0, "tune");
+  CHECK(emqxgm_tune(hd, "keyed", keyed_mode) == 0 && emqxgm_tune(hf, "keyed", keyed_mode) == 0, "tune");
   CHECK(emqxgm_set_local_node(hd, 1) == 0 && emqxgm_set_local_node(hf, 1) == 0, "node");
   Oracle orc;
   std::set<std::string> in_trie, keyed;
@@ -281,6 +286,7 @@ int main(int argc, char** argv) {
       emqxgm_destroy(hd);
       hd = nullptr;
       CHECK(emqxgm_create(&cfg, &hd) == 0, "create");
+      CHECK(emqxgm_tune(hd, "keyed", keyed_mode) == 0, "tune");
       CHECK(emqxgm_snapshot_load(hd, snap.c_str()) == 0, "load: %s", hd->err.c_str());
       emqxgm_t* other = nullptr;
       CHECK(emqxgm_create(&cfg, &other) == 0, "create");

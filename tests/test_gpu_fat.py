@@ -110,3 +110,68 @@ def test_fat_buckets_delta_churn(emqx):
         eng.commit()
         _check(eng, py, topics)
     assert eng.stats()["delta_commits"] > 0
+
+
+def _wide_tree(rng, n):
+    """Filters whose nodes have many literal children, some shared between a literal parent and
+    its '+' twin (the cfg3 shape site/S/device/D vs site/+/device/D), plus '#', '$' and deep
+    levels past the topic record's 7 tokens."""
+    filters = set()
+    for _ in range(n):
+        s = rng.randrange(40)
+        d = s * 100 + rng.randrange(100)
+        r = rng.random()
+        if r < 0.5:
+            f = f"site/{s}/device/{d}/#"
+        elif r < 0.7:
+            f = f"site/+/device/{d}/#"
+        elif r < 0.8:
+            f = f"site/{s}/device/{d}/+/{rng.randrange(8)}"
+        elif r < 0.9:
+            f = f"site/{s}/device/{d}/a/b/c/d/e/{rng.randrange(4)}"
+        else:
+            f = f"{rng.choice(['$SYS', 'x', ''])}/{rng.randrange(60)}/{rng.choice(['+', 'q'])}"
+        filters.add(f.encode())
+    return sorted(filters)
+
+
+@pytest.mark.parametrize("keyed", [0, 1, 2])
+@pytest.mark.parametrize("bits", [0, 4])
+def test_keyed_parents_full_build_and_delta(emqx, keyed, bits):
+    """Token-keyed parents (gm_common.h edge_home; tune "keyed": 0 none, 1 auto, 2 every
+    eligible node): full build, then delta churn that adds and removes children of keyed
+    parents, checked against the Python restatement after every commit."""
+    rng = random.Random(41 + keyed + bits)
+    filters = _wide_tree(rng, 3000)
+    topics = []
+    for _ in range(4000):
+        s = rng.randrange(45)
+        d = s * 100 + rng.randrange(110)
+        tail = "/".join(str(rng.randrange(9)) if rng.random() < 0.5 else rng.choice("abcdeq")
+                        for _ in range(rng.randint(0, 7)))
+        topics.append((f"site/{s}/device/{d}" + ("/" + tail if tail else "")).encode())
+    topics += [f"{p}/{k}/q".encode() for p in ("$SYS", "x", "") for k in range(0, 70, 7)]
+    eng = emqx.Engine(word_hash_bits=bits)
+    eng.tune("keyed", keyed)
+    eng.tune("delta_commit", 2)
+    py = R.Trie()
+    for f in filters:
+        eng.trie_insert(f)
+        py.insert(f)
+    eng.commit()
+    _check(eng, py, topics)
+    live = list(filters)
+    for _ in range(6):
+        for _ in range(60):
+            if rng.random() < 0.45 and live:
+                f = live.pop(rng.randrange(len(live)))
+                eng.trie_delete(f)
+                py.delete(f)
+            else:
+                f = rng.choice(_wide_tree(rng, 1))
+                if f not in live:
+                    live.append(f)
+                    eng.trie_insert(f)
+                    py.insert(f)
+        eng.commit()
+        _check(eng, py, topics)

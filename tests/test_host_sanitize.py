@@ -37,12 +37,15 @@ def _build():
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("seed,rounds,hash_bits", [(11, 25, 0), (12, 12, 3)])
-def test_engine_host_code_under_asan_ubsan(seed, rounds, hash_bits, tmp_path):
+@pytest.mark.parametrize("seed,rounds,hash_bits,keyed", [(11, 25, 0, 1), (12, 12, 3, 1),
+                                                         (13, 20, 0, 2), (14, 10, 3, 2)])
+def test_engine_host_code_under_asan_ubsan(seed, rounds, hash_bits, keyed, tmp_path):
+    """keyed 2: every eligible trie node token-keyed (gm_common.h edge_home), so the CPU walk
+    and the delta commits run over keyed placements."""
     exe = _build()
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
-    r = subprocess.run([exe, str(seed), str(rounds), str(hash_bits), str(tmp_path)],
+    r = subprocess.run([exe, str(seed), str(rounds), str(hash_bits), str(tmp_path), str(keyed)],
                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env,
                        timeout=540)
     assert r.returncode == 0, r.stdout[-6000:]
