@@ -139,13 +139,26 @@ struct emqxgm_async {
     if (s.n == 0) s.off[0] = 0;
   }
 
+  bool pipe_free() const {
+    for (uint32_t v : outstanding)
+      if (v < EMQXGM_HOST_PIPES) return true;
+    return false;
+  }
+
+  // Windows grow while every pipe is busy: the window_us timer seals the open window only when a
+  // pipe could take it at once (and nothing sealed is waiting), so an idle broker answers within
+  // window_us plus a pass, and a loaded one submits windows as large as the pipes' pace allows
+  // (sealing on the timer regardless made windows of a few hundred calls queue behind the busy
+  // pipes: r04 nif_concurrent, 3 M calls/s at 330 calls per window).
   void flusher_loop() {
     std::unique_lock<std::mutex> g(mu);
     for (;;) {
       const int oi = open.load(std::memory_order_acquire);
       if (oi >= 0) {
         const uint64_t f = slots[oi]->first_ns.load(std::memory_order_acquire);
-        if (stop || (f != 0 && mono_ns() >= f + 1000ull * cfg.window_us)) seal(oi);
+        if (stop || (f != 0 && ready.empty() && pipe_free() &&
+                     mono_ns() >= f + 1000ull * cfg.window_us))
+          seal(oi);
       }
       bool progressed = false;
       while (!ready.empty()) {
@@ -198,7 +211,7 @@ struct emqxgm_async {
       if (stop && open.load() < 0 && ready.empty()) break;
       const int o2 = open.load(std::memory_order_acquire);
       const uint64_t f = o2 >= 0 ? slots[o2]->first_ns.load(std::memory_order_acquire) : 0;
-      if (f != 0 && ready.empty()) {
+      if (f != 0 && ready.empty() && pipe_free()) {
         const uint64_t due = f + 1000ull * cfg.window_us, t = mono_ns();
         if (due > t) cv_flush.wait_for(g, std::chrono::nanoseconds(due - t));
       } else {

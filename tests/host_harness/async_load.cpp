@@ -21,6 +21,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -49,11 +52,21 @@ uint64_t fnv1a(const uint8_t* p, uint32_t n) {
   return h;
 }
 
+// A publisher thread ("scheduler"): its calls outstanding, and where it sleeps when it has P of
+// them (a BEAM scheduler whose processes all wait in receive sleeps too; spinning threads would
+// take the CPUs the engine's flusher and completer threads need).
+struct Pub {
+  std::atomic<int64_t> outstanding{0};
+  std::mutex m;
+  std::condition_variable cv;
+};
+
 struct Load {
   uint64_t calls_per_thread = 0;
   std::vector<uint64_t> t0;               // per call: when it was made
   std::vector<uint32_t> lat_us;           // per call: call -> result
-  std::atomic<int64_t>* outstanding = nullptr;
+  Pub* pubs = nullptr;
+  uint32_t threads = 0;
   uint32_t* out_count = nullptr;
   uint64_t* out_hash = nullptr;
   uint8_t* out_exact = nullptr;
@@ -63,6 +76,9 @@ struct Load {
 void on_window(void* user, const emqxgm_async_window* w) {
   Load* L = (Load*)user;
   const uint64_t now = mono_ns();
+  // reports per publisher thread, released once per window (one wake-up, not one per call)
+  thread_local std::vector<uint32_t> done;
+  done.assign(L->threads, 0);
   for (uint32_t i = 0; i < w->n; ++i) {
     const uint64_t c = w->tag[i];
     if (c == EMQXGM_TAG_CANCELLED) continue;
@@ -77,9 +93,18 @@ void on_window(void* user, const emqxgm_async_window* w) {
       L->out_exact[c] = w->exact_id[i] != EMQXGM_NONE;
     }
     L->lat_us[c] = (uint32_t)std::min<uint64_t>((now - L->t0[c]) / 1000, 0xFFFFFFFFu);
-    L->outstanding[w->owner[i]].fetch_sub(1, std::memory_order_release);
-    L->reported++;
+    done[w->owner[i]] += 1;
   }
+  uint64_t total = 0;
+  for (uint32_t k = 0; k < L->threads; ++k) {
+    if (!done[k]) continue;
+    total += done[k];
+    Pub& p = L->pubs[k];
+    p.outstanding.fetch_sub(done[k], std::memory_order_release);
+    { std::lock_guard<std::mutex> g(p.m); }
+    p.cv.notify_one();
+  }
+  L->reported += total;
 }
 
 }  // namespace
@@ -99,9 +124,9 @@ int async_load_run(emqxgm_t* const* hs, uint32_t nh, const emqxgm_async_cfg* cfg
   L.calls_per_thread = calls_per_thread;
   L.t0.assign(total, 0);
   L.lat_us.assign(total, 0);
-  std::vector<std::atomic<int64_t>> outstanding(threads);
-  for (auto& o : outstanding) o.store(0);
-  L.outstanding = outstanding.data();
+  std::vector<Pub> pubs(threads);
+  L.pubs = pubs.data();
+  L.threads = threads;
   L.out_count = out_count;
   L.out_hash = out_hash;
   L.out_exact = out_exact;
@@ -114,24 +139,32 @@ int async_load_run(emqxgm_t* const* hs, uint32_t nh, const emqxgm_async_cfg* cfg
   std::vector<std::thread> th;
   for (uint32_t k = 0; k < threads; ++k) {
     th.emplace_back([&, k] {
+      Pub& p = pubs[k];
       for (uint64_t i = 0; i < calls_per_thread; ++i) {
         const uint64_t c = (uint64_t)k * calls_per_thread + i;
         const uint64_t t = c % n_topics;
         if (out_topic) out_topic[c] = (uint32_t)t;
-        while (outstanding[k].load(std::memory_order_acquire) >= (int64_t)procs)
-          std::this_thread::yield();
-        outstanding[k].fetch_add(1, std::memory_order_relaxed);
+        if (p.outstanding.load(std::memory_order_acquire) >= (int64_t)procs) {
+          std::unique_lock<std::mutex> g(p.m);
+          p.cv.wait(g, [&] { return p.outstanding.load(std::memory_order_acquire) < (int64_t)procs; });
+        }
+        p.outstanding.fetch_add(1, std::memory_order_relaxed);
         L.t0[c] = mono_ns();
         for (;;) {
           const int r = emqxgm_async_match(a, tb + toff[t], (uint32_t)(toff[t + 1] - toff[t]), c, k);
           if (r == 0) break;
           if (r != -EBUSY) {
             err.store(r);
-            outstanding[k].fetch_sub(1);
+            p.outstanding.fetch_sub(1);
             break;
           }
+          // every window full or in flight: sleep until one of this thread's calls is reported
+          // (or a moment, when none is outstanding)
           busy++;
-          std::this_thread::yield();
+          const int64_t before = p.outstanding.load();
+          std::unique_lock<std::mutex> g(p.m);
+          p.cv.wait_for(g, std::chrono::microseconds(50),
+                        [&] { return p.outstanding.load() < before; });
         }
         if (err.load()) return;
       }

@@ -13,6 +13,7 @@
   cfg1, on a 1M-filter cfg3 slice, and with two engines (replicas) taking windows round robin.
 """
 import random
+import time
 
 import numpy as np
 import pytest
@@ -168,14 +169,23 @@ def test_async_matcher_calls_one_at_a_time(emqx):
     flt = [w.filter(i) for i in range(w.nf)]
     am = emqx.AsyncMatcher([eng], window_topics=4096, window_us=100, max_levels=8)
     keys = []
+
+    def call(topic, tag, owner):
+        # -EBUSY (every window full or in flight: a publisher would take the reference's path)
+        # is retried here, after the completers had a moment
+        while True:
+            rc = am.match(topic, tag, owner=owner)
+            if rc != -16:
+                return rc
+            time.sleep(0.0002)
     for i in range(w.nt):
-        assert am.match(w.topic(i), i, owner=1) == 0
+        assert call(w.topic(i), i, 1) == 0
         keys.append((i, 1))
     # edge calls: a wildcard name (trie [] but its exact key), an empty topic, too deep
     eng2_topics = [b"l0w1/+", b"", b"a/b/c/d/e/f/g/h/i"]
-    assert am.match(eng2_topics[0], 10**9, owner=2) == 0
-    assert am.match(eng2_topics[1], 10**9 + 1, owner=2) == 0
-    assert am.match(eng2_topics[2], 10**9 + 2, owner=2) == -7  # -E2BIG: 9 levels > 8
+    assert call(eng2_topics[0], 10**9, 2) == 0
+    assert call(eng2_topics[1], 10**9 + 1, 2) == 0
+    assert call(eng2_topics[2], 10**9 + 2, 2) == -7  # -E2BIG: 9 levels > 8
     assert am.wait(keys + [(10**9, 2), (10**9 + 1, 2)], timeout=60)
     for i in range(w.nt):
         r = am.results[(i, 1)]
@@ -192,13 +202,14 @@ def test_async_matcher_calls_one_at_a_time(emqx):
     outcomes = []
     for k in range(200):
         tag = 2 * 10**9 + k
-        assert am.match(w.topic(k), tag, owner=3) == 0
+        assert call(w.topic(k), tag, 3) == 0
         outcomes.append((tag, am.cancel(tag, owner=3)))
+    st = am.stats()
+    assert st["too_deep"] == 1
     am.close()  # reports every accepted call
     for tag, cancelled in outcomes:
         assert ((tag, 3) in am.results) != cancelled, tag
-    st = am.stats()
-    assert st["too_deep"] == 1 and st["failed"] == 0
+    assert all(r.status == 0 for r in am.results.values())
 
 
 def _oracle_rows(w):

@@ -53,7 +53,8 @@ step_bench() {
   topics=${rest%%:*}
   [ "$rest" != "$topics" ] && extra=${rest#*:}
   local T=""; [ -n "$topics" ] && [ "$topics" != 0 ] && T="--topics $topics"
-  local name=bench_c${cfg}_${topics:-0}
+  local tag=${extra//[^a-zA-Z0-9=]/_}
+  local name=bench_c${cfg}_${topics:-0}${tag:+_$tag}
   (cd $R && timeout -k 10 900 python -u bench.py --cfg $cfg $T ${extra//,/ }) > $O/$name.json 2> $O/$name.log
 }
 
