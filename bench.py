@@ -129,8 +129,8 @@ def main():
     eng, _ = _build_engine(Engine, w, np.arange(w.nf), args, local)
     est = eng.stats()
     log(f"[rank {rank}] index: {est['n_trie_filters']} trie filters, {est['n_route_keys']} route "
-        f"keys, {est['n_nodes']} nodes, {est['device_bytes'] / 2**20:.0f} MiB in "
-        f"{time.time() - t0:.1f}s")
+        f"keys, {est['n_nodes']} nodes ({est['keyed_nodes']} token-keyed), "
+        f"{est['device_bytes'] / 2**20:.0f} MiB in {time.time() - t0:.1f}s")
 
     if args.only_nif:
         out = _nif_concurrent(eng, w, args.nif)
@@ -351,6 +351,7 @@ def main():
                     (f"topic-replica x{world}" if args.shard == "topics" or world == 1
                      else f"filter-shard x{world}"),
                 "pairs_per_batch": int(census["pairs"]),
+                "trie_nodes": int(est["n_nodes"]), "token_keyed_nodes": int(est["keyed_nodes"]),
                 "trie_states_per_batch": int(census["states"]),
                 "walk_states_visited_per_batch": int(census["states_visited"]),
                 "edge_slot_loads_unpruned_per_batch": int(census_full["slot_loads"]),

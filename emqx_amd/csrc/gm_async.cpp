@@ -1,11 +1,11 @@
 // gm_async.cpp -- the concurrent publish entry (include/emqx_gpumatch.h "concurrent publish
 // entry"): any number of threads hand in one topic each, the layer packs them into windows in
-// pinned host memory, a flusher thread submits a window when it is full or window_us after its
-// first topic (emqxgm_match_batch_submit_filters), and one completer thread per engine handle
-// waits for its windows in submission order (emqxgm_match_batch_wait_filters, which waits
-// without holding the engine's locks) and hands each completed window to the caller's callback.
-// With several handles (one engine per GPU, each holding the whole index: the replica layout of
-// DESIGN.md 5) windows go round robin to the handles with a pipe free.
+// pinned host memory, a flusher thread submits a window when it is full or (with a pipe free)
+// window_us after its first topic (emqxgm_match_batch_submit_filters), and one completer thread
+// per engine handle waits for its windows in submission order (emqxgm_match_batch_wait_filters,
+// which waits without holding the engine's locks) and hands each completed window to the
+// caller's callback.  With several handles (one engine per GPU, each holding the whole index:
+// the replica layout of DESIGN.md 5) windows go round robin to the handles with a pipe free.
 //
 // The reference matches each publish inside the publisher's own process, concurrently on every
 // scheduler, against read_concurrency ETS tables (emqx_broker:publish/1 ->
@@ -14,13 +14,15 @@
 // (c_src/emqx_trie_gpu_nif.c) is this layer's emqxgm_async_match, called from those processes
 // directly, and its callback enif_sends each caller its result.
 //
-// A call takes no lock: it reserves its place in the open window with one atomic add on the
-// window's (calls, bytes) cursor, copies its topic there and counts itself settled.  Places are
-// handed out in order, so the reservations that fit are a prefix of the window; the first one
-// that does not fit (or the flusher's timer) seals the window: a seal adds SEAL calls to the
-// cursor, so every later reservation fails and goes to the next window.  The flusher submits a
-// sealed window once every reservation made before the seal has settled.  Only the slow paths
-// (a window full or due, no window open, the flusher and completers) take the layer's mutex.
+// Contention.  A call appends its topic to its own thread's staging chunk (a spinlock nobody else
+// takes except the flusher, when it seals a window): no shared cache line per call.  A full chunk
+// -- or the flusher, before it seals a window -- moves the chunk into the open window with ONE
+// atomic add on the window's (calls, bytes) cursor and one copy.  Places are handed out in
+// order, so the reservations that fit are a prefix of the window; the first that does not seals
+// it (a seal adds SEAL calls to the cursor: every later reservation fails and goes to the next
+// window).  The flusher submits a sealed window once every reservation made before the seal has
+// settled.  (r04: one atomic reservation per call put every call on two contended lines and the
+// calls' neighbouring tags on shared lines: 4 M calls/s whatever the thread count.)
 #include <errno.h>
 #include <string.h>
 #include <time.h>
@@ -48,21 +50,24 @@ uint64_t mono_ns() {
 
 enum SlotState { FREE, OPEN, READY, SUBMITTING, INFLIGHT, DELIVERING };
 
-constexpr uint64_t CALL1 = 1ull << 32;     // one call in the cursor's high half
 constexpr uint32_t SEAL = 1u << 31;        // calls a seal adds: every later reservation fails
+constexpr uint32_t CHUNK_CALLS = 64;       // a thread's staging chunk (at most: a window's size)
+constexpr uint32_t CHUNK_BYTES = 4096;
 
 static_assert(sizeof(std::atomic<uint64_t>) == sizeof(uint64_t), "tags are read as uint64_t");
+
+std::atomic<uint64_t> g_layer_ids{1};
 
 // One window: its packed topics in pinned memory (the H2D source of its pass) and the callers.
 struct Slot {
   uint8_t* bytes = nullptr;  // pinned [window_bytes]
   uint32_t* off = nullptr;   // pinned [window_topics + 1]
   std::unique_ptr<std::atomic<uint64_t>[]> tag, owner;  // [window_topics]
-  std::atomic<uint64_t> cursor{0};    // (calls reserved << 32) | bytes reserved
-  std::atomic<uint32_t> settled{0};   // reservations made before the seal that are done
-  std::atomic<uint32_t> limit{~0u};   // the first reservation that did not fit
+  alignas(64) std::atomic<uint64_t> cursor{0};  // (calls reserved << 32) | bytes reserved
+  alignas(64) std::atomic<uint32_t> settled{0};  // calls of reservations before the seal, done
+  std::atomic<uint32_t> limit{~0u};   // the first call of the first reservation that did not fit
   std::atomic<bool> sealed{false};
-  std::atomic<uint64_t> first_ns{0};
+  std::atomic<uint64_t> first_ns{0};  // its oldest call
   uint32_t reserved = 0;  // calls reserved before the seal (set by the sealer)
   uint32_t n = 0;         // calls in the window (set once they settled)
   int state = FREE;       // guarded by the layer's mutex
@@ -71,32 +76,77 @@ struct Slot {
   uint64_t ticket = 0, flush_ns = 0;
 };
 
+// Calls on their way into a window: a thread's staging chunk, or one long call on its own.
+struct Span {
+  uint32_t k = 0, b = 0;  // calls, bytes
+  uint32_t* len = nullptr;
+  uint64_t *tag = nullptr, *owner = nullptr;
+  const uint8_t* bytes = nullptr;
+  uint64_t first_ns = 0;
+};
+
+// One producer thread's staging chunk.  Its spinlock is taken by its own thread per call and by
+// the flusher when it drains every chunk before a seal.
+struct alignas(64) Chunk {
+  std::atomic<bool> busy{false};
+  std::atomic<uint64_t> first_ns{0};  // its oldest call (0: empty)
+  uint32_t k = 0, b = 0;
+  uint64_t accepted = 0;  // calls this thread handed in (stats)
+  std::unique_ptr<uint32_t[]> len;
+  std::unique_ptr<uint64_t[]> tag, owner;
+  std::unique_ptr<uint8_t[]> bytes;
+  void lock() {
+    while (busy.exchange(true, std::memory_order_acquire))
+      while (busy.load(std::memory_order_relaxed)) std::this_thread::yield();
+  }
+  void unlock() { busy.store(false, std::memory_order_release); }
+  Span span() {
+    Span s;
+    s.k = k;
+    s.b = b;
+    s.len = len.get();
+    s.tag = tag.get();
+    s.owner = owner.get();
+    s.bytes = bytes.get();
+    s.first_ns = first_ns.load(std::memory_order_relaxed);
+    return s;
+  }
+  void clear() {
+    k = b = 0;
+    first_ns.store(0, std::memory_order_relaxed);
+  }
+};
+
 }  // namespace
 
 struct emqxgm_async {
+  uint64_t id = 0;
   std::vector<emqxgm_t*> hs;
   emqxgm_async_cfg cfg{};
+  uint32_t chunk_calls = CHUNK_CALLS, chunk_bytes = CHUNK_BYTES;
   emqxgm_async_cb cb = nullptr;
   void* user = nullptr;
   std::vector<std::unique_ptr<Slot>> slots;
   std::vector<int> free_slots;
+  std::vector<std::unique_ptr<Chunk>> chunks;    // registered staging chunks (mu)
   std::atomic<int> open{-1};                     // the slot taking calls, or -1
   std::deque<int> ready;                         // sealed windows, oldest first
   std::vector<std::deque<int>> inflight;         // per handle, in submission order
   std::vector<uint32_t> outstanding;             // per handle: submitted and not yet released
   uint32_t rr = 0;                               // next handle to try
   bool stop = false, flusher_done = false;
+  std::atomic<int> flusher_idle{0};              // the flusher sleeps with nothing pending
   std::mutex mu;
-  std::condition_variable cv_flush;              // the flusher: a window ready / opened, a pipe free
+  std::condition_variable cv_flush;              // the flusher: work, a pipe free
   std::condition_variable cv_done;               // a window was released (cancel)
   std::vector<std::unique_ptr<std::condition_variable>> cv_comp;  // completer k: work on handle k
   std::thread flusher;
   std::vector<std::thread> completers;
-  std::atomic<uint64_t> st_calls{0}, st_busy{0}, st_too_big{0};
+  std::atomic<uint64_t> st_direct{0}, st_busy{0}, st_too_big{0};
   uint64_t st_windows = 0, st_cancelled = 0, st_errors = 0, st_delivered = 0;
 
   // Seals slot si (with mu held): no reservation after this one succeeds; the window goes to the
-  // ready queue (the flusher submits it once its reservations settled) or, empty, back to free.
+  // ready queue (the flusher submits it once its reservations settled).
   void seal(int si) {
     Slot& s = *slots[si];
     if (s.state != OPEN || s.sealed.exchange(true)) return;
@@ -127,38 +177,145 @@ struct emqxgm_async {
     open.store(si, std::memory_order_release);
     return true;
   }
-  // The calls of a sealed window, once every reservation made before its seal settled (mu not
-  // needed: `reserved` was set under mu before the window became READY).
-  bool settled(Slot& s) const {
-    return s.settled.load(std::memory_order_acquire) >= s.reserved;
-  }
+  bool settled(Slot& s) const { return s.settled.load(std::memory_order_acquire) >= s.reserved; }
   void finish_window(Slot& s) {
     const uint32_t lim = s.limit.load(std::memory_order_relaxed);
     s.n = std::min({s.reserved, lim, cfg.window_topics});
-    // off[i] = start of call i; the end of the last one was stored by it as off[n]
-    if (s.n == 0) s.off[0] = 0;
+    if (s.n == 0) s.off[0] = 0;  // (off[n] was stored by the last reservation that fit)
   }
-
   bool pipe_free() const {
     for (uint32_t v : outstanding)
       if (v < EMQXGM_HOST_PIPES) return true;
     return false;
   }
 
-  // Windows grow while every pipe is busy: the window_us timer seals the open window only when a
-  // pipe could take it at once (and nothing sealed is waiting), so an idle broker answers within
-  // window_us plus a pass, and a loaded one submits windows as large as the pipes' pace allows
-  // (sealing on the timer regardless made windows of a few hundred calls queue behind the busy
-  // pipes: r04 nif_concurrent, 3 M calls/s at 330 calls per window).
+  // Moves span x into the open window (opening / sealing windows as they fill).  0, or -EBUSY
+  // (no window to take it: every slot full or in flight), -ESHUTDOWN.  Lock-free except when a
+  // window fills or none is open.
+  int place(const Span& x) {
+    const uint32_t WT = cfg.window_topics, WB = cfg.window_bytes;
+    for (;;) {
+      const int si = open.load(std::memory_order_acquire);
+      if (si < 0) {
+        std::lock_guard<std::mutex> g(mu);
+        if (stop && flusher_done) return -ESHUTDOWN;
+        if (open.load() < 0 && !open_slot()) return -EBUSY;
+        continue;
+      }
+      Slot& s = *slots[si];
+      const uint64_t c = s.cursor.fetch_add(((uint64_t)x.k << 32) | x.b, std::memory_order_acq_rel);
+      const uint32_t n = (uint32_t)(c >> 32), b0 = (uint32_t)c;
+      if (n >= SEAL) {  // sealed: the next window
+        std::lock_guard<std::mutex> g(mu);
+        if (open.load() == si) seal(si);
+        if (open.load() < 0 && !open_slot()) return -EBUSY;
+        continue;
+      }
+      const bool fits = (uint64_t)n + x.k <= WT && (uint64_t)b0 + x.b <= WB;
+      if (fits) {
+        if (x.b) memcpy(s.bytes + b0, x.bytes, x.b);
+        uint32_t o = b0;
+        for (uint32_t i = 0; i < x.k; ++i) {
+          __atomic_store_n(&s.off[n + i], o, __ATOMIC_RELAXED);
+          o += x.len[i];
+          s.tag[n + i].store(x.tag[i], std::memory_order_relaxed);
+          s.owner[n + i].store(x.owner[i], std::memory_order_relaxed);
+        }
+        __atomic_store_n(&s.off[n + x.k], o, __ATOMIC_RELAXED);
+        const uint64_t xf = x.first_ns ? x.first_ns : mono_ns();
+        uint64_t f = s.first_ns.load(std::memory_order_relaxed);
+        while ((f == 0 || xf < f) &&
+               !s.first_ns.compare_exchange_weak(f, xf, std::memory_order_release)) {
+        }
+      } else {
+        // the first reservation that does not fit bounds the window (no later one can fit:
+        // places and bytes are handed out in order)
+        uint32_t cur = s.limit.load(std::memory_order_relaxed);
+        while (n < cur && !s.limit.compare_exchange_weak(cur, n, std::memory_order_relaxed)) {
+        }
+      }
+      s.settled.fetch_add(x.k, std::memory_order_release);
+      const bool full = fits && ((uint64_t)n + x.k == WT || (uint64_t)b0 + x.b == WB);
+      if (fits && !full) return 0;
+      std::lock_guard<std::mutex> g(mu);
+      if (open.load() == si) seal(si);
+      if (fits) return 0;
+      if (open.load() < 0 && !open_slot()) return -EBUSY;
+    }
+  }
+
+  Chunk* my_chunk() {
+    thread_local std::vector<std::pair<uint64_t, Chunk*>> cache;
+    for (auto& e : cache)
+      if (e.first == id) return e.second;
+    std::unique_ptr<Chunk> c(new (std::nothrow) Chunk());
+    if (!c) return nullptr;
+    c->len.reset(new (std::nothrow) uint32_t[chunk_calls]);
+    c->tag.reset(new (std::nothrow) uint64_t[chunk_calls]);
+    c->owner.reset(new (std::nothrow) uint64_t[chunk_calls]);
+    c->bytes.reset(new (std::nothrow) uint8_t[chunk_bytes]);
+    if (!c->len || !c->tag || !c->owner || !c->bytes) return nullptr;
+    Chunk* p = c.get();
+    {
+      std::lock_guard<std::mutex> g(mu);
+      chunks.push_back(std::move(c));
+    }
+    cache.emplace_back(id, p);  // ids are never reused: a destroyed layer's entry never matches
+    return p;
+  }
+
+  // Every chunk into the windows (the flusher, before it seals; mu not held).  false: a chunk
+  // could not be placed (no window free), it stays staged.
+  bool drain_all() {
+    std::vector<Chunk*> cs;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      for (auto& c : chunks) cs.push_back(c.get());
+    }
+    bool ok = true;
+    for (Chunk* c : cs) {
+      if (c->first_ns.load(std::memory_order_acquire) == 0) continue;
+      c->lock();
+      if (c->k) {
+        if (place(c->span()) == 0) c->clear();
+        else ok = false;
+      }
+      c->unlock();
+    }
+    return ok;
+  }
+  // The oldest staged call of any chunk (0: none); mu held.
+  uint64_t oldest_staged() const {
+    uint64_t f = 0;
+    for (auto& c : chunks) {
+      const uint64_t x = c->first_ns.load(std::memory_order_seq_cst);
+      if (x && (!f || x < f)) f = x;
+    }
+    return f;
+  }
+
+  // Windows grow while every pipe is busy: the window_us timer seals the open window (after
+  // draining the staging chunks into it) only when a pipe could take it at once and nothing
+  // sealed is waiting, so an idle broker answers within window_us plus a pass, and a loaded one
+  // submits windows as large as the pipes' pace allows (sealing on the timer regardless made
+  // windows of a few hundred calls queue behind the busy pipes, r04).
   void flusher_loop() {
     std::unique_lock<std::mutex> g(mu);
     for (;;) {
       const int oi = open.load(std::memory_order_acquire);
-      if (oi >= 0) {
-        const uint64_t f = slots[oi]->first_ns.load(std::memory_order_acquire);
-        if (stop || (f != 0 && ready.empty() && pipe_free() &&
-                     mono_ns() >= f + 1000ull * cfg.window_us))
-          seal(oi);
+      const uint64_t fw = oi >= 0 ? slots[oi]->first_ns.load(std::memory_order_acquire) : 0;
+      const uint64_t fc = oldest_staged();
+      const uint64_t f = (fw && fc) ? std::min(fw, fc) : (fw | fc);
+      if (stop || (f != 0 && ready.empty() && pipe_free() &&
+                   mono_ns() >= f + 1000ull * cfg.window_us)) {
+        g.unlock();
+        const bool drained = drain_all();
+        g.lock();
+        const int o2 = open.load();
+        if (o2 >= 0 && slots[o2]->cursor.load() != 0) seal(o2);
+        if (stop && !drained) {  // staged calls and no window free: wait for a completer
+          if (ready.empty()) cv_flush.wait_for(g, std::chrono::microseconds(100));
+        }
       }
       bool progressed = false;
       while (!ready.empty()) {
@@ -174,7 +331,7 @@ struct emqxgm_async {
         if (k == H) break;  // every pipe busy: a completer's release wakes us
         const int si = ready.front();
         Slot& s = *slots[si];
-        if (!settled(s)) {  // a caller is still copying its topic in: a moment
+        if (!settled(s)) {  // a caller is still copying its calls in: a moment
           g.unlock();
           std::this_thread::yield();
           g.lock();
@@ -183,7 +340,7 @@ struct emqxgm_async {
         }
         ready.pop_front();
         finish_window(s);
-        if (s.n == 0) {  // sealed before anyone's reservation fit
+        if (s.n == 0) {  // sealed before any reservation fit
           s.state = FREE;
           free_slots.push_back(si);
           progressed = true;
@@ -208,15 +365,23 @@ struct emqxgm_async {
         progressed = true;
       }
       if (progressed) continue;
-      if (stop && open.load() < 0 && ready.empty()) break;
-      const int o2 = open.load(std::memory_order_acquire);
-      const uint64_t f = o2 >= 0 ? slots[o2]->first_ns.load(std::memory_order_acquire) : 0;
-      if (f != 0 && ready.empty() && pipe_free()) {
-        const uint64_t due = f + 1000ull * cfg.window_us, t = mono_ns();
+      const int o3 = open.load(std::memory_order_acquire);
+      const bool window_empty = o3 < 0 || slots[o3]->cursor.load() == 0;
+      if (stop && window_empty && ready.empty() && oldest_staged() == 0) break;
+      const uint64_t fw2 = o3 >= 0 ? slots[o3]->first_ns.load(std::memory_order_acquire) : 0;
+      flusher_idle.store(1, std::memory_order_seq_cst);
+      const uint64_t fc2 = oldest_staged();  // (re-read after announcing the idle sleep)
+      const uint64_t f2 = (fw2 && fc2) ? std::min(fw2, fc2) : (fw2 | fc2);
+      if (f2 != 0) flusher_idle.store(0, std::memory_order_relaxed);
+      if (f2 != 0 && ready.empty() && pipe_free()) {
+        const uint64_t due = f2 + 1000ull * cfg.window_us, t = mono_ns();
         if (due > t) cv_flush.wait_for(g, std::chrono::nanoseconds(due - t));
+      } else if (f2 != 0 || !ready.empty()) {
+        cv_flush.wait(g);  // pipes busy: a completer's release wakes us
       } else {
-        cv_flush.wait(g);
+        cv_flush.wait(g);  // nothing pending: a producer's first staged call wakes us
       }
+      flusher_idle.store(0, std::memory_order_relaxed);
     }
     flusher_done = true;
     for (auto& c : cv_comp) c->notify_all();
@@ -280,6 +445,7 @@ int emqxgm_async_create(emqxgm_t* const* hs, uint32_t n_handles, const emqxgm_as
     if (!hs[k]) return -EINVAL;
   emqxgm_async* a = new (std::nothrow) emqxgm_async();
   if (!a) return -ENOMEM;
+  a->id = g_layer_ids.fetch_add(1);
   a->hs.assign(hs, hs + n_handles);
   if (cfg) a->cfg = *cfg;
   if (!a->cfg.window_topics) a->cfg.window_topics = 65536;
@@ -290,6 +456,9 @@ int emqxgm_async_create(emqxgm_t* const* hs, uint32_t n_handles, const emqxgm_as
     delete a;
     return -EINVAL;
   }
+  // a chunk always fits an empty window
+  a->chunk_calls = std::min(CHUNK_CALLS, a->cfg.window_topics);
+  a->chunk_bytes = std::min(CHUNK_BYTES, a->cfg.window_bytes);
   a->cb = cb;
   a->user = user;
   const uint32_t n_slots = n_handles * EMQXGM_HOST_PIPES + 1 + a->cfg.queued_windows;
@@ -340,7 +509,7 @@ void emqxgm_async_destroy(emqxgm_async_t* a) {
     a->stop = true;
     a->cv_flush.notify_all();
   }
-  a->flusher.join();  // seals and submits what is left, then wakes the completers
+  a->flusher.join();  // drains the chunks, seals and submits what is left, wakes the completers
   for (auto& t : a->completers) t.join();  // deliver every accepted call
   const uint32_t H = (uint32_t)a->hs.size();
   for (size_t i = 0; i < a->slots.size(); ++i) {
@@ -364,62 +533,73 @@ int emqxgm_async_match(emqxgm_async_t* a, const uint8_t* topic, uint32_t len, ui
       return -E2BIG;
     }
   }
-  const uint32_t WT = a->cfg.window_topics, WB = a->cfg.window_bytes;
-  for (;;) {
-    const int si = a->open.load(std::memory_order_acquire);
-    if (si >= 0) {
-      Slot& s = *a->slots[si];
-      const uint64_t c = s.cursor.fetch_add(CALL1 | len, std::memory_order_acq_rel);
-      const uint32_t n = (uint32_t)(c >> 32), b = (uint32_t)c;
-      if (n < SEAL) {  // a reservation made before the window was sealed
-        const bool fits = n < WT && (uint64_t)b + len <= WB;
-        if (fits) {
-          if (len) memcpy(s.bytes + b, topic, len);
-          __atomic_store_n(&s.off[n], b, __ATOMIC_RELAXED);
-          __atomic_store_n(&s.off[n + 1], b + len, __ATOMIC_RELAXED);
-          s.tag[n].store(tag, std::memory_order_relaxed);
-          s.owner[n].store(owner, std::memory_order_relaxed);
-          if (n == 0) s.first_ns.store(mono_ns(), std::memory_order_release);
-        } else {
-          // the first reservation that does not fit bounds the window (the later ones cannot
-          // fit either: places and bytes are handed out in order)
-          uint32_t cur = s.limit.load(std::memory_order_relaxed);
-          while (n < cur && !s.limit.compare_exchange_weak(cur, n, std::memory_order_relaxed)) {
-          }
-        }
-        s.settled.fetch_add(1, std::memory_order_release);
-        if (fits) {
-          a->st_calls.fetch_add(1, std::memory_order_relaxed);
-          const bool full = n + 1 == WT || (uint64_t)b + len == WB;
-          if (n == 0 || full) {
-            std::lock_guard<std::mutex> g(a->mu);
-            if (full) a->seal(si);  // no room for the next one
-            else a->cv_flush.notify_one();  // arms the flusher's window_us timer
-          }
-          return 0;
-        }
-      }
-      // the window is full or sealed: seal it (if nobody did) and go to the next one
-      std::lock_guard<std::mutex> g(a->mu);
-      if (a->stop) return -ESHUTDOWN;
-      if (a->open.load() == si) a->seal(si);
-      if (a->open.load() < 0 && !a->open_slot()) {
-        a->st_busy.fetch_add(1, std::memory_order_relaxed);
-        return -EBUSY;  // every window is full or in flight: the caller answers this one itself
-      }
-      continue;
-    }
-    std::lock_guard<std::mutex> g(a->mu);
-    if (a->stop) return -ESHUTDOWN;
-    if (a->open.load() < 0 && !a->open_slot()) {
-      a->st_busy.fetch_add(1, std::memory_order_relaxed);
-      return -EBUSY;
-    }
+  if (len > a->chunk_bytes) {  // a long topic goes into the window on its own
+    Span x;
+    x.k = 1;
+    x.b = len;
+    x.len = &len;
+    x.tag = &tag;
+    x.owner = &owner;
+    x.bytes = topic;
+    x.first_ns = mono_ns();
+    const int rc = a->place(x);
+    if (rc == -EBUSY) a->st_busy.fetch_add(1, std::memory_order_relaxed);
+    if (rc == 0) a->st_direct.fetch_add(1, std::memory_order_relaxed);
+    return rc;
   }
+  Chunk* c = a->my_chunk();
+  if (!c) return -ENOMEM;
+  c->lock();
+  if (c->k == a->chunk_calls || c->b + len > a->chunk_bytes) {
+    const int rc = a->place(c->span());
+    if (rc) {
+      c->unlock();
+      if (rc == -EBUSY) a->st_busy.fetch_add(1, std::memory_order_relaxed);
+      return rc;  // every window full or in flight: the caller answers this one itself
+    }
+    c->clear();
+  }
+  const uint32_t i = c->k;
+  if (len) memcpy(c->bytes.get() + c->b, topic, len);
+  c->len[i] = len;
+  c->tag[i] = tag;
+  c->owner[i] = owner;
+  c->k = i + 1;
+  c->b += len;
+  c->accepted += 1;
+  const bool first = i == 0;
+  if (first) c->first_ns.store(mono_ns(), std::memory_order_seq_cst);
+  c->unlock();
+  // the chunk's first call: an idle flusher arms its window_us timer
+  if (first && a->flusher_idle.load(std::memory_order_seq_cst)) {
+    std::lock_guard<std::mutex> g(a->mu);
+    a->cv_flush.notify_one();
+  }
+  return 0;
 }
 
 int emqxgm_async_cancel(emqxgm_async_t* a, uint64_t tag, uint64_t owner) {
   if (!a || tag == EMQXGM_TAG_CANCELLED) return -EINVAL;
+  // staged calls first, without the layer's mutex (a producer holds its chunk's lock while it
+  // places the chunk, which may take the mutex).  A call only ever moves from a chunk into a
+  // window, under the chunk's lock: if this scan misses it, the window scan below finds it.
+  std::vector<Chunk*> cs;
+  {
+    std::lock_guard<std::mutex> g(a->mu);
+    for (auto& c : a->chunks) cs.push_back(c.get());
+  }
+  for (Chunk* c : cs) {
+    c->lock();
+    for (uint32_t j = 0; j < c->k; ++j)
+      if (c->tag[j] == tag && c->owner[j] == owner) {
+        c->tag[j] = EMQXGM_TAG_CANCELLED;  // still matched, never reported
+        c->unlock();
+        std::lock_guard<std::mutex> g(a->mu);
+        a->st_cancelled += 1;
+        return 1;
+      }
+    c->unlock();
+  }
   std::unique_lock<std::mutex> g(a->mu);
   int delivering = -1;
   for (size_t i = 0; i < a->slots.size() && delivering < 0; ++i) {
@@ -451,8 +631,19 @@ int emqxgm_async_cancel(emqxgm_async_t* a, uint64_t tag, uint64_t owner) {
 
 int emqxgm_async_stats(emqxgm_async_t* a, uint64_t out[8]) {
   if (!a || !out) return -EINVAL;
+  std::vector<Chunk*> cs;
+  {
+    std::lock_guard<std::mutex> g(a->mu);
+    for (auto& c : a->chunks) cs.push_back(c.get());
+  }
+  uint64_t calls = a->st_direct.load();
+  for (Chunk* c : cs) {  // (chunk locks never taken under the mutex: see cancel)
+    c->lock();
+    calls += c->accepted;
+    c->unlock();
+  }
   std::lock_guard<std::mutex> g(a->mu);
-  out[0] = a->st_calls.load();
+  out[0] = calls;
   out[1] = a->st_windows;
   out[2] = a->st_delivered;
   out[3] = a->st_busy.load();

@@ -871,6 +871,7 @@ void commit_stats(emqxgm* h, double ms, bool delta) {
   h->st.n_nodes = m.n_edges + 1;
   h->st.n_edges = m.n_edges;
   h->st.edge_slots = m.ecap;
+  h->st.keyed_nodes = (uint64_t)std::count(m.keyed.begin(), m.keyed.end(), (uint8_t)1);
   h->st.exact_slots = (m.xcap_p + m.xcap_w) * XBUCKET;
   h->st.max_depth = m.max_depth;
   h->st.device_bytes = m.ecap * SLOT_U4 * 16 + (m.xcap_p + m.xcap_w) * XBUCKET * XENT_U4 * 16 + m.tn_cap * 4 +

@@ -133,6 +133,7 @@ typedef struct emqxgm_stats {
   double tok_ms;            /* summed tokenizer-kernel time (HIP events), if profiling is on */
   uint64_t tok_launches;
   double exact_ms;          /* summed exact route-key probe time (k_exact; 0 without plain keys) */
+  uint64_t keyed_nodes;     /* trie nodes whose literal children are placed by token */
 } emqxgm_stats;
 
 int emqxgm_abi_version(void);

@@ -202,6 +202,7 @@ int main(int argc, char** argv) {
   const int handles = argc > 3 ? atoi(argv[3]) : 2;
   const uint32_t window = argc > 4 ? atoi(argv[4]) : 64;
   const uint64_t calls_per_thread = argc > 5 ? atoll(argv[5]) : 3000;
+  const uint32_t cancel_every = argc > 6 ? (uint32_t)atoi(argv[6]) : 17;  // 0: no cancels
   std::mt19937 rng(seed);
   // the index: random filters (trie + route keys) and some exact keys
   std::vector<uint8_t> fb;
@@ -257,6 +258,7 @@ int main(int argc, char** argv) {
   emqxgm_async_t* a = nullptr;
   CHECK(emqxgm_async_create(hs.data(), handles, &cfg, on_window, nullptr, &a) == 0, "create");
   std::atomic<uint64_t> accepted{0}, cancelled{0}, busy{0}, too_deep{0};
+  const auto t_start = std::chrono::steady_clock::now();
   std::vector<std::thread> th;
   for (int k = 0; k < threads; ++k) {
     th.emplace_back([&, k] {
@@ -282,7 +284,7 @@ int main(int argc, char** argv) {
         }
         CHECK(rc == 0, "async_match %d", rc);
         accepted++;
-        if (r() % 17 == 0) {  // a caller that gives up at once
+        if (cancel_every && r() % cancel_every == 0) {  // a caller that gives up at once
           // mark first: the callback must not report it once the cancel succeeds
           const int cr = emqxgm_async_cancel(a, tag, k);
           CHECK(cr == 0 || cr == 1, "cancel %d", cr);
@@ -315,6 +317,7 @@ int main(int argc, char** argv) {
   for (auto& e : engines) eb += e.busy.load();
   CHECK(eb == 0, "the layer overran a handle's pipes (%llu -EBUSY)", (unsigned long long)eb);
   ref_destroy(g_ref);
+  fprintf(stderr, "calls/s %.0f\n", accepted.load() / std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count());
   printf("OK %llu %llu %llu %llu %llu\n", (unsigned long long)accepted.load(),
          (unsigned long long)g_reported.load(), (unsigned long long)cancelled.load(),
          (unsigned long long)busy.load(), (unsigned long long)too_deep.load());

@@ -6,7 +6,8 @@
 #   tools/job.sh TAG STEP [STEP ...]
 #
 # steps:
-#   tests[=PYTEST_ARGS]     python -m pytest tests -m gpu (default: the whole GPU suite)
+#   tests[=PYTEST_ARGS]     python -m pytest tests -m gpu (default: the whole GPU suite); ARGS:
+#                           commas for spaces
 #   smoke                   __graft_entry__.smoke()
 #   bench=CFG[:TOPICS[:ARGS]]  bench.py --cfg CFG (default bench line, or --topics TOPICS);
 #                           ARGS: extra bench arguments, commas for spaces
@@ -35,7 +36,8 @@ KRE="k_walk|k_tok|k_exact|k_scatter|k_verify|k_scan"
 NOCPU="--no-cpu-baseline --no-e2e"
 
 step_tests() {
-  local args=${1:-tests -m gpu}
+  local args=${1:-tests,-m,gpu}
+  args=${args//,/ }
   (cd $R && timeout -k 10 1000 python -u -m pytest $args -x -v --timeout 300 --timeout-method thread) \
     > $O/pytest.log 2>&1
   local rc=$?
