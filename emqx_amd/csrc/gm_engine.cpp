@@ -945,10 +945,13 @@ int upload_model(emqxgm* h, TrieModel& m) {
 }
 
 // Token-keyed parents (gm_common.h edge_home) of a full build.  mode 1: parents with at least
-// KEYED_MIN_FANOUT literal children, every child token of which is the child of at most
-// EBUCKET such parents (their edges then share one bucket per token); mode 2 (tests): every
-// eligible parent; 0: none.  Never the root or a node reached by a '+' edge.
+// KEYED_MIN_FANOUT literal children, none of whose child tokens is the child of more than
+// KEYED_MAX_SHARE candidates and at most 1/16 of them of more than EBUCKET (their edges then
+// share one bucket per token; the few crowded tokens only lengthen their own chains -- on cfg3 the
+// device ids 0..9999 are also site numbers, children of `site`); mode 2 (tests): every eligible
+// parent; 0: none.  Never the root or a node reached by a '+' edge.
 constexpr uint32_t KEYED_MIN_FANOUT = 16;
+constexpr uint32_t KEYED_MAX_SHARE = 8;
 void select_keyed(TrieModel& m, uint32_t mode) {
   const size_t nn = m.parent.size();
   m.keyed.assign(nn, 0u);
@@ -967,21 +970,25 @@ void select_keyed(TrieModel& m, uint32_t mode) {
     if (m.tok[c] != PLUS_TOK && eligible(m.parent[c])) toks.push_back(m.tok[c]);
   if (toks.empty()) return;
   std::sort(toks.begin(), toks.end());
-  std::vector<uint64_t> crowded;  // tokens under more than EBUCKET candidates
+  std::vector<std::pair<uint64_t, uint32_t>> crowded;  // tokens under more than EBUCKET candidates
   for (size_t i = 0; i < toks.size();) {
     size_t j = i;
     while (j < toks.size() && toks[j] == toks[i]) ++j;
-    if (j - i > EBUCKET) crowded.push_back(toks[i]);
+    if (j - i > EBUCKET) crowded.emplace_back(toks[i], (uint32_t)std::min<size_t>(j - i, ~0u));
     i = j;
   }
+  std::vector<uint32_t> n_crowded(nn, 0);
   std::vector<uint8_t> ok(nn, 0);
   for (uint32_t x = 1; x < nn; ++x) ok[x] = eligible(x) ? 1 : 0;
   for (uint32_t c = 1; c < nn; ++c) {
     const uint32_t p = m.parent[c];
-    if (ok[p] && m.tok[c] != PLUS_TOK && std::binary_search(crowded.begin(), crowded.end(), m.tok[c]))
-      ok[p] = 0;
+    if (!ok[p] || m.tok[c] == PLUS_TOK) continue;
+    auto it = std::lower_bound(crowded.begin(), crowded.end(), std::make_pair(m.tok[c], 0u));
+    if (it == crowded.end() || it->first != m.tok[c]) continue;
+    if (it->second > KEYED_MAX_SHARE) ok[p] = 0;
+    else n_crowded[p] += 1;
   }
-  for (uint32_t x = 1; x < nn; ++x) m.keyed[x] = ok[x];
+  for (uint32_t x = 1; x < nn; ++x) m.keyed[x] = ok[x] && n_crowded[x] * 16 <= m.nlit[x];
 }
 
 // Full build of the device index from the pending registry; swaps it in and rebuilds the host

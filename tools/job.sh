@@ -13,9 +13,10 @@
 #                           ARGS: extra bench arguments, commas for spaces
 #   onepass=CFG             rocprofv3 --kernel-trace --stats over bench.py --no-pipeline (the
 #                           roofline's kernel time: one pass at a time)
-#   prof=CFG                rocprofv3 kernel stats + the PMC passes (one counter group per
+#   prof=CFG[:ARGS]         rocprofv3 kernel stats + the PMC passes (one counter group per
 #                           run: FETCH_SIZE; WRITE_SIZE + L2 hit/miss; TCP->TCC requests), then
-#                           tools/pmc_summary.py
+#                           tools/pmc_summary.py; ARGS: extra bench arguments, commas for spaces
+#                           (the output directories then carry them in their names)
 #   sq=CFG[:TOPICS]         PMC issue counters of k_walk (SQ_* groups)
 #   ab=SPECS/VARIANTS       A/B of engine builds build/lib_<V>.so (tools/ab_build.sh) against
 #                           the in-tree one, base first and last; SPECS "cfg:topics,..." (0 =
@@ -33,7 +34,7 @@ shift
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 KRE="k_walk|k_tok|k_exact|k_scatter|k_verify|k_scan"
-NOCPU="--no-cpu-baseline --no-e2e"
+NOCPU="--no-cpu-baseline --no-e2e --nif="
 
 step_tests() {
   local args=${1:-tests,-m,gpu}
@@ -67,20 +68,24 @@ step_onepass() {
 }
 
 step_prof() {
-  local c=$1 steps=5
+  local c=${1%%:*} extra= steps=5
+  [ "$1" != "$c" ] && extra=${1#*:}
+  local tag=${extra//[^a-zA-Z0-9=]/_}
+  local d=cfg$c${tag:+_$tag}
+  extra=${extra//,/ }
   [ $c = 3 ] && steps=10
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/stats_cfg$c -o run --output-format csv \
-    -- python3 $R/bench.py --cfg $c $NOCPU --steps $steps --warmup 2 \
-    > $O/stats_cfg$c.json 2> $O/stats_cfg$c.log || return 1
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/stats_$d -o run --output-format csv \
+    -- python3 $R/bench.py --cfg $c $NOCPU $extra --steps $steps --warmup 2 \
+    > $O/stats_$d.json 2> $O/stats_$d.log || return 1
   local i=0 grp
   for grp in "FETCH_SIZE" "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" \
              "TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TOTAL_CACHE_ACCESSES_sum"; do
     i=$((i+1))
-    timeout -s KILL 400 rocprofv3 --pmc $grp --kernel-include-regex "$KRE" -d $O/pmc_cfg$c/p$i -o run \
-      --output-format csv -- python3 $R/bench.py --cfg $c $NOCPU --steps 3 --warmup 1 \
-      > $O/pmc_cfg${c}_p$i.log 2>&1 || return 1
+    timeout -s KILL 400 rocprofv3 --pmc $grp --kernel-include-regex "$KRE" -d $O/pmc_$d/p$i -o run \
+      --output-format csv -- python3 $R/bench.py --cfg $c $NOCPU $extra --steps 3 --warmup 1 \
+      > $O/pmc_${d}_p$i.log 2>&1 || return 1
   done
-  python3 $R/tools/pmc_summary.py $O/pmc_cfg$c > $O/pmc_cfg${c}_summary.txt 2>&1
+  python3 $R/tools/pmc_summary.py $O/pmc_$d > $O/pmc_${d}_summary.txt 2>&1
 }
 
 step_sq() {
