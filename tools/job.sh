@@ -18,10 +18,13 @@
 #                           tools/pmc_summary.py; ARGS: extra bench arguments, commas for spaces
 #                           (the output directories then carry them in their names)
 #   sq=CFG[:TOPICS]         PMC issue counters of k_walk (SQ_* groups)
-#   ab=SPECS/VARIANTS       A/B of engine builds build/lib_<V>.so (tools/ab_build.sh) against
+#   ab=SPECS/VARIANTS       A/B of engine builds ablib/lib_<V>.so (tools/ab_build.sh) against
 #                           the in-tree one, base first and last; SPECS "cfg:topics,..." (0 =
 #                           default topics), VARIANTS "v1,v2"
 #   load=CFG[:FILTERS]      the concurrent publish entry's load (bench.py --only-nif)
+#   latency                 tools/latency_probe.hip (built on the box): the dependent-step floor
+#   winlat[=ARGS]           tools/window_latency.py (one window at a time), default copies and
+#                           again with HSA_ENABLE_SDMA=0 (blit-kernel copies); ARGS commas
 #   dist[=filters]          bench.py's N=2 path with two ranks sharing this box's one GPU over
 #                           gloo (RCCL refuses two ranks on one device): the control flow at full
 #                           size, not a timing; "filters" makes the filter-sharded layout the
@@ -104,17 +107,17 @@ step_sq() {
 
 step_ab() {
   local specs=${1%%/*} variants=${1#*/} V spec
-  cp $R/emqx_amd/libemqx_gpumatch.so $R/build/lib_base.so || return 1
+  cp $R/emqx_amd/libemqx_gpumatch.so $R/ablib/lib_base.so || return 1
   for V in base ${variants//,/ } base; do
-    cp $R/build/lib_$V.so $R/emqx_amd/libemqx_gpumatch.so || return 1
+    cp $R/ablib/lib_$V.so $R/emqx_amd/libemqx_gpumatch.so || return 1
     for spec in ${specs//,/ }; do
       local c=${spec%%:*} t=${spec##*:} T=""
       [ "$t" != 0 ] && T="--topics $t"
       (cd $R && timeout -k 10 300 python -u bench.py --cfg $c $T $NOCPU --steps 50 --warmup 5) \
-        > $O/${V}_c${c}_${t}.json 2> $O/${V}_c${c}_${t}.log || { cp $R/build/lib_base.so $R/emqx_amd/libemqx_gpumatch.so; return 1; }
+        > $O/${V}_c${c}_${t}.json 2> $O/${V}_c${c}_${t}.log || { cp $R/ablib/lib_base.so $R/emqx_amd/libemqx_gpumatch.so; return 1; }
     done
   done
-  cp $R/build/lib_base.so $R/emqx_amd/libemqx_gpumatch.so
+  cp $R/ablib/lib_base.so $R/emqx_amd/libemqx_gpumatch.so
   python3 $R/tools/ab_lib_summary.py $O > $O/ab_summary.txt 2>&1
 }
 
@@ -122,6 +125,21 @@ step_load() {
   local c=${1%%:*} f=
   [ "$1" != "$c" ] && f="--filters ${1#*:}"
   (cd $R && timeout -k 10 600 python -u bench.py --cfg $c $f --only-nif) > $O/load_c$c.json 2> $O/load_c$c.log
+}
+
+step_latency() {
+  hipcc --offload-arch=gfx950 -O3 $R/tools/latency_probe.hip -o $O/latency_probe || return 1
+  timeout -k 10 180 $O/latency_probe > $O/latency_probe.txt 2>&1
+  local rc=$?
+  rm -f $O/latency_probe
+  cat $O/latency_probe.txt
+  return $rc
+}
+
+step_winlat() {
+  local extra=${1//,/ }
+  (cd $R && timeout -k 10 300 python -u tools/window_latency.py $extra) > $O/winlat.json 2> $O/winlat.log || return 1
+  (cd $R && HSA_ENABLE_SDMA=0 timeout -k 10 300 python -u tools/window_latency.py $extra) > $O/winlat_nosdma.json 2> $O/winlat_nosdma.log
 }
 
 step_dist() {
