@@ -187,6 +187,7 @@ struct Epoch {
   std::atomic<uint32_t> walk_level{WALK_SHALLOW};
   std::atomic<uint32_t> census_level{WALK_SHALLOW};  // the same for diagnostic census passes
                                                       // (their unpruned walks stack deeper)
+  std::atomic<bool> ready_seen{false};  // `ready` has completed (a pass then skips its query)
   ~Epoch() {
     if (ready) (void)hipEventDestroy(ready);
   }
@@ -485,6 +486,7 @@ struct emqxgm {
     // emqxgm_match_batch_submit_filters: the gather and every copy were enqueued behind the
     // pass, sized by the estimates below; the wait then takes one stream synchronisation
     bool fb_async = false;
+    bool rows_enq = false;  // the submit enqueued the row pointers' copy into h_row
     uint64_t fb_pairs_copy = 0, fb_bytes_copy = 0;  // pairs / bytes the packed block holds
     Pinned h_blk;                                   // the packed block (FbLayout)
     bool fb_fast = false;                           // the last completion came from the block
@@ -1692,7 +1694,12 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
   DevIndex ix = E.ix;
   ix.leafp_mask = h->leafp_mask;
   // the epoch's uploads / patches must have landed (a full build's have: its wait is skipped)
-  if (hipEventQuery(E.ready) != hipSuccess) HIPCHK(h, hipStreamWaitEvent(st, E.ready, 0));
+  if (!E.ready_seen.load(std::memory_order_relaxed)) {
+    if (hipEventQuery(E.ready) == hipSuccess)
+      const_cast<Epoch&>(E).ready_seen.store(true, std::memory_order_relaxed);
+    else
+      HIPCHK(h, hipStreamWaitEvent(st, E.ready, 0));
+  }
   if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[0], st));
   RoctxRange rr(h->roctx, census ? "emqxgm.pass.census" : "emqxgm.pass");
   bool ctl_sent = false;  // the control words already go to the host mirror
@@ -2073,11 +2080,11 @@ int host_pipe_reserve(emqxgm* h, emqxgm::HostPipe& p, uint64_t n, uint64_t bytes
 // PCIe for them -- a 4M-topic batch's 16 MB).
 int host_pipe_copy_out(emqxgm* h, emqxgm::HostPipe& p) {
   const Scratch& s = p.c.sc;
-  void *dr = nullptr, *de = nullptr, *df = nullptr;
-  HIPCHK(h, hipHostGetDevicePointer(&dr, p.h_row, 0));
-  HIPCHK(h, hipHostGetDevicePointer(&de, p.h_exact, 0));
-  HIPCHK(h, hipHostGetDevicePointer(&df, p.h_fid, 0));
   if (h->host_out_mode == 1) {
+    void *dr = nullptr, *de = nullptr, *df = nullptr;
+    HIPCHK(h, hipHostGetDevicePointer(&dr, p.h_row, 0));
+    HIPCHK(h, hipHostGetDevicePointer(&de, p.h_exact, 0));
+    HIPCHK(h, hipHostGetDevicePointer(&df, p.h_fid, 0));
     CopyOut a{s.row, (uint32_t*)dr, p.n + 1, nullptr, p.n + 1};
     CopyOut b{s.exact_id, (uint32_t*)de, p.n, nullptr, p.n};
     CopyOut f{s.out, (uint32_t*)df, 0, s.ctl + CTL_TOTAL, (uint32_t)std::min<uint64_t>(p.fid_cap, s.p_cap)};
@@ -2132,18 +2139,20 @@ int host_pipe_complete(emqxgm* h, emqxgm::HostPipe& p, bool gather = false) {
   HIPCHK(h, hipStreamSynchronize(p.c.stream));
   bool legacy = false;
   int rc = pass_check(h, p.c, p.n, p.bytes_len, 0, legacy);
-  // copy_out enqueued the row pointers behind the pass (both modes), the copy kernel (mode 1)
-  // the exact ids and up to fid_cap filter ids too; a redone pass copies everything here
-  bool rows_copied = true;
+  // copy_out enqueued the row pointers behind the pass (both modes; with the gather behind the
+  // pass they travel in its block instead), the copy kernel (mode 1) the exact ids and up to
+  // fid_cap filter ids too; a redone pass copies everything here
+  bool rows_copied = p.rows_enq, redone = false;
   if (rc == 0) {
     rc = pass_finish(h, p.c, p.n, false, &p.pairs, nullptr);
   } else if (rc == 1) {
     rc = run_device(h, p.c, p.d_bytes, p.d_off, p.n, p.bytes_len, &p.pairs);
     rows_copied = false;
+    redone = true;
   }
   // submitted with the gather behind the pass: done when its copies covered the window
   const uint32_t blk_total = p.fb_async ? *(const uint32_t*)p.h_blk.p : 0u;
-  const bool async_done = rc == 0 && gather && p.fb_async && rows_copied &&
+  const bool async_done = rc == 0 && gather && p.fb_async && !redone &&
                           p.pairs <= p.fb_pairs_copy && blk_total <= p.fb_bytes_copy;
   if (async_done) p.fb_bytes = p.pairs ? blk_total : 0;
   p.fb_fast = async_done;
@@ -3085,8 +3094,11 @@ int batch_submit(emqxgm* h, const uint8_t* bytes, const uint32_t* offsets, uint3
   } else {
     if (nb) HIPCHK(h, hipMemcpyAsync(p.d_bytes, bytes, nb, hipMemcpyHostToDevice, p.c.stream));
     HIPCHK(h, hipMemcpyAsync(p.d_off, offsets, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, p.c.stream));
+    // with the gather behind the pass the row pointers travel in its block (one copy less)
+    p.rows_enq = !want_fb || h->host_out_mode == 1;
     if ((rc = pass_submit(h, p.c, p.d_bytes, p.d_off, n, false, false)) ||
-        (rc = host_pipe_copy_out(h, p)) || (want_fb && (rc = host_pipe_enqueue_gather(h, p))))
+        (p.rows_enq && (rc = host_pipe_copy_out(h, p))) ||
+        (want_fb && (rc = host_pipe_enqueue_gather(h, p))))
       return rc;
     if (!p.fin) HIPCHK(h, hipEventCreateWithFlags(&p.fin, hipEventDisableTiming));
     HIPCHK(h, hipEventRecord(p.fin, p.c.stream));
@@ -3129,8 +3141,8 @@ int host_pipe_enqueue_gather(emqxgm* h, emqxgm::HostPipe& p) {
   const uint32_t* npairs = s.ctl + CTL_TOTAL;  // written by the pass's scan
   hipStream_t st = p.c.stream;
   HIPCHK(h, launch_filter_len_dev(s.out, npairs, cap, ix.foff, len, ooff, tmp, total, st));
-  HIPCHK(h, launch_fb_pack(s.out, npairs, ix.foff, ix.fbytes, ooff, total, s.exact_id, p.n, want_p,
-                           want_b, block, st));
+  HIPCHK(h, launch_fb_pack(s.out, npairs, ix.foff, ix.fbytes, ooff, total, s.exact_id, s.row, p.n,
+                           want_p, want_b, block, st));
   HIPCHK(h, hipMemcpyAsync(p.h_blk.p, block, (size_t)blk, hipMemcpyDeviceToHost, st));
   p.fb_pairs_copy = want_p;
   p.fb_bytes_copy = want_b;
@@ -3214,6 +3226,7 @@ int emqxgm_match_batch_wait_filters(emqxgm_t* h, uint64_t ticket, emqxgm_batch_o
   if (p.fb_fast) {  // one block: FbLayout for the pipe's n and copy sizes
     const FbLayout L(p.n, (uint32_t)p.fb_pairs_copy);
     const uint8_t* b = (const uint8_t*)p.h_blk.p;
+    out->row_ptr = (const uint32_t*)(b + L.row);
     out->filter_id = (const uint32_t*)(b + L.fid);
     out->exact_id = (const uint32_t*)(b + L.exact);
     *foff = (const uint32_t*)(b + L.ooff);

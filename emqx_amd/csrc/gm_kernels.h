@@ -280,20 +280,22 @@ hipError_t launch_filter_len_dev(const uint32_t* fid, const uint32_t* pairs_dev,
 // A host window's whole result packed into one block (one D2H copy): byte offsets of the
 // block's parts for n topics and up to cap_p pairs; the filter bytes follow at `bytes`.
 struct FbLayout {
-  uint64_t total = 0, ooff, fid, exact, bytes;
+  uint64_t total = 0, ooff, fid, exact, row, bytes;
   FbLayout(uint32_t n, uint32_t cap_p) {
     ooff = 16;
     fid = (ooff + 4ull * (cap_p + 1) + 15) & ~15ull;
     exact = (fid + 4ull * cap_p + 15) & ~15ull;
-    bytes = (exact + 4ull * n + 15) & ~15ull;
+    row = (exact + 4ull * n + 15) & ~15ull;
+    bytes = (row + 4ull * (n + 1) + 15) & ~15ull;
   }
 };
-// {byte total, byte offsets, filter ids, exact ids, bytes} of a pass into `block` (FbLayout),
-// its pair count read on the device; beyond cap_p pairs or cap_b bytes only the total is written.
+// {byte total, byte offsets, filter ids, exact ids, row pointers, bytes} of a pass into `block`
+// (FbLayout), its pair count read on the device; beyond cap_p pairs or cap_b bytes only the total
+// is written.
 hipError_t launch_fb_pack(const uint32_t* fid, const uint32_t* pairs_dev, const uint64_t* foff,
                           const uint8_t* pool, const uint32_t* ooff, const uint32_t* total,
-                          const uint32_t* exact, uint32_t n, uint32_t cap_p, uint64_t cap_b,
-                          uint8_t* block, hipStream_t s);
+                          const uint32_t* exact, const uint32_t* row, uint32_t n, uint32_t cap_p,
+                          uint64_t cap_b, uint8_t* block, hipStream_t s);
 // out[i] = base + row[i], i < m (u64 CSR row pointers of the host API, built on the device)
 hipError_t launch_row64(const uint32_t* row, uint64_t base, uint64_t* out, uint32_t m,
                         hipStream_t s);

@@ -434,12 +434,14 @@ struct FbPack {
   const uint32_t* ooff;   // the scan of the pairs' filter lengths (pairs + 1 entries)
   const uint32_t* total;  // bytes of all pairs
   const uint32_t* exact;
+  const uint32_t* row;    // the pass's row pointers (n + 1)
   uint32_t n, cap_p;
   uint64_t cap_b;
   uint32_t* b_total;
   uint32_t* b_ooff;
   uint32_t* b_fid;
   uint32_t* b_exact;
+  uint32_t* b_row;
   uint8_t* b_bytes;
 };
 
@@ -447,9 +449,10 @@ __global__ __launch_bounds__(WG) void k_fb_pack(FbPack A) {
   const uint32_t pairs = *A.pairs_dev, total = *A.total;
   if (blockIdx.x == 0 && threadIdx.x == 0) *A.b_total = total;
   if (pairs > A.cap_p || total > A.cap_b) return;
-  const uint32_t m = max(pairs + 1, A.n);
+  const uint32_t m = max(pairs, A.n) + 1;
   for (uint32_t i = blockIdx.x * WG + threadIdx.x; i < m; i += gridDim.x * WG) {
     if (i < A.n) A.b_exact[i] = A.exact[i];
+    if (i <= A.n) A.b_row[i] = A.row[i];
     if (i <= pairs) A.b_ooff[i] = A.ooff[i];
     if (i < pairs) {
       const uint32_t f = A.fid[i], o = A.ooff[i];
@@ -846,8 +849,8 @@ hipError_t launch_filter_gather(const uint32_t* fid, uint32_t pairs, const uint6
 
 hipError_t launch_fb_pack(const uint32_t* fid, const uint32_t* pairs_dev, const uint64_t* foff,
                           const uint8_t* pool, const uint32_t* ooff, const uint32_t* total,
-                          const uint32_t* exact, uint32_t n, uint32_t cap_p, uint64_t cap_b,
-                          uint8_t* block, hipStream_t s) {
+                          const uint32_t* exact, const uint32_t* row, uint32_t n, uint32_t cap_p,
+                          uint64_t cap_b, uint8_t* block, hipStream_t s) {
   const FbLayout L(n, cap_p);
   FbPack a;
   a.fid = fid;
@@ -857,6 +860,7 @@ hipError_t launch_fb_pack(const uint32_t* fid, const uint32_t* pairs_dev, const 
   a.ooff = ooff;
   a.total = total;
   a.exact = exact;
+  a.row = row;
   a.n = n;
   a.cap_p = cap_p;
   a.cap_b = cap_b;
@@ -864,8 +868,9 @@ hipError_t launch_fb_pack(const uint32_t* fid, const uint32_t* pairs_dev, const 
   a.b_ooff = (uint32_t*)(block + L.ooff);
   a.b_fid = (uint32_t*)(block + L.fid);
   a.b_exact = (uint32_t*)(block + L.exact);
+  a.b_row = (uint32_t*)(block + L.row);
   a.b_bytes = block + L.bytes;
-  hipLaunchKernelGGL(k_fb_pack, dim3(grid_for(std::max<uint32_t>(cap_p + 1, n), 2048)), dim3(WG), 0, s, a);
+  hipLaunchKernelGGL(k_fb_pack, dim3(grid_for(std::max<uint32_t>(cap_p, n) + 1, 2048)), dim3(WG), 0, s, a);
   return hipGetLastError();
 }
 

@@ -23,8 +23,10 @@
 #                           default topics), VARIANTS "v1,v2"
 #   load=CFG[:FILTERS]      the concurrent publish entry's load (bench.py --only-nif)
 #   latency                 tools/latency_probe.hip (built on the box): the dependent-step floor
-#   winlat[=ARGS]           tools/window_latency.py (one window at a time), default copies and
-#                           again with HSA_ENABLE_SDMA=0 (blit-kernel copies); ARGS commas
+#   winlat[=ARGS]           tools/window_latency.py (one window at a time); ARGS commas (r04:
+#                           HSA_ENABLE_SDMA=0, blit-kernel copies, was slower: profiles/r04/latency)
+#   wintrace[=ARGS]         rocprofv3 kernel + memory-copy + HIP runtime traces of
+#                           tools/window_latency.py (the timeline of one window at a time)
 #   dist[=filters]          bench.py's N=2 path with two ranks sharing this box's one GPU over
 #                           gloo (RCCL refuses two ranks on one device): the control flow at full
 #                           size, not a timing; "filters" makes the filter-sharded layout the
@@ -138,8 +140,14 @@ step_latency() {
 
 step_winlat() {
   local extra=${1//,/ }
-  (cd $R && timeout -k 10 300 python -u tools/window_latency.py $extra) > $O/winlat.json 2> $O/winlat.log || return 1
-  (cd $R && HSA_ENABLE_SDMA=0 timeout -k 10 300 python -u tools/window_latency.py $extra) > $O/winlat_nosdma.json 2> $O/winlat_nosdma.log
+  (cd $R && timeout -k 10 300 python -u tools/window_latency.py $extra) > $O/winlat.json 2> $O/winlat.log
+}
+
+step_wintrace() {
+  local extra=${1//,/ }
+  timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace --hip-runtime-trace -d $O/wintrace \
+    -o run --output-format csv -- python3 $R/tools/window_latency.py $extra \
+    > $O/wintrace.json 2> $O/wintrace.log
 }
 
 step_dist() {
