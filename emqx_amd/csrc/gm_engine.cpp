@@ -3140,7 +3140,8 @@ int host_pipe_enqueue_gather(emqxgm* h, emqxgm::HostPipe& p) {
   uint8_t* block = (uint8_t*)p.d_fb.p + at;
   const uint32_t* npairs = s.ctl + CTL_TOTAL;  // written by the pass's scan
   hipStream_t st = p.c.stream;
-  HIPCHK(h, launch_filter_len_dev(s.out, npairs, cap, ix.foff, len, ooff, tmp, total, st));
+  // (sized by the block's pair capacity: a window with more pairs is finished in the wait)
+  HIPCHK(h, launch_filter_len_dev(s.out, npairs, want_p, ix.foff, len, ooff, tmp, total, st));
   HIPCHK(h, launch_fb_pack(s.out, npairs, ix.foff, ix.fbytes, ooff, total, s.exact_id, s.row, p.n,
                            want_p, want_b, block, st));
   HIPCHK(h, hipMemcpyAsync(p.h_blk.p, block, (size_t)blk, hipMemcpyDeviceToHost, st));

@@ -492,7 +492,9 @@ hipError_t launch_scan_ctl(const uint32_t* in, uint32_t* out, uint32_t n, uint32
                            hipStream_t s) {
   const uint32_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
   if (nb == 0) return hipErrorInvalidValue;  // a pass has topics
-  hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(WG), 0, s, in, n, tmp, (const uint32_t*)nullptr);
+  // one tile: k_scan_final's block 0 needs no partials (a launch less for small windows)
+  if (nb > 1)
+    hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(WG), 0, s, in, n, tmp, (const uint32_t*)nullptr);
   hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(WG), 0, s, in, n, tmp, nb, out, total_dst,
                      (const uint32_t*)nullptr, ctl, ctl_host_dev);
   return hipGetLastError();
@@ -507,7 +509,8 @@ hipError_t launch_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* 
     if (e == hipSuccess && total_dst) e = hipMemsetAsync(total_dst, 0, 4, s);
     return e;
   }
-  hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(WG), 0, s, in, n, tmp, (const uint32_t*)nullptr);
+  if (nb > 1)
+    hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(WG), 0, s, in, n, tmp, (const uint32_t*)nullptr);
   hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(WG), 0, s, in, n, tmp, nb, out, total_dst,
                      (const uint32_t*)nullptr);
   return hipGetLastError();
@@ -832,7 +835,8 @@ hipError_t launch_filter_len_dev(const uint32_t* fid, const uint32_t* pairs_dev,
   const uint32_t c = std::max<uint32_t>(cap, 1);
   hipLaunchKernelGGL(k_filter_len, dim3(grid_for(c, 1024)), dim3(WG), 0, s, fid, c, foff, len, pairs_dev);
   const uint32_t nb = (c + SCAN_TILE - 1) / SCAN_TILE;
-  hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(WG), 0, s, (const uint32_t*)len, c, tmp, pairs_dev);
+  if (nb > 1)
+    hipLaunchKernelGGL(k_scan_partials, dim3(nb), dim3(WG), 0, s, (const uint32_t*)len, c, tmp, pairs_dev);
   hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(WG), 0, s, (const uint32_t*)len, c, (const uint32_t*)tmp,
                      nb, ooff, total, pairs_dev);
   return hipGetLastError();
