@@ -30,7 +30,7 @@ import emqx_amd  # noqa: E402
 from emqx_amd import engine as E  # noqa: E402
 import workloads  # noqa: E402
 
-sizes = [int(x) for x in a.sizes.split(",")]
+sizes = [int(x) for x in a.sizes.replace(":", ",").split(",")]  # (":" for tools/job.sh)
 w = workloads.generate(3, a.filters, max(sizes) * 4)
 eng = emqx_amd.Engine()
 for kv in a.tune:
