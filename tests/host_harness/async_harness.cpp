@@ -119,6 +119,15 @@ int emqxgm_match_batch_submit_filters(emqxgm_t* h, const uint8_t* bytes, const u
   return 0;
 }
 
+}  // extern "C"
+// the layer's window submit (gm_engine.cpp skips the offsets check there; the mock checks them)
+int gm_submit_window(emqxgm_t* h, const uint8_t* bytes, const uint32_t* off, uint32_t n,
+                     uint64_t* ticket) {
+  for (uint32_t i = 0; i < n; ++i) CHECK(off[i + 1] >= off[i], "window offsets increase");
+  return emqxgm_match_batch_submit_filters(h, bytes, off, n, ticket);
+}
+extern "C" {
+
 int emqxgm_match_batch_wait_filters(emqxgm_t* h, uint64_t ticket, emqxgm_batch_out* out,
                                     const uint32_t** foff, const uint8_t** fbytes) {
   // the "device" takes a while; the layer must not hold its own lock meanwhile
