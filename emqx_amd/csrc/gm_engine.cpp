@@ -207,6 +207,10 @@ struct PassCtx {
   bool own_stream = false;    // false: the stream is one of the handle's shared pipe streams
   uint32_t walk_level = 0;    // walk variant of that pass (WalkLevel)
   bool census = false;        // that pass was a census pass
+  // copy-through input of the next pass enqueued here (pinned host memory, k_tok's TokArgs);
+  // cleared by the enqueue
+  const uint8_t* src_bytes = nullptr;
+  const uint32_t* src_off = nullptr;
 };
 
 constexpr uint64_t DEAD = ~0ull;  // TrieModel::slot of the root and of removed nodes
@@ -487,6 +491,7 @@ struct emqxgm {
     // pass, sized by the estimates below; the wait then takes one stream synchronisation
     bool fb_async = false;
     bool rows_enq = false;  // the submit enqueued the row pointers' copy into h_row
+    bool zc = false;        // this submit's input / result block went without DMA copies
     uint64_t fb_pairs_copy = 0, fb_bytes_copy = 0;  // pairs / bytes the packed block holds
     Pinned h_blk;                                   // the packed block (FbLayout)
     bool fb_fast = false;                           // the last completion came from the block
@@ -501,6 +506,10 @@ struct emqxgm {
   // memory over PCIe.  Measured on cfg3 (profiles/r02/pcie_e2e.json): 1.24 vs 1.02 G topics/s
   // host-in/host-out -- the kernel's PCIe writes contend with the uploads
   uint32_t host_out_mode = 0;
+  // windows of the concurrent entry up to this many topics (and 8 MiB of topic bytes) go
+  // without DMA copies: k_tok reads the pinned window itself (copy-through) and k_fb_pack writes
+  // the result block into pinned memory (emqxgm_tune "zc_topics"; 0: always DMA)
+  uint32_t zc_topics = 65536;
   uint64_t xrange_bytes = 0;  // emqxgm_tune("exact_range_kb")
 
   // ---- delta commits (writer side) ----
@@ -1719,7 +1728,9 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
   uint32_t claim0[WALK_SHARDS] = {};
   if (!ix.trie_empty) walk_claim_init(h->geom, n, c.walk_level, claim0);
   HIPCHK(h, launch_tok(d_bytes, d_off, n, ix, s, st, stat * STAGE_CHUNK,
-                       !ix.trie_empty && (ix.needs_verify || legacy), claim0));
+                       !ix.trie_empty && (ix.needs_verify || legacy), claim0, c.src_bytes, c.src_off));
+  c.src_bytes = nullptr;
+  c.src_off = nullptr;
   if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[4], st));
   roctx_mark(h->roctx, "k_exact");
   HIPCHK(h, launch_exact(d_bytes, d_off, n, ix, s, h->geom, st));
@@ -3089,12 +3100,26 @@ int batch_submit(emqxgm* h, const uint8_t* bytes, const uint32_t* offsets, uint3
   p.bytes_len = nb;
   p.pairs = 0;
   p.fb_async = false;
+  // small windows of pinned memory (the concurrent entry's): no DMA copies (PassCtx src_*)
+  p.zc = false;
+  if (trusted && want_fb && n && n <= h->zc_topics && nb <= (8u << 20) && h->host_out_mode == 0 &&
+      !((uintptr_t)bytes & 15u)) {
+    void *db = nullptr, *doff = nullptr;
+    p.zc = hipHostGetDevicePointer(&db, (void*)bytes, 0) == hipSuccess &&
+           hipHostGetDevicePointer(&doff, (void*)offsets, 0) == hipSuccess && db && doff;
+    if (p.zc) {
+      p.c.src_bytes = (const uint8_t*)db;
+      p.c.src_off = (const uint32_t*)doff;
+    }
+  }
   if (n == 0) {
     p.h_row[0] = 0;
     p.state = 2;
   } else {
-    if (nb) HIPCHK(h, hipMemcpyAsync(p.d_bytes, bytes, nb, hipMemcpyHostToDevice, p.c.stream));
-    HIPCHK(h, hipMemcpyAsync(p.d_off, offsets, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, p.c.stream));
+    if (!p.zc) {
+      if (nb) HIPCHK(h, hipMemcpyAsync(p.d_bytes, bytes, nb, hipMemcpyHostToDevice, p.c.stream));
+      HIPCHK(h, hipMemcpyAsync(p.d_off, offsets, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, p.c.stream));
+    }
     // with the gather behind the pass the row pointers travel in its block (one copy less)
     p.rows_enq = !want_fb || h->host_out_mode == 1;
     if ((rc = pass_submit(h, p.c, p.d_bytes, p.d_off, n, false, false)) ||
@@ -3139,13 +3164,17 @@ int host_pipe_enqueue_gather(emqxgm* h, emqxgm::HostPipe& p) {
   uint32_t* total = ooff + cap + 1;
   uint32_t* tmp = total + 2;
   uint8_t* block = (uint8_t*)p.d_fb.p + at;
+  // a small window's block goes straight into the pinned buffer (no D2H copy behind the pass)
+  void* hb = nullptr;
+  const bool direct = p.zc && hipHostGetDevicePointer(&hb, p.h_blk.p, 0) == hipSuccess && hb;
+  if (direct) block = (uint8_t*)hb;
   const uint32_t* npairs = s.ctl + CTL_TOTAL;  // written by the pass's scan
   hipStream_t st = p.c.stream;
   // (sized by the block's pair capacity: a window with more pairs is finished in the wait)
   HIPCHK(h, launch_filter_len_dev(s.out, npairs, want_p, ix.foff, len, ooff, tmp, total, st));
   HIPCHK(h, launch_fb_pack(s.out, npairs, ix.foff, ix.fbytes, ooff, total, s.exact_id, s.row, p.n,
                            want_p, want_b, block, st));
-  HIPCHK(h, hipMemcpyAsync(p.h_blk.p, block, (size_t)blk, hipMemcpyDeviceToHost, st));
+  if (!direct) HIPCHK(h, hipMemcpyAsync(p.h_blk.p, block, (size_t)blk, hipMemcpyDeviceToHost, st));
   p.fb_pairs_copy = want_p;
   p.fb_bytes_copy = want_b;
   p.fb_async = true;
@@ -3603,6 +3632,12 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
     if (value < 0 || value > 1) return -EINVAL;
     std::lock_guard<std::mutex> g(h->mmu);
     h->leafp_mask = value ? CF_HMASK : 0u;
+    return 0;
+  }
+  if (strcmp(key, "zc_topics") == 0) {  // concurrent-entry windows without DMA copies: max topics
+    if (value < 0) return -EINVAL;
+    std::lock_guard<std::mutex> g(h->mmu);
+    h->zc_topics = (uint32_t)value;
     return 0;
   }
   if (strcmp(key, "host_out") == 0) {  // host pipes' result copy: 0 hipMemcpyAsync (default), 1 kernel

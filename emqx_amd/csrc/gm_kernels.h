@@ -147,10 +147,13 @@ hipError_t launch_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* 
 uint32_t scan_tmp_words(uint32_t n);
 // tokenise: levels (nw), 64-B topic records (rec: first REC_TOKS tokens inline), tokens of
 // deeper levels (wh, at off[t] + t + level); exact route-key ids (exact_id, NONE if absent)
-// of wildcard names when there are no plain keys, else X_WILDPEND marks for launch_exact
+// of wildcard names when there are no plain keys, else X_WILDPEND marks for launch_exact.
+// src_bytes / src_off (copy-through, TokArgs): the input is read there (pinned host memory) and
+// stored into bytes / off, the pass's device buffers.
 hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
                       Scratch& sc, hipStream_t s, uint32_t pair_top0, bool zero_rej,
-                      const uint32_t* claim0 = nullptr);
+                      const uint32_t* claim0 = nullptr, const uint8_t* src_bytes = nullptr,
+                      const uint32_t* src_off = nullptr);
 // exact route-key ids of every name (after launch_tok; a no-op when there are no plain keys)
 hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
                         Scratch& sc, const WalkGeom& g, hipStream_t s);

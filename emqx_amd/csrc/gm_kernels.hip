@@ -532,9 +532,13 @@ static ExactArgs exact_args(const DevIndex& ix, uint32_t xseq) {
 
 hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
                       Scratch& sc, hipStream_t s, uint32_t pair_top0, bool zero_rej,
-                      const uint32_t* claim0) {
+                      const uint32_t* claim0, const uint8_t* src_bytes, const uint32_t* src_off) {
   if (n == 0) return hipSuccess;
   TokArgs a;
+  a.cp_bytes = src_bytes ? const_cast<uint8_t*>(bytes) : nullptr;
+  a.cp_off = src_off ? const_cast<uint32_t*>(off) : nullptr;
+  if (src_bytes) bytes = src_bytes;
+  if (src_off) off = src_off;
   for (uint32_t cs = 0; cs < WALK_SHARDS; ++cs) a.claim0[cs] = claim0 ? claim0[cs] : 0u;
   a.pair_top0 = pair_top0;
   a.rej = zero_rej ? sc.rej : nullptr;

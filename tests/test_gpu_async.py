@@ -263,3 +263,51 @@ def test_async_load_cfg3_slice_every_call(emqx):
     r = publishers.run([eng], w.tbytes, w.toff.astype(np.uint64), 64, 4096, 6_000, 65536,
                        record=True)
     _check_load(r, want)
+
+
+def test_async_copy_through_long_and_odd_topics(emqx):
+    """Windows of the concurrent entry go without DMA copies (k_tok reads the pinned window and
+    stores the device copies the later kernels read; k_fb_pack writes the result block into
+    pinned memory): topics long enough that a tile does not fit k_tok's LDS (the per-lane path
+    copies them), a 65,535-byte topic, empty levels, '$' names -- every call's answer equals the
+    host API's (DMA path) and, with copy-through off (zc_topics 0), the same."""
+    w, (eng,) = _cfg1(emqx, nt=2_000)
+    rng = random.Random(5)
+    words = [w.topic(i).split(b"/") for i in range(200)]
+    topics = []
+    for i in range(600):
+        base = list(rng.choice(words))
+        if i % 3 == 0:  # long levels: a tile of these outgrows the LDS buffer
+            base = base + [b"x" * rng.randint(80, 400) for _ in range(rng.randint(1, 3))]
+        elif i % 7 == 0:
+            base = [b"$SYS"] + base
+        elif i % 11 == 0:
+            base = base[:1] + [b""] + base[1:]
+        topics.append(b"/".join(base))
+    topics.append(b"a/" + b"b" * 65533)
+    topics.append(b"")
+    want = eng.match(topics)
+    flt = {}
+
+    def answer(am, owner):
+        for i, t in enumerate(topics):
+            while True:
+                rc = am.match(t, i, owner=owner)
+                if rc != -16:
+                    break
+                time.sleep(0.0002)
+            assert rc == 0, (i, rc)
+        assert am.wait([(i, owner) for i in range(len(topics))], timeout=60)
+        return {i: sorted(am.results[(i, owner)].filters) for i in range(len(topics))}
+
+    for zc in (65536, 0):
+        eng.tune("zc_topics", zc)
+        am = emqx.AsyncMatcher([eng], window_topics=256, window_bytes=1 << 20, window_us=200,
+                               max_levels=4096)
+        got = answer(am, 7)
+        am.close()
+        for i in range(len(topics)):
+            ids = want.row(i)
+            exp = sorted(flt.setdefault(int(f), eng.filter_bytes(int(f))) for f in ids)
+            assert got[i] == exp, (zc, i, topics[i][:80])
+    eng.tune("zc_topics", 65536)
