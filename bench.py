@@ -50,6 +50,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--settle-s", type=float, default=0.5,
+                    help="untimed steps for this long before the warmup steps: the GPU's clocks "
+                         "ramp over ~100 ms of load (r04: 20 timed steps after 5 warmup steps "
+                         "ran 6%% slower than after 300), 0 = none")
     ap.add_argument("--cfg", type=int, default=3)
     ap.add_argument("--filters", type=int, default=None)
     ap.add_argument("--topics", type=int, default=None, help="topics per GPU batch")
@@ -191,6 +195,13 @@ def main():
     def step():
         return step_pipe() if pipelined else step_sync()
 
+    # settle: untimed steps until the GPU runs at its loaded clocks (then the W warmup steps)
+    settle_steps = 0
+    t_settle = time.perf_counter()
+    while time.perf_counter() - t_settle < args.settle_s:
+        step()
+        settle_steps += 1
+    drain()
     for _ in range(args.warmup):
         step()
     drain()
@@ -363,6 +374,7 @@ def main():
                                         for k, v in census["loads_by_level"].items()},
                 "pipeline_ms_per_batch": round(pipe_ms, 4),
                 "tune": args.tune,
+                "settle": {"seconds": args.settle_s, "untimed_steps": settle_steps},
                 "passes_in_flight": dev_inflight if pipelined else 1,
                 "one_pass_at_a_time": (None if sync_ms is None else {
                     "value": round(topics_total / (sync_ms * 1e-3), 1), "ms_per_step": round(sync_ms, 4)}),

@@ -506,9 +506,10 @@ struct emqxgm {
   // memory over PCIe.  Measured on cfg3 (profiles/r02/pcie_e2e.json): 1.24 vs 1.02 G topics/s
   // host-in/host-out -- the kernel's PCIe writes contend with the uploads
   uint32_t host_out_mode = 0;
-  // windows of the concurrent entry up to this many topics (and 8 MiB of topic bytes) go
-  // without DMA copies: k_tok reads the pinned window itself (copy-through) and k_fb_pack writes
-  // the result block into pinned memory (emqxgm_tune "zc_topics"; 0: always DMA)
+  // host windows with the filter-byte gather (emqxgm_match_batch_submit_filters: the concurrent
+  // entry's, the batcher's) of up to this many topics (and 8 MiB of topic bytes) in pinned memory
+  // go without DMA copies: k_tok reads the window itself (copy-through) and k_fb_pack writes the
+  // result block into pinned memory (emqxgm_tune "zc_topics"; 0: always DMA)
   uint32_t zc_topics = 65536;
   uint64_t xrange_bytes = 0;  // emqxgm_tune("exact_range_kb")
 
@@ -3100,9 +3101,10 @@ int batch_submit(emqxgm* h, const uint8_t* bytes, const uint32_t* offsets, uint3
   p.bytes_len = nb;
   p.pairs = 0;
   p.fb_async = false;
-  // small windows of pinned memory (the concurrent entry's): no DMA copies (PassCtx src_*)
+  // small windows in pinned (device-mapped) memory -- the concurrent entry's, a batcher's: no
+  // DMA copies (PassCtx src_*); pageable memory has no device pointer and takes the copies
   p.zc = false;
-  if (trusted && want_fb && n && n <= h->zc_topics && nb <= (8u << 20) && h->host_out_mode == 0 &&
+  if (want_fb && n && n <= h->zc_topics && nb <= (8u << 20) && h->host_out_mode == 0 &&
       !((uintptr_t)bytes & 15u)) {
     void *db = nullptr, *doff = nullptr;
     p.zc = hipHostGetDevicePointer(&db, (void*)bytes, 0) == hipSuccess &&

@@ -552,10 +552,18 @@ hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, con
   a.ctl = sc.ctl;
   a.test_mask = ix.test_mask;
   a.wild_empty = ix.wild_empty;
-  if (ix.plain_empty)
-    hipLaunchKernelGGL(k_tok<false>, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a, exact_args(ix, sc.xseq));
-  else
-    hipLaunchKernelGGL(k_tok<true>, dim3(grid_for(n, 8192)), dim3(WG), 0, s, a, exact_args(ix, sc.xseq));
+  const dim3 grid(grid_for(n, 8192));
+  const ExactArgs X = exact_args(ix, sc.xseq);
+  if (a.cp_bytes) {
+    if (ix.plain_empty)
+      hipLaunchKernelGGL((k_tok<false, true>), grid, dim3(WG), 0, s, a, X);
+    else
+      hipLaunchKernelGGL((k_tok<true, true>), grid, dim3(WG), 0, s, a, X);
+  } else if (ix.plain_empty) {
+    hipLaunchKernelGGL((k_tok<false, false>), grid, dim3(WG), 0, s, a, X);
+  } else {
+    hipLaunchKernelGGL((k_tok<true, false>), grid, dim3(WG), 0, s, a, X);
+  }
   return hipGetLastError();
 }
 

@@ -139,8 +139,9 @@ step_latency() {
 }
 
 step_winlat() {
-  local extra=${1//,/ }
-  (cd $R && timeout -k 10 300 python -u tools/window_latency.py $extra) > $O/winlat.json 2> $O/winlat.log
+  local extra=${1//,/ } tag=${1//[^a-zA-Z0-9=]/_}
+  (cd $R && timeout -k 10 300 python -u tools/window_latency.py $extra) > $O/winlat${tag:+_$tag}.json \
+    2> $O/winlat${tag:+_$tag}.log
 }
 
 step_wintrace() {
