@@ -3065,6 +3065,17 @@ int emqxgm_match_device_wait(emqxgm_t* h, uint64_t ticket, emqxgm_dev_out* out) 
 }  // extern "C"
 namespace {
 int host_pipe_enqueue_gather(emqxgm* h, emqxgm::HostPipe& p);
+// The device address of pinned host memory, or null (pageable memory: the failed lookup's error
+// is cleared, or the next launch's hipGetLastError would report it)
+void* mapped_ptr(const void* host) {
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, const_cast<void*>(host), 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return d;
+}
+
 int batch_submit(emqxgm* h, const uint8_t* bytes, const uint32_t* offsets, uint32_t n,
                  uint64_t* ticket, bool want_fb, bool trusted = false) {
   if (!h || !ticket || !offsets || offsets[0] != 0 || (!bytes && offsets[n])) return -EINVAL;
@@ -3106,9 +3117,9 @@ int batch_submit(emqxgm* h, const uint8_t* bytes, const uint32_t* offsets, uint3
   p.zc = false;
   if (want_fb && n && n <= h->zc_topics && nb <= (8u << 20) && h->host_out_mode == 0 &&
       !((uintptr_t)bytes & 15u)) {
-    void *db = nullptr, *doff = nullptr;
-    p.zc = hipHostGetDevicePointer(&db, (void*)bytes, 0) == hipSuccess &&
-           hipHostGetDevicePointer(&doff, (void*)offsets, 0) == hipSuccess && db && doff;
+    void* db = mapped_ptr(bytes);
+    void* doff = db ? mapped_ptr(offsets) : nullptr;
+    p.zc = db && doff;
     if (p.zc) {
       p.c.src_bytes = (const uint8_t*)db;
       p.c.src_off = (const uint32_t*)doff;
@@ -3167,8 +3178,8 @@ int host_pipe_enqueue_gather(emqxgm* h, emqxgm::HostPipe& p) {
   uint32_t* tmp = total + 2;
   uint8_t* block = (uint8_t*)p.d_fb.p + at;
   // a small window's block goes straight into the pinned buffer (no D2H copy behind the pass)
-  void* hb = nullptr;
-  const bool direct = p.zc && hipHostGetDevicePointer(&hb, p.h_blk.p, 0) == hipSuccess && hb;
+  void* hb = p.zc ? mapped_ptr(p.h_blk.p) : nullptr;
+  const bool direct = hb != nullptr;
   if (direct) block = (uint8_t*)hb;
   const uint32_t* npairs = s.ctl + CTL_TOTAL;  // written by the pass's scan
   hipStream_t st = p.c.stream;
