@@ -37,6 +37,7 @@ hipError_t hipFree(void* p) {
 }
 hipError_t hipHostMalloc(void** p, size_t bytes, unsigned) { return hipMalloc(p, bytes); }
 hipError_t hipHostFree(void* p) { return hipFree(p); }
+hipError_t hipGetLastError() { return hipSuccess; }
 hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned) {
   *d = h;
   return hipSuccess;

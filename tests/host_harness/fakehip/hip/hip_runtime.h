@@ -44,6 +44,7 @@ hipError_t hipGetDeviceCount(int* n);
 hipError_t hipSetDevice(int d);
 hipError_t hipGetDeviceProperties(hipDeviceProp_t* p, int d);
 const char* hipGetErrorString(hipError_t e);
+hipError_t hipGetLastError();
 hipError_t hipMalloc(void** p, size_t bytes);
 hipError_t hipFree(void* p);
 hipError_t hipHostMalloc(void** p, size_t bytes, unsigned flags);
