@@ -492,7 +492,7 @@ def _nif_concurrent(eng, w, spec):
     runs = [tuple(int(x) for x in item.split(":")) for item in spec.split(",") if item]
     for T, W in runs:
         procs = max(1, -(-W * (eng.HOST_PIPES + 1) // T))
-        calls = max(2 * procs, min(4_000_000, 25 * W) // T)
+        calls = max(2 * procs, min(8_000_000, 100 * W) // T)
         publishers.run([eng], tb, to, T, procs, min(calls, 4 * procs), W)  # warm-up
         r = publishers.run([eng], tb, to, T, procs, calls, W)
         out[f"T{T}_W{W}"] = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}
