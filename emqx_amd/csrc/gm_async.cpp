@@ -306,16 +306,28 @@ struct emqxgm_async {
   // windows of a few hundred calls queue behind the busy pipes, r04).
   void flusher_loop() {
     std::unique_lock<std::mutex> g(mu);
+    const uint64_t W = 1000ull * cfg.window_us;
+    bool drain_blocked = false;  // staged calls found no window: wait for a release
     for (;;) {
+      // Staged calls older than window_us go into the open window now, whether or not a pipe is
+      // free: a publisher thread whose chunk stopped filling (its processes all waiting) left
+      // them there until the next timer seal, which waits for an idle pipe (r04: p99 ~3 ms under
+      // load).  The window itself still seals by size, or by the timer when a pipe is free.
+      const uint64_t fc0 = oldest_staged();
+      if (fc0 != 0 && !drain_blocked && mono_ns() >= fc0 + W) {
+        g.unlock();
+        drain_blocked = !drain_all();
+        g.lock();
+      }
       const int oi = open.load(std::memory_order_acquire);
       const uint64_t fw = oi >= 0 ? slots[oi]->first_ns.load(std::memory_order_acquire) : 0;
       const uint64_t fc = oldest_staged();
       const uint64_t f = (fw && fc) ? std::min(fw, fc) : (fw | fc);
-      if (stop || (f != 0 && ready.empty() && pipe_free() &&
-                   mono_ns() >= f + 1000ull * cfg.window_us)) {
+      if (stop || (f != 0 && ready.empty() && pipe_free() && mono_ns() >= f + W)) {
         g.unlock();
         const bool drained = drain_all();
         g.lock();
+        drain_blocked = !drained;
         const int o2 = open.load();
         if (o2 >= 0 && slots[o2]->cursor.load() != 0) seal(o2);
         if (stop && !drained) {  // staged calls and no window free: wait for a completer
@@ -348,6 +360,7 @@ struct emqxgm_async {
         if (s.n == 0) {  // sealed before any reservation fit
           s.state = FREE;
           free_slots.push_back(si);
+          drain_blocked = false;
           progressed = true;
           continue;
         }
@@ -378,13 +391,19 @@ struct emqxgm_async {
       const uint64_t fc2 = oldest_staged();  // (re-read after announcing the idle sleep)
       const uint64_t f2 = (fw2 && fc2) ? std::min(fw2, fc2) : (fw2 | fc2);
       if (f2 != 0) flusher_idle.store(0, std::memory_order_relaxed);
-      if (f2 != 0 && ready.empty() && pipe_free()) {
-        const uint64_t due = f2 + 1000ull * cfg.window_us, t = mono_ns();
+      // the next deadline: the timer seal (a pipe free) or the oldest staged call's drain
+      uint64_t due = 0;
+      if (f2 != 0 && ready.empty() && pipe_free()) due = f2 + W;
+      if (fc2 != 0 && !drain_blocked && (due == 0 || fc2 + W < due)) due = fc2 + W;
+      if (due != 0) {
+        const uint64_t t = mono_ns();
         if (due > t) cv_flush.wait_for(g, std::chrono::nanoseconds(due - t));
-      } else if (f2 != 0 || !ready.empty()) {
-        cv_flush.wait(g);  // pipes busy: a completer's release wakes us
+        drain_blocked = false;  // (a release may have woken us: try again)
       } else {
-        cv_flush.wait(g);  // nothing pending: a producer's first staged call wakes us
+        // pipes busy (a completer's release wakes us), or nothing pending (a producer's first
+        // staged call does)
+        cv_flush.wait(g);
+        drain_blocked = false;
       }
       flusher_idle.store(0, std::memory_order_relaxed);
     }
