@@ -25,6 +25,7 @@
 // calls' neighbouring tags on shared lines: 4 M calls/s whatever the thread count.)
 #include <errno.h>
 #include <string.h>
+#include <sys/prctl.h>
 #include <time.h>
 
 #include <algorithm>
@@ -305,6 +306,9 @@ struct emqxgm_async {
   // submits windows as large as the pipes' pace allows (sealing on the timer regardless made
   // windows of a few hundred calls queue behind the busy pipes, r04).
   void flusher_loop() {
+    // the window_us timer: Linux lets a normal thread's timed waits run up to 50 us late (its
+    // timer slack), as long as the timer itself at the default window_us
+    (void)prctl(PR_SET_TIMERSLACK, 1000ul, 0ul, 0ul, 0ul);
     std::unique_lock<std::mutex> g(mu);
     const uint64_t W = 1000ull * cfg.window_us;
     bool drain_blocked = false;  // staged calls found no window: wait for a release
