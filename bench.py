@@ -494,9 +494,14 @@ def _nif_concurrent(eng, w, spec):
         procs = max(1, -(-W * (eng.HOST_PIPES + 1) // T))
         calls = max(2 * procs, min(8_000_000, 100 * W) // T)
         publishers.run([eng], tb, to, T, procs, min(calls, 4 * procs), W)  # warm-up
+        th0 = _cgroup_throttled()
         r = publishers.run([eng], tb, to, T, procs, calls, W)
+        th1 = _cgroup_throttled()
         out[f"T{T}_W{W}"] = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}
         out[f"T{T}_W{W}"]["processes_per_thread"] = procs
+        if th0 and th1:  # the job's CPU quota stopping every thread (publishers + the layer's)
+            out[f"T{T}_W{W}"]["cgroup_throttled"] = {"periods": th1[0] - th0[0],
+                                                   "us": th1[1] - th0[1]}
     if runs:
         r = publishers.run([eng], tb, to, 16, 1, 2000, 65536)
         out["idle_T16_P1"] = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}
@@ -841,6 +846,20 @@ def _cpu_leg(ref, w, threads, seconds):
             ref.time_match(w.tbytes, w.toff[: n + 1], threads)
         dt = (time.perf_counter() - t0) / reps
     return n / dt, n, reps, dt
+
+
+def _cgroup_throttled():
+    """(nr_throttled, throttled_usec) of this cgroup (v2 cpu.stat), or None: the quota's
+    periods in which every thread of the job was stopped."""
+    try:
+        st = {}
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for line in f:
+                k, v = line.split()
+                st[k] = int(v)
+        return st.get("nr_throttled", 0), st.get("throttled_usec", 0)
+    except (OSError, ValueError):
+        return None
 
 
 def _cgroup_cpus():
