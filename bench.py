@@ -494,11 +494,15 @@ def _nif_concurrent(eng, w, spec):
         procs = max(1, -(-W * (eng.HOST_PIPES + 1) // T))
         calls = max(2 * procs, min(8_000_000, 100 * W) // T)
         publishers.run([eng], tb, to, T, procs, min(calls, 4 * procs), W)  # warm-up
-        th0 = _cgroup_throttled()
+        th0, s0 = _cgroup_throttled(), eng.stats()
         r = publishers.run([eng], tb, to, T, procs, calls, W)
-        th1 = _cgroup_throttled()
+        th1, s1 = _cgroup_throttled(), eng.stats()
         out[f"T{T}_W{W}"] = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}
         out[f"T{T}_W{W}"]["processes_per_thread"] = procs
+        # stalls inside the engine during the point: buffer reallocations (a hipFree syncs the
+        # device), windows whose filter block outgrew its estimate, passes redone
+        out[f"T{T}_W{W}"]["engine"] = {k: s1[k] - s0[k] for k in ("buffer_grows", "sync_gathers",
+                                                                   "reruns")}
         if th0 and th1:  # the job's CPU quota stopping every thread (publishers + the layer's)
             out[f"T{T}_W{W}"]["cgroup_throttled"] = {"periods": th1[0] - th0[0],
                                                    "us": th1[1] - th0[1]}

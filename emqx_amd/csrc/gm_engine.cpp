@@ -1620,6 +1620,7 @@ int ensure_scratch(emqxgm* h, PassCtx& c, uint32_t n, uint64_t words, uint32_t p
       s.spill_lanes == h->geom.lanes && s.ctl)
     return 0;
   HIPCHK(h, hipStreamSynchronize(c.stream));
+  h->st.buffer_grows += 1;
   const uint32_t ncap = std::max(n, s.n_cap);
   const uint64_t wcap = std::max(words, s.w_cap);
   const uint32_t pcap = (std::max(pairs, s.p_cap) + STAGE_CHUNK - 1) / STAGE_CHUNK * STAGE_CHUNK;
@@ -1982,6 +1983,7 @@ int run_fanout(emqxgm* h, uint32_t n, uint32_t* n_routes, uint32_t* n_deliv) {
 // Grows a pinned host buffer to `bytes` (keep: preserve the old contents).
 int pinned_reserve(emqxgm* h, emqxgm::Pinned& b, size_t bytes, bool keep) {
   if (bytes <= b.cap) return 0;
+  h->st.buffer_grows += 1;
   const size_t cap = std::max<size_t>(bytes + bytes / 4, 1 << 16);
   void* p = nullptr;
   HIPCHK(h, hipHostMalloc(&p, cap, hipHostMallocDefault));
@@ -2044,6 +2046,7 @@ int host_buf(emqxgm* h, uint32_t** p, uint64_t entries) {
 
 int host_pipe_reserve(emqxgm* h, emqxgm::HostPipe& p, uint64_t n, uint64_t bytes, uint64_t fid) {
   if (bytes > p.bytes_cap) {
+    h->st.buffer_grows += 1;
     if (p.d_bytes) (void)hipFree(p.d_bytes);
     p.d_bytes = nullptr;
     p.bytes_cap = 0;
@@ -2052,6 +2055,7 @@ int host_pipe_reserve(emqxgm* h, emqxgm::HostPipe& p, uint64_t n, uint64_t bytes
     p.bytes_cap = cap;
   }
   if (n + 1 > p.off_cap) {
+    h->st.buffer_grows += 1;
     if (p.d_off) (void)hipFree(p.d_off);
     p.d_off = nullptr;
     p.off_cap = 0;
@@ -2060,6 +2064,7 @@ int host_pipe_reserve(emqxgm* h, emqxgm::HostPipe& p, uint64_t n, uint64_t bytes
     p.off_cap = cap;
   }
   if (n + 1 > p.row_cap) {
+    h->st.buffer_grows += 1;
     if (p.h_row) (void)hipHostFree(p.h_row);
     if (p.h_exact) (void)hipHostFree(p.h_exact);
     delete[] p.h_none;
@@ -2074,6 +2079,7 @@ int host_pipe_reserve(emqxgm* h, emqxgm::HostPipe& p, uint64_t n, uint64_t bytes
     p.row_cap = cap;
   }
   if (fid > p.fid_cap) {
+    h->st.buffer_grows += 1;
     if (p.h_fid) (void)hipHostFree(p.h_fid);
     p.h_fid = nullptr;
     p.fid_cap = 0;
@@ -2168,7 +2174,10 @@ int host_pipe_complete(emqxgm* h, emqxgm::HostPipe& p, bool gather = false) {
                           p.pairs <= p.fb_pairs_copy && blk_total <= p.fb_bytes_copy;
   if (async_done) p.fb_bytes = p.pairs ? blk_total : 0;
   p.fb_fast = async_done;
-  if (rc == 0 && gather && !async_done) rc = host_pipe_gather(h, p);
+  if (rc == 0 && gather && !async_done) {
+    if (p.fb_async) h->st.sync_gathers += 1;
+    rc = host_pipe_gather(h, p);
+  }
   p.fb_async = false;
   p.c.epoch.reset();
   if (rc < 0) {
@@ -2216,6 +2225,7 @@ int host_pipe_complete(emqxgm* h, emqxgm::HostPipe& p, bool gather = false) {
 // A device buffer of at least `bytes`, its contents kept (stream-ordered on s).
 int grow_dev(emqxgm* h, DevBuf& b, uint64_t bytes, hipStream_t s) {
   if (bytes <= b.bytes && b.p) return 0;
+  h->st.buffer_grows += 1;
   const uint64_t cap = std::max<uint64_t>(bytes + bytes / 4, 1 << 20);
   void* p = nullptr;
   HIPCHK(h, hipMalloc(&p, cap));

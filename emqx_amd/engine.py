@@ -103,7 +103,8 @@ class _Stats(C.Structure):
                 ("total_ms", C.c_double), ("full_commits", C.c_uint64),
                 ("delta_commits", C.c_uint64), ("last_commit_ms", C.c_double),
                 ("tok_ms", C.c_double), ("tok_launches", C.c_uint64),
-                ("exact_ms", C.c_double), ("keyed_nodes", C.c_uint64)]
+                ("exact_ms", C.c_double), ("keyed_nodes", C.c_uint64),
+                ("buffer_grows", C.c_uint64), ("sync_gathers", C.c_uint64)]
 
 
 # name -> (restype, argtypes): exactly the entry points declared in include/emqx_gpumatch.h

@@ -134,6 +134,9 @@ typedef struct emqxgm_stats {
   uint64_t tok_launches;
   double exact_ms;          /* summed exact route-key probe time (k_exact; 0 without plain keys) */
   uint64_t keyed_nodes;     /* trie nodes whose literal children are placed by token */
+  uint64_t buffer_grows;    /* pass scratch / host-pipe buffers reallocated (each a stall) */
+  uint64_t sync_gathers;    /* host windows whose filter block outgrew its estimate (finished
+                               synchronously in the wait) */
 } emqxgm_stats;
 
 int emqxgm_abi_version(void);
