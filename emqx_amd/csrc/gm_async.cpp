@@ -45,6 +45,8 @@
 // increase (a window's are built increasing here)
 int gm_submit_window(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets, uint32_t n,
                      uint64_t* ticket);
+// gm_engine.cpp: every host pipe of h sized for windows of n topics / nb bytes
+int gm_reserve_windows(emqxgm_t* h, uint32_t n, uint64_t nb);
 
 namespace {
 
@@ -509,6 +511,10 @@ int emqxgm_async_create(emqxgm_t* const* hs, uint32_t n_handles, const emqxgm_as
     else s->off[0] = 0;
     a->free_slots.push_back((int)(n_slots - 1 - i));
   }
+  // each engine's host pipes at the windows' size now (a reallocation later would stall every
+  // pass on the device)
+  for (uint32_t k = 0; k < n_handles && !rc; ++k)
+    rc = gm_reserve_windows(a->hs[k], a->cfg.window_topics, a->cfg.window_bytes);
   if (rc) {
     for (size_t i = 0; i < a->slots.size(); ++i) {
       emqxgm_host_free(a->hs[i % n_handles], a->slots[i]->bytes);

@@ -1984,7 +1984,7 @@ int run_fanout(emqxgm* h, uint32_t n, uint32_t* n_routes, uint32_t* n_deliv) {
 int pinned_reserve(emqxgm* h, emqxgm::Pinned& b, size_t bytes, bool keep) {
   if (bytes <= b.cap) return 0;
   h->st.buffer_grows += 1;
-  const size_t cap = std::max<size_t>(bytes + bytes / 4, 1 << 16);
+  const size_t cap = std::max<size_t>(bytes + bytes / 2, 1 << 16);
   void* p = nullptr;
   HIPCHK(h, hipHostMalloc(&p, cap, hipHostMallocDefault));
   if (keep && b.p && b.cap) memcpy(p, b.p, b.cap);
@@ -2226,7 +2226,7 @@ int host_pipe_complete(emqxgm* h, emqxgm::HostPipe& p, bool gather = false) {
 int grow_dev(emqxgm* h, DevBuf& b, uint64_t bytes, hipStream_t s) {
   if (bytes <= b.bytes && b.p) return 0;
   h->st.buffer_grows += 1;
-  const uint64_t cap = std::max<uint64_t>(bytes + bytes / 4, 1 << 20);
+  const uint64_t cap = std::max<uint64_t>(bytes + bytes / 2, 1 << 20);
   void* p = nullptr;
   HIPCHK(h, hipMalloc(&p, cap));
   if (b.p) {
@@ -3221,6 +3221,39 @@ int emqxgm_match_batch_submit_filters(emqxgm_t* h, const uint8_t* bytes, const u
 int gm_submit_window(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets, uint32_t n,
                      uint64_t* ticket) {
   return batch_submit(h, bytes, offsets, n, ticket, true, true);
+}
+
+// gm_async.cpp at create: every host pipe's buffers sized for windows of n topics / nb bytes
+// (and the filter block for the default density estimate), so that no window of a running
+// layer reallocates -- a hipFree synchronises the whole device (r04: 8 reallocations in a load
+// point's first windows gave its calls a 3-7 ms p99)
+int gm_reserve_windows(emqxgm_t* h, uint32_t n, uint64_t nb) {
+  if (!h || !n) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->mmu);
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
+  for (uint32_t k = 0; k < EMQXGM_HOST_PIPES; ++k) {
+    emqxgm::HostPipe& p = h->hpipes[k];
+    if (p.state == 1) continue;  // in flight (a layer on a busy engine): it grows as it goes
+    hipStream_t ps = pipe_stream(h, k);
+    if (!ps) return -EIO;
+    int rc = ctx_init(h, p.c, ps);
+    if (rc || (rc = pass_prepare(h, p.c, n, nb)) < 0 ||
+        (rc = host_pipe_reserve(h, p, n, std::max<uint64_t>(nb, 1), 1)))
+      return rc < 0 ? rc : 0;
+    // the block host_pipe_enqueue_gather asks for at the default estimates
+    const uint32_t cap = p.c.sc.p_cap;
+    const double exp_p = 4.0 * n;
+    const uint32_t want_p = (uint32_t)std::min<uint64_t>(cap, (uint64_t)(1.2 * exp_p) + 256);
+    const uint64_t want_b = (uint64_t)(1.2 * 32.0 * exp_p) + 4096;
+    const FbLayout L(n, want_p);
+    const uint64_t blk = L.bytes + want_b;
+    const uint64_t words = 2ull * cap + 1 + scan_tmp_words(cap) + 2;
+    const uint64_t at = ((words * 4 + 255) / 256) * 256;
+    if ((rc = grow_dev(h, p.d_fb, at + blk, p.c.stream)) ||
+        (rc = pinned_reserve(h, p.h_blk, (size_t)blk, false)))
+      return rc;
+  }
+  return 0;
 }
 extern "C" {
 

@@ -120,6 +120,8 @@ int emqxgm_match_batch_submit_filters(emqxgm_t* h, const uint8_t* bytes, const u
 }
 
 }  // extern "C"
+// the engine's buffers sized for the layer's windows (nothing to size in the mock)
+int gm_reserve_windows(emqxgm_t* h, uint32_t n, uint64_t) { return h && n ? 0 : -EINVAL; }
 // the layer's window submit (gm_engine.cpp skips the offsets check there; the mock checks them)
 int gm_submit_window(emqxgm_t* h, const uint8_t* bytes, const uint32_t* off, uint32_t n,
                      uint64_t* ticket) {
