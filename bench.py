@@ -71,10 +71,11 @@ def main():
     ap.add_argument("--windows", default="16384,65536,262144,1048576",
                     help="NIF batcher window sizes (topics) for the operating-point sweep "
                          "('' = skip); rank 0, N=1, with the host-in/host-out timing")
-    ap.add_argument("--nif", default="16:16384,16:65536,64:16384,64:65536",
-                    help="concurrent publish entry load (threads:window, '' = skip): publisher "
-                         "threads each calling emqxgm_async_match one topic at a time; rank 0, "
-                         "N=1")
+    ap.add_argument("--nif", default="16:16384,16:65536,64:16384,64:65536,16:16384:1024,16:65536:4096",
+                    help="concurrent publish entry load (threads:window[:processes per thread], "
+                         "'' = skip): publisher threads each calling emqxgm_async_match one topic "
+                         "at a time; processes default to (host pipes + 1) windows outstanding; "
+                         "rank 0, N=1")
     ap.add_argument("--only-nif", action="store_true",
                     help="build the index and run only the concurrent-entry load (no timed steps)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -490,29 +491,33 @@ def _nif_concurrent(eng, w, spec):
     to = w.toff.astype(np.uint64)
     out = {}
     runs = [tuple(int(x) for x in item.split(":")) for item in spec.split(",") if item]
-    for T, W in runs:
-        procs = max(1, -(-W * (eng.HOST_PIPES + 1) // T))
+    for run in runs:
+        T, W = run[0], run[1]
+        # closed loop: calls outstanding = T x procs, so by Little's law the latency is that over
+        # the rate -- (pipes + 1) windows' worth saturates the pipes, one window's worth shows
+        # the latency at a lighter load
+        procs = run[2] if len(run) > 2 else max(1, -(-W * (eng.HOST_PIPES + 1) // T))
+        key = f"T{T}_W{W}" + (f"_P{procs}" if len(run) > 2 else "")
         calls = max(2 * procs, min(8_000_000, 100 * W) // T)
         publishers.run([eng], tb, to, T, procs, min(calls, 4 * procs), W)  # warm-up
         th0, s0 = _cgroup_throttled(), eng.stats()
         r = publishers.run([eng], tb, to, T, procs, calls, W)
         th1, s1 = _cgroup_throttled(), eng.stats()
-        out[f"T{T}_W{W}"] = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}
-        out[f"T{T}_W{W}"]["processes_per_thread"] = procs
+        out[key] = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}
+        out[key]["processes_per_thread"] = procs
         # stalls inside the engine during the point: buffer reallocations (a hipFree syncs the
         # device), windows whose filter block outgrew its estimate, passes redone
-        out[f"T{T}_W{W}"]["engine"] = {k: s1[k] - s0[k] for k in ("buffer_grows", "sync_gathers",
-                                                                   "reruns")}
+        out[key]["engine"] = {k: s1[k] - s0[k] for k in ("buffer_grows", "sync_gathers", "reruns")}
         if th0 and th1:  # the job's CPU quota stopping every thread (publishers + the layer's)
-            out[f"T{T}_W{W}"]["cgroup_throttled"] = {"periods": th1[0] - th0[0],
-                                                   "us": th1[1] - th0[1]}
+            out[key]["cgroup_throttled"] = {"periods": th1[0] - th0[0], "us": th1[1] - th0[1]}
     if runs:
         r = publishers.run([eng], tb, to, 16, 1, 2000, 65536)
         out["idle_T16_P1"] = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}
     out["includes"] = ("T threads x P processes, one emqxgm_async_match call per topic (the NIF's "
                        "match_async/3), windows filled lock-free and flushed when full or "
-                       "window_us (50) after their first call, H2D, the device pass, every "
-                       "pair's filter bytes to pinned memory, the callback reporting each call; "
+                       "window_us (50) after their first call, the window read from pinned memory "
+                       "(copy-through up to 64k topics, else H2D), the device pass, every pair's "
+                       "filter bytes to pinned memory, the callback reporting each call; "
                        "latency = call -> its report (the NIF's term building and enif_send "
                        "excluded)")
     return out
