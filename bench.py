@@ -64,8 +64,11 @@ def main():
     ap.add_argument("--wg-per-cu", type=int, default=0)
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="emqxgm_tune before the index is built (A/B runs), e.g. fat_buckets=0")
-    ap.add_argument("--no-filter-shard", action="store_true",
-                    help="N>1: skip the filter-sharded measurement beside the replicas")
+    ap.add_argument("--filter-shard", action="store_true",
+                    help="N>1: also measure the filter-sharded layout beside the replicas (its "
+                         "RCCL branch has run under gloo only, so the default N>1 run -- the "
+                         "scaling measurement -- leaves it out; --shard filters makes it the "
+                         "headline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-in/host-out timing")
     ap.add_argument("--windows", default="16384,65536,262144,1048576",
@@ -234,7 +237,7 @@ def main():
     # N > 1: the north-star layout beside the replicas, on the same ranks (filters split by hash,
     # rank 0's batch broadcast, results gathered and merged on rank 0 every step)
     fsh = None
-    if world > 1 and (args.shard == "filters" or not args.no_filter_shard):
+    if world > 1 and (args.shard == "filters" or args.filter_shard):
         fsh = _filter_sharded_run(Engine, D, args, w, dbat, rank, world, dev, local)
     # kernel timing with HIP events on the engine's stream, in extra passes after the timed
     # region (the events themselves add gaps between launches), one pass at a time so that a

@@ -27,7 +27,7 @@
 #                           HSA_ENABLE_SDMA=0, blit-kernel copies, was slower: profiles/r04/latency)
 #   wintrace[=ARGS]         rocprofv3 kernel + memory-copy + HIP runtime traces of
 #                           tools/window_latency.py (the timeline of one window at a time)
-#   dist[=filters]          bench.py's N=2 path with two ranks sharing this box's one GPU over
+#   dist[=filters|both]     bench.py's N=2 path with two ranks sharing this box's one GPU over
 #                           gloo (RCCL refuses two ranks on one device): the control flow at full
 #                           size, not a timing; "filters" makes the filter-sharded layout the
 #                           headline
@@ -154,6 +154,7 @@ step_wintrace() {
 step_dist() {
   local extra=""
   [ "$1" = filters ] && extra="--shard filters"
+  [ "$1" = both ] && extra="--filter-shard"
   (cd $R && EMQXGM_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
     --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 $extra \
     --steps 5 --warmup 1) > $O/dist_n2${1:+_$1}.json 2> $O/dist_n2${1:+_$1}.log
