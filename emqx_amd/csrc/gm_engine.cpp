@@ -511,6 +511,9 @@ struct emqxgm {
   // go without DMA copies: k_tok reads the window itself (copy-through) and k_fb_pack writes the
   // result block into pinned memory (emqxgm_tune "zc_topics"; 0: always DMA)
   uint32_t zc_topics = 65536;
+  // a host pipe's wait polls its completion event for up to this long before it blocks in
+  // hipEventSynchronize (emqxgm_tune "spin_us"; 0: block at once)
+  std::atomic<uint32_t> spin_us{0};
   uint64_t xrange_bytes = 0;  // emqxgm_tune("exact_range_kb")
 
   // ---- delta commits (writer side) ----
@@ -3267,7 +3270,21 @@ static int host_pipe_prewait(emqxgm* h, uint64_t ticket) {
     const emqxgm::HostPipe& p = h->hpipes[ticket % EMQXGM_HOST_PIPES];
     if (ticket != 0 && p.ticket == ticket && p.state == 1) ev = p.fin;
   }
-  if (ev && (hipSetDevice(h->cfg.device) != hipSuccess || hipEventSynchronize(ev) != hipSuccess)) {
+  if (!ev) return 0;
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
+  if (const uint32_t spin = h->spin_us.load(std::memory_order_relaxed)) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      const hipError_t q = hipEventQuery(ev);
+      if (q == hipSuccess) return 0;
+      if (q != hipErrorNotReady ||
+          std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin))
+        break;  // (an error: the synchronisation below reports it)
+      __builtin_ia32_pause();
+    }
+    (void)hipGetLastError();  // a pending query's "not ready" is not this thread's error
+  }
+  if (hipEventSynchronize(ev) != hipSuccess) {
     set_err(h, "hipEventSynchronize failed");
     return -EIO;
   }
@@ -3688,6 +3705,11 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
     if (value < 0 || value > 1) return -EINVAL;
     std::lock_guard<std::mutex> g(h->mmu);
     h->leafp_mask = value ? CF_HMASK : 0u;
+    return 0;
+  }
+  if (strcmp(key, "spin_us") == 0) {  // host pipes' waits poll before they block
+    if (value < 0 || value > 1000000) return -EINVAL;
+    h->spin_us.store((uint32_t)value, std::memory_order_relaxed);
     return 0;
   }
   if (strcmp(key, "zc_topics") == 0) {  // concurrent-entry windows without DMA copies: max topics
