@@ -535,7 +535,9 @@ int emqxgm_set_profiling(emqxgm_t* h, int on);
  * (rocprofv3 --marker-trace; also EMQXGM_ROCTX=1 at create), 0 (default) = none;
  * "keyed": token-keyed trie parents from the next full build: 1 (default) =
  * automatic, 0 = none, 2 = every eligible node (tests); "zc_topics": the largest pinned window
- * of _submit_filters that goes without DMA copies (65536 default, 0 = always copies). */
+ * of _submit_filters that goes without DMA copies (65536 default, 0 = always copies); "spin_us":
+ * host pipes' waits poll the pass's completion for up to this long before they block (200
+ * default, 0 = block at once). */
 int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value);
 int emqxgm_get_stats(emqxgm_t* h, emqxgm_stats* st);
 /* Last HIP error string seen by the handle (for diagnostics). */
