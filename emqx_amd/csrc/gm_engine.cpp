@@ -3198,10 +3198,16 @@ int host_pipe_enqueue_gather(emqxgm* h, emqxgm::HostPipe& p) {
   if (direct) block = (uint8_t*)hb;
   const uint32_t* npairs = s.ctl + CTL_TOTAL;  // written by the pass's scan
   hipStream_t st = p.c.stream;
-  // (sized by the block's pair capacity: a window with more pairs is finished in the wait)
-  HIPCHK(h, launch_filter_len_dev(s.out, npairs, want_p, ix.foff, len, ooff, tmp, total, st));
-  HIPCHK(h, launch_fb_pack(s.out, npairs, ix.foff, ix.fbytes, ooff, total, s.exact_id, s.row, p.n,
-                           want_p, want_b, block, st));
+  // (sized by the block's pair capacity: a window with more pairs is finished in the wait); a
+  // small block in one single-block launch instead of three
+  if (want_p <= FB_SMALL_PAIRS) {
+    HIPCHK(h, launch_fb_small(s.out, npairs, ix.foff, ix.fbytes, s.exact_id, s.row, p.n, want_p,
+                              want_b, block, st));
+  } else {
+    HIPCHK(h, launch_filter_len_dev(s.out, npairs, want_p, ix.foff, len, ooff, tmp, total, st));
+    HIPCHK(h, launch_fb_pack(s.out, npairs, ix.foff, ix.fbytes, ooff, total, s.exact_id, s.row, p.n,
+                             want_p, want_b, block, st));
+  }
   if (!direct) HIPCHK(h, hipMemcpyAsync(p.h_blk.p, block, (size_t)blk, hipMemcpyDeviceToHost, st));
   p.fb_pairs_copy = want_p;
   p.fb_bytes_copy = want_b;

@@ -299,6 +299,12 @@ hipError_t launch_fb_pack(const uint32_t* fid, const uint32_t* pairs_dev, const 
                           const uint8_t* pool, const uint32_t* ooff, const uint32_t* total,
                           const uint32_t* exact, const uint32_t* row, uint32_t n, uint32_t cap_p,
                           uint64_t cap_b, uint8_t* block, hipStream_t s);
+// launch_filter_len_dev + launch_fb_pack in one single-block launch, for cap_p <= SCAN_TILE pairs
+// (the scan of the lengths in LDS); -> hipErrorInvalidValue beyond
+hipError_t launch_fb_small(const uint32_t* fid, const uint32_t* pairs_dev, const uint64_t* foff,
+                           const uint8_t* pool, const uint32_t* exact, const uint32_t* row,
+                           uint32_t n, uint32_t cap_p, uint64_t cap_b, uint8_t* block, hipStream_t s);
+constexpr uint32_t FB_SMALL_PAIRS = 4096;  // = SCAN_TILE (gm_kernels.hip)
 // out[i] = base + row[i], i < m (u64 CSR row pointers of the host API, built on the device)
 hipError_t launch_row64(const uint32_t* row, uint64_t base, uint64_t* out, uint32_t m,
                         hipStream_t s);

@@ -23,6 +23,7 @@ constexpr uint32_t CH = STAGE_CHUNK;  // staged-pair slots reserved per wave per
 constexpr uint32_t TBLK = 128;  // topics claimed per wave per atomic (r02: 64 / 256 no better)
 constexpr uint32_t SCAN_ITEMS = 16;
 constexpr uint32_t SCAN_TILE = WG * SCAN_ITEMS;
+static_assert(FB_SMALL_PAIRS == SCAN_TILE, "k_fb_small scans one tile");
 constexpr uint32_t TILE_BYTES = 16384;  // tokenizer LDS tile (256 topics)
 constexpr uint32_t TILE_CHUNKS = TILE_BYTES / 16 + 2;
 // The route-key probe over a table beyond the TLB's reach: random lines over a 2-3 GiB table
@@ -462,6 +463,53 @@ __global__ __launch_bounds__(WG) void k_fb_pack(FbPack A) {
   }
 }
 
+// The whole filter-byte gather of a small window in one block (k_filter_len + the length scan +
+// k_fb_pack in one launch, r04): every pair's filter length, their exclusive scan in LDS, then
+// the packed block as k_fb_pack writes it.  For a block of at most SCAN_TILE pairs (cap_p).
+__global__ __launch_bounds__(WG) void k_fb_small(FbPack A) {
+  __shared__ uint32_t s_w[WG / 64];
+  __shared__ uint32_t s_off[SCAN_TILE + 1];
+  const uint32_t pairs = *A.pairs_dev;
+  const uint32_t c = min(pairs, A.cap_p);  // (a window beyond cap_p is finished by the host)
+  uint32_t len[SCAN_ITEMS];
+  uint32_t acc = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < SCAN_ITEMS; ++k) {
+    const uint32_t j = threadIdx.x * SCAN_ITEMS + k;
+    uint32_t l = 0;
+    if (j < c) {
+      const uint32_t f = A.fid[j];
+      l = (uint32_t)(A.foff[f + 1] - A.foff[f]);
+    }
+    len[k] = l;
+    acc += l;
+  }
+  uint32_t total;
+  uint32_t x = block_excl_scan(acc, s_w, total);
+#pragma unroll
+  for (uint32_t k = 0; k < SCAN_ITEMS; ++k) {
+    s_off[threadIdx.x * SCAN_ITEMS + k] = x;
+    x += len[k];
+  }
+  if (threadIdx.x == 0) {
+    s_off[c] = total;
+    *A.b_total = total;
+  }
+  __syncthreads();
+  if (pairs > A.cap_p || total > A.cap_b) return;
+  const uint32_t m = max(pairs, A.n) + 1;
+  for (uint32_t i = threadIdx.x; i < m; i += WG) {
+    if (i < A.n) A.b_exact[i] = A.exact[i];
+    if (i <= A.n) A.b_row[i] = A.row[i];
+    if (i <= pairs) A.b_ooff[i] = s_off[i];
+    if (i < pairs) {
+      const uint32_t f = A.fid[i], o = s_off[i];
+      A.b_fid[i] = f;
+      copy_filter(A.pool, A.foff[f], s_off[i + 1] - o, A.b_bytes + o);
+    }
+  }
+}
+
 uint32_t grid_for(uint64_t items, uint32_t cap_blocks) {
   uint64_t b = (items + WG - 1) / WG;
   if (b == 0) b = 1;
@@ -887,6 +935,33 @@ hipError_t launch_fb_pack(const uint32_t* fid, const uint32_t* pairs_dev, const 
   a.b_row = (uint32_t*)(block + L.row);
   a.b_bytes = block + L.bytes;
   hipLaunchKernelGGL(k_fb_pack, dim3(grid_for(std::max<uint32_t>(cap_p, n) + 1, 2048)), dim3(WG), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_fb_small(const uint32_t* fid, const uint32_t* pairs_dev, const uint64_t* foff,
+                           const uint8_t* pool, const uint32_t* exact, const uint32_t* row,
+                           uint32_t n, uint32_t cap_p, uint64_t cap_b, uint8_t* block, hipStream_t s) {
+  if (cap_p > SCAN_TILE) return hipErrorInvalidValue;
+  const FbLayout L(n, cap_p);
+  FbPack a;
+  a.fid = fid;
+  a.pairs_dev = pairs_dev;
+  a.foff = foff;
+  a.pool = pool;
+  a.ooff = nullptr;
+  a.total = nullptr;
+  a.exact = exact;
+  a.row = row;
+  a.n = n;
+  a.cap_p = cap_p;
+  a.cap_b = cap_b;
+  a.b_total = (uint32_t*)(block + L.total);
+  a.b_ooff = (uint32_t*)(block + L.ooff);
+  a.b_fid = (uint32_t*)(block + L.fid);
+  a.b_exact = (uint32_t*)(block + L.exact);
+  a.b_row = (uint32_t*)(block + L.row);
+  a.b_bytes = block + L.bytes;
+  hipLaunchKernelGGL(k_fb_small, dim3(1), dim3(WG), 0, s, a);
   return hipGetLastError();
 }
 

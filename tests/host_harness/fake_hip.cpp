@@ -127,6 +127,7 @@ hipError_t launch_wire_exact(const uint2* const*, const uint32_t*, uint32_t, uin
 hipError_t launch_filter_len(const uint32_t*, uint32_t, const uint64_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, hipStream_t) { NOT_HERE; }
 hipError_t launch_filter_gather(const uint32_t*, uint32_t, const uint64_t*, const uint8_t*, const uint32_t*, uint8_t*, hipStream_t) { NOT_HERE; }
 hipError_t launch_filter_len_dev(const uint32_t*, const uint32_t*, uint32_t, const uint64_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, hipStream_t) { NOT_HERE; }
+hipError_t launch_fb_small(const uint32_t*, const uint32_t*, const uint64_t*, const uint8_t*, const uint32_t*, const uint32_t*, uint32_t, uint32_t, uint64_t, uint8_t*, hipStream_t) { NOT_HERE; }
 hipError_t launch_fb_pack(const uint32_t*, const uint32_t*, const uint64_t*, const uint8_t*, const uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*, uint32_t, uint32_t, uint64_t, uint8_t*, hipStream_t) { NOT_HERE; }
 
 }  // namespace gm
