@@ -641,7 +641,7 @@ hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, c
 // Workgroups of one walk launch.  The deep-stack variants fit fewer blocks per CU (LDS): only
 // as many are launched as are resident at once, so that no block of the persistent grid starts
 // after the others have drained.  A batch that gives the grid less than one topic per lane
-// launches only the blocks it fills (at least one per CU): the waves a full grid adds only queue
+// launches only the blocks it fills: the waves a full grid adds only queue
 // failed claims on the exhausted shard counters (r03: a cfg3 walk took 79 us at 64k topics and
 // 80 us at 262k).
 uint32_t walk_blocks(const WalkGeom& g, uint32_t n, uint32_t level) {
@@ -650,7 +650,9 @@ uint32_t walk_blocks(const WalkGeom& g, uint32_t n, uint32_t level) {
                        : level == WALK_DEEP ? walk_lds_bytes(WALK_STK_DEEP, WALK_CPT)
                                             : walk_lds_bytes(WALK_STK_SHALLOW, WALK_CPT);
   uint32_t blocks = std::min<uint32_t>(g.blocks, g.cus * (LDS_CU / lds));
-  return std::min<uint32_t>(blocks, std::max<uint32_t>((n + WG - 1) / WG, g.cus));
+  // one topic per lane (static_one): only the blocks that hold topics (r04: a 16-topic window
+  // launched one block per CU, all but one of them empty)
+  return std::min<uint32_t>(blocks, std::max<uint32_t>((n + WG - 1) / WG, 1u));
 }
 
 // Topics per claim: a batch too small to give every wave TBLK topics is spread over all of them
