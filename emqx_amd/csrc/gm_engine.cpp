@@ -1752,12 +1752,16 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
       // pairs of filters made of short (exact) tokens need no byte check (gm_verify.inc)
       roctx_mark(h->roctx && ix.needs_verify, "k_verify");
       if (ix.needs_verify) HIPCHK(h, launch_verify(d_bytes, d_off, ix, s, n, h->geom, st));
-      roctx_mark(h->roctx, "k_scan");
-      // the scan's last block mirrors the control words to the host (no launch of its own)
-      HIPCHK(h, launch_scan_ctl(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, s.ctl, s.ctl_host_dev, st));
+      // the scan's last block mirrors the control words to the host (no launch of its own); a
+      // batch of one scan tile has its scan done inside k_scatter (one launch less)
+      const bool fuse = n <= SCATTER_SCAN_MAX;
+      if (!fuse) {
+        roctx_mark(h->roctx, "k_scan");
+        HIPCHK(h, launch_scan_ctl(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, s.ctl, s.ctl_host_dev, st));
+      }
       ctl_sent = true;
       roctx_mark(h->roctx, "k_scatter");
-      HIPCHK(h, launch_scatter(s, n, h->geom, st, ctl_sent));
+      HIPCHK(h, launch_scatter(s, n, h->geom, st, ctl_sent, fuse));
     } else {
       HIPCHK(h, launch_scan(s.cnt, s.row, n, s.scan_tmp, s.ctl + CTL_TOTAL, st));
       HIPCHK(h, launch_verify_scatter(d_bytes, d_off, ix, s, n, st));

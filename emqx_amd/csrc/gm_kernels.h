@@ -216,8 +216,10 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
 // production: verify (flags + counts) -> [scan] -> deferred scatter
 hipError_t launch_verify(const uint8_t* bytes, const uint32_t* off, const DevIndex& ix,
                          Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_t s);
+// fuse_scan: the row scan inside k_scatter (n <= SCATTER_SCAN_MAX; no launch_scan_ctl before)
+constexpr uint32_t SCATTER_SCAN_MAX = 4096;  // = SCAN_TILE (gm_kernels.hip)
 hipError_t launch_scatter(Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_t s,
-                          bool mirror_ctl = false);
+                          bool mirror_ctl = false, bool fuse_scan = false);
 // a pass's row scan whose last block also copies the control words to the host mirror
 hipError_t launch_scan_ctl(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* tmp,
                            uint32_t* total_dst, const uint32_t* ctl, uint32_t* ctl_host_dev,

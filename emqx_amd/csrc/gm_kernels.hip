@@ -24,6 +24,7 @@ constexpr uint32_t TBLK = 128;  // topics claimed per wave per atomic (r02: 64 /
 constexpr uint32_t SCAN_ITEMS = 16;
 constexpr uint32_t SCAN_TILE = WG * SCAN_ITEMS;
 static_assert(FB_SMALL_PAIRS == SCAN_TILE, "k_fb_small scans one tile");
+static_assert(SCATTER_SCAN_MAX == SCAN_TILE, "k_scatter<true> scans one tile");
 constexpr uint32_t TILE_BYTES = 16384;  // tokenizer LDS tile (256 topics)
 constexpr uint32_t TILE_CHUNKS = TILE_BYTES / 16 + 2;
 // The route-key probe over a table beyond the TLB's reach: random lines over a 2-3 GiB table
@@ -583,6 +584,7 @@ hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, con
                       const uint32_t* claim0, const uint8_t* src_bytes, const uint32_t* src_off) {
   if (n == 0) return hipSuccess;
   TokArgs a;
+  a.ctl_host = sc.ctl_host_dev;
   a.cp_bytes = src_bytes ? const_cast<uint8_t*>(bytes) : nullptr;
   a.cp_off = src_off ? const_cast<uint32_t*>(off) : nullptr;
   if (src_bytes) bytes = src_bytes;
@@ -771,9 +773,11 @@ hipError_t launch_verify(const uint8_t* bytes, const uint32_t* off, const DevInd
 }
 
 hipError_t launch_scatter(Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_t s,
-                          bool mirror_ctl) {
-  (void)n;
+                          bool mirror_ctl, bool fuse_scan) {
   ScatterArgs a;
+  a.cnt = sc.cnt;
+  a.n = n;
+  a.row_out = sc.row;
   a.ctl_host = mirror_ctl ? sc.ctl_host_dev : nullptr;
   a.stg = sc.stg;
   a.chk = sc.chk;
@@ -785,7 +789,13 @@ hipError_t launch_scatter(Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_
   a.out = sc.out;
   a.ocap = sc.o_cap;
   a.ctl = sc.ctl;
-  hipLaunchKernelGGL(k_scatter, dim3(grid_for(sc.p_cap, g.cus * 8)), dim3(WG), 0, s, a);
+  if (fuse_scan) {
+    if (n > SCAN_TILE || !sc.ctl_host_dev) return hipErrorInvalidValue;
+    a.ctl_host = sc.ctl_host_dev;
+    hipLaunchKernelGGL(k_scatter<true>, dim3(grid_for(sc.p_cap, g.cus * 8)), dim3(WG), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(k_scatter<false>, dim3(grid_for(sc.p_cap, g.cus * 8)), dim3(WG), 0, s, a);
+  }
   return hipGetLastError();
 }
 

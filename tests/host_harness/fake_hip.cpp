@@ -108,7 +108,7 @@ hipError_t launch_walk(const DevIndex&, Scratch&, uint32_t, const WalkGeom&, hip
 uint32_t walk_blocks(const WalkGeom&, uint32_t, uint32_t) { return 0; }
 uint32_t walk_static_chunks(const WalkGeom&, uint32_t, uint32_t, uint32_t) { return 0; }
 hipError_t launch_verify(const uint8_t*, const uint32_t*, const DevIndex&, Scratch&, uint32_t, const WalkGeom&, hipStream_t) { NOT_HERE; }
-hipError_t launch_scatter(Scratch&, uint32_t, const WalkGeom&, hipStream_t, bool) { NOT_HERE; }
+hipError_t launch_scatter(Scratch&, uint32_t, const WalkGeom&, hipStream_t, bool, bool) { NOT_HERE; }
 hipError_t launch_scan_ctl(const uint32_t*, uint32_t*, uint32_t, uint32_t*, uint32_t*, const uint32_t*, uint32_t*, hipStream_t) { NOT_HERE; }
 hipError_t launch_verify_scatter(const uint8_t*, const uint32_t*, const DevIndex&, Scratch&, uint32_t, hipStream_t) { NOT_HERE; }
 hipError_t launch_fixup(Scratch&, uint32_t, hipStream_t) { NOT_HERE; }
