@@ -207,6 +207,7 @@ struct PassCtx {
   bool own_stream = false;    // false: the stream is one of the handle's shared pipe streams
   uint32_t walk_level = 0;    // walk variant of that pass (WalkLevel)
   bool census = false;        // that pass was a census pass
+  bool pipelined = false;     // a device / host pipe (walks with emqxgm::geom_pipe)
   // copy-through input of the next pass enqueued here (pinned host memory, k_tok's TokArgs);
   // cleared by the enqueue
   const uint8_t* src_bytes = nullptr;
@@ -421,6 +422,13 @@ struct emqxgm {
   // ---- reader side (mmu) ----
   PassCtx sync;                    // synchronous calls
   WalkGeom geom;
+  // the walk geometry of pipelined passes (device and host pipes: two passes in flight), never
+  // wider than geom.  Three workgroups per CU instead of four leave room beside a walk for the
+  // other pass's tokenizer and scatter (a walk of four holds ~450 of a SIMD's 512 VGPRs): r04
+  // cfg3 pipelined step 0.412 -> 0.403 ms, 9.71 -> 9.93 G topics/s, though the walk alone is
+  // slower at three (0.319 -> 0.377 ms; one pass at a time keeps four).  tune "walk_wg_per_cu_pipe"
+  WalkGeom geom_pipe;
+  uint32_t pipe_wg_per_cu = 3;
   uint32_t leafp_mask = CF_HMASK;  // depth-code pruning (tune "leaf_prune")
   uint64_t census_depth[2 * CENSUS_DEPTHS] = {};  // the last census pass's loads per level
   uint8_t* d_in_bytes = nullptr;
@@ -1591,6 +1599,14 @@ hipStream_t pipe_stream(emqxgm* h, uint32_t k) {
   return h->pipe_streams[k];
 }
 
+// emqxgm::geom_pipe from geom and pipe_wg_per_cu (same CUs, at most geom's workgroups per CU,
+// so the scratch sized for geom -- spill lanes, census waves -- fits it)
+void set_pipe_geometry(emqxgm* h) {
+  const uint32_t wg = std::max<uint32_t>(1, std::min(h->pipe_wg_per_cu, h->geom.blocks / std::max<uint32_t>(1, h->geom.cus)));
+  h->geom_pipe = walk_geometry(h->cfg.device, wg);
+  h->geom_pipe.xrange_bytes = h->geom.xrange_bytes;
+}
+
 int ctx_init(emqxgm* h, PassCtx& c, hipStream_t shared = nullptr) {
   if (c.stream) return 0;
   if (shared) {
@@ -1727,13 +1743,15 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
                              st));
   c.census = census;
   c.walk_level = (census ? E.census_level : E.walk_level).load(std::memory_order_relaxed);
-  const uint32_t stat = ix.trie_empty ? 0u : walk_static_chunks(h->geom, n, c.walk_level, s.p_cap);
+  // (census passes and the synchronous ones keep the full geometry)
+  const WalkGeom& WG_ = (c.pipelined && !census) ? h->geom_pipe : h->geom;
+  const uint32_t stat = ix.trie_empty ? 0u : walk_static_chunks(WG_, n, c.walk_level, s.p_cap);
   roctx_mark(h->roctx, "k_tok");
   // (per-topic reject counts: only the verification passes write -- and then read -- them;
   // k_tok zeroes them as it goes, like the control words: a memset launch between the passes of
   // two pipes serialised them, r03)
   uint32_t claim0[WALK_SHARDS] = {};
-  if (!ix.trie_empty) walk_claim_init(h->geom, n, c.walk_level, claim0);
+  if (!ix.trie_empty) walk_claim_init(WG_, n, c.walk_level, claim0);
   HIPCHK(h, launch_tok(d_bytes, d_off, n, ix, s, st, stat * STAGE_CHUNK,
                        !ix.trie_empty && (ix.needs_verify || legacy), claim0, c.src_bytes, c.src_off));
   c.src_bytes = nullptr;
@@ -1746,7 +1764,7 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
     HIPCHK(h, hipMemsetAsync(s.row, 0, (size_t)(n + 1) * 4, st));
   } else {
     roctx_mark(h->roctx, "k_walk");
-    HIPCHK(h, launch_walk(ix, s, n, h->geom, st, census ? s.census : nullptr, c.walk_level, stat));
+    HIPCHK(h, launch_walk(ix, s, n, WG_, st, census ? s.census : nullptr, c.walk_level, stat));
     if (h->profiling) HIPCHK(h, hipEventRecord(c.ev[2], st));
     if (!legacy) {
       // pairs of filters made of short (exact) tokens need no byte check (gm_verify.inc)
@@ -2303,6 +2321,7 @@ int emqxgm_create(const emqxgm_cfg* cfg, emqxgm_t** out) {
   h->wstream = h->sync.stream;
   h->geom = walk_geometry(h->cfg.device, h->cfg.walk_wg_per_cu);
   h->geom.xrange_bytes = h->xrange_bytes;
+  set_pipe_geometry(h);
   int rc = commit_locked(h);  // empty index: epoch 1
   if (rc) {
     emqxgm_destroy(h);
@@ -3039,6 +3058,7 @@ int emqxgm_match_device_submit(emqxgm_t* h, const uint8_t* d_bytes, const uint32
     return -EIO;
   }
   int rc = ctx_init(h, p.c, ps);
+  p.c.pipelined = true;
   if (rc) return rc;
   rc = pass_prepare(h, p.c, n, bytes_len);
   if (rc < 0) return rc;
@@ -3118,6 +3138,7 @@ int batch_submit(emqxgm* h, const uint8_t* bytes, const uint32_t* offsets, uint3
     return -EIO;
   }
   int rc = ctx_init(h, p.c, ps);
+  p.c.pipelined = true;
   if (rc) return rc;
   rc = pass_prepare(h, p.c, n, nb);
   if (rc < 0) return rc;
@@ -3252,6 +3273,7 @@ int gm_reserve_windows(emqxgm_t* h, uint32_t n, uint64_t nb) {
     hipStream_t ps = pipe_stream(h, k);
     if (!ps) return -EIO;
     int rc = ctx_init(h, p.c, ps);
+    p.c.pipelined = true;
     if (rc || (rc = pass_prepare(h, p.c, n, nb)) < 0 ||
         (rc = host_pipe_reserve(h, p, n, std::max<uint64_t>(nb, 1), 1)))
       return rc < 0 ? rc : 0;
@@ -3711,7 +3733,16 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
     h->cfg.walk_wg_per_cu = (uint32_t)value;
     h->geom = walk_geometry(h->cfg.device, h->cfg.walk_wg_per_cu);
     h->geom.xrange_bytes = h->xrange_bytes;
+    set_pipe_geometry(h);
     return 0;  // spill scratch is re-sized by the next match (ensure_scratch)
+  }
+  if (strcmp(key, "walk_wg_per_cu_pipe") == 0) {  // pipelined passes' walk (never above the other)
+    if (value < 1 || value > 16) return -EINVAL;
+    std::lock_guard<std::mutex> g(h->mmu);
+    if (int rc = drain_pipes(h)) return rc;
+    h->pipe_wg_per_cu = (uint32_t)value;
+    set_pipe_geometry(h);
+    return 0;
   }
   if (strcmp(key, "leaf_prune") == 0) {  // 1 (default): the walk skips leaf-only children
     if (value < 0 || value > 1) return -EINVAL;
@@ -3744,6 +3775,7 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
     if (int rc = drain_pipes(h)) return rc;  // in-flight passes read the geometry
     h->xrange_bytes = (uint64_t)value << 10;
     h->geom.xrange_bytes = h->xrange_bytes;
+    h->geom_pipe.xrange_bytes = h->xrange_bytes;
     return 0;
   }
   if (strcmp(key, "delta_commit") == 0) {
