@@ -39,7 +39,7 @@ shift
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 KRE="k_walk|k_tok|k_exact|k_scatter|k_verify|k_scan"
-NOCPU="--no-cpu-baseline --no-e2e --nif="
+NOCPU="--no-cpu-baseline --no-e2e --nif= --settle-s 0"
 
 step_tests() {
   local args=${1:-tests,-m,gpu}
