@@ -2292,6 +2292,7 @@ struct WriterLock {
 extern "C" {
 
 int emqxgm_abi_version(void) { return EMQXGM_ABI_VERSION; }
+int emqxgm_device_pipes(void) { return EMQXGM_PIPES; }
 
 int emqxgm_create(const emqxgm_cfg* cfg, emqxgm_t** out) {
   if (!out) return -EINVAL;

@@ -114,6 +114,7 @@ _U32P = C.POINTER(C.c_uint32)
 _U64P = C.POINTER(C.c_uint64)
 SYMBOLS = {
     "emqxgm_abi_version": (C.c_int, []),
+    "emqxgm_device_pipes": (C.c_int, []),
     "emqxgm_create": (C.c_int, [C.POINTER(_Cfg), C.POINTER(_P)]),
     "emqxgm_destroy": (None, [_P]),
     "emqxgm_trie_insert": (C.c_int, [_P, C.c_char_p, C.c_uint32, _U32P]),
@@ -300,6 +301,7 @@ class Engine:
             raise EngineError(f"emqxgm_create failed ({rc}): no usable HIP device {device}")
         self._h = h
         self._pinned = []
+        self.PIPES = int(self._lib.emqxgm_device_pipes())  # EMQXGM_PIPES of this build
 
     def close(self):
         if getattr(self, "_h", None):
@@ -506,7 +508,7 @@ class Engine:
         return DeviceResult(o.n, o.n_pairs, o.row_ptr or 0, o.filter_id or 0, o.exact_id or 0,
                             o.n_words or 0)
 
-    PIPES = 2  # EMQXGM_PIPES
+    PIPES = 2  # EMQXGM_PIPES (each engine reads its library's: emqxgm_device_pipes)
 
     def match_device_submit(self, d_bytes: int, d_off: int, n: int, bytes_len: int) -> int:
         """emqxgm_match_device_submit: enqueue a device pass, return its ticket (pipelined: up

@@ -217,7 +217,11 @@ int emqxgm_match_device(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_o
  * it before ticket k was waited for returns -EBUSY.  The caller keeps d_bytes/d_offsets alive
  * until the wait.  A commit first completes every pass in flight (results stay retrievable).
  * Results are identical to emqxgm_match_device's. */
+#ifndef EMQXGM_PIPES
 #define EMQXGM_PIPES 2
+#endif
+/* EMQXGM_PIPES of the library's build (a caller compiled against another header asks). */
+int emqxgm_device_pipes(void);
 
 /* Pinned (page-locked) host memory on the handle's device, for the caller's topic staging: a
  * batcher that packs its window into it gets full-speed H2D copies from emqxgm_match_batch.

@@ -39,7 +39,8 @@ shift
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 KRE="k_walk|k_tok|k_exact|k_scatter|k_verify|k_scan"
-NOCPU="--no-cpu-baseline --no-e2e --nif= --settle-s 0"
+NOCPU="--no-cpu-baseline --no-e2e --nif="
+PROF="$NOCPU --settle-s 0"  # profiled runs: every launch is profiled, so no settle phase
 
 step_tests() {
   local args=${1:-tests,-m,gpu}
@@ -68,7 +69,7 @@ step_bench() {
 
 step_onepass() {
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/onepass_c$1 -o run --output-format csv \
-    -- python3 $R/bench.py --cfg $1 --no-pipeline $NOCPU --steps 20 --warmup 3 \
+    -- python3 $R/bench.py --cfg $1 --no-pipeline $PROF --steps 20 --warmup 3 \
     > $O/onepass_c$1.json 2> $O/onepass_c$1.log
 }
 
@@ -80,14 +81,14 @@ step_prof() {
   extra=${extra//,/ }
   [ $c = 3 ] && steps=10
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/stats_$d -o run --output-format csv \
-    -- python3 $R/bench.py --cfg $c $NOCPU $extra --steps $steps --warmup 2 \
+    -- python3 $R/bench.py --cfg $c $PROF $extra --steps $steps --warmup 2 \
     > $O/stats_$d.json 2> $O/stats_$d.log || return 1
   local i=0 grp
   for grp in "FETCH_SIZE" "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" \
              "TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TOTAL_CACHE_ACCESSES_sum"; do
     i=$((i+1))
     timeout -s KILL 400 rocprofv3 --pmc $grp --kernel-include-regex "$KRE" -d $O/pmc_$d/p$i -o run \
-      --output-format csv -- python3 $R/bench.py --cfg $c $NOCPU $extra --steps 3 --warmup 1 \
+      --output-format csv -- python3 $R/bench.py --cfg $c $PROF $extra --steps 3 --warmup 1 \
       > $O/pmc_${d}_p$i.log 2>&1 || return 1
   done
   python3 $R/tools/pmc_summary.py $O/pmc_$d > $O/pmc_${d}_summary.txt 2>&1
@@ -101,7 +102,7 @@ step_sq() {
              "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE"; do
     i=$((i+1))
     timeout -s KILL 300 rocprofv3 --pmc $grp --kernel-include-regex "k_walk" -d $O/sq_cfg$c/p$i -o run \
-      --output-format csv -- python3 $R/bench.py --cfg $c $topics $NOCPU --steps 3 --warmup 1 \
+      --output-format csv -- python3 $R/bench.py --cfg $c $topics $PROF --steps 3 --warmup 1 \
       > $O/sq_cfg${c}_p$i.log 2>&1 || return 1
   done
   python3 $R/tools/pmc_summary.py $O/sq_cfg$c > $O/sq_cfg${c}_summary.txt 2>&1
