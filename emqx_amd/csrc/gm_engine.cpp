@@ -3176,8 +3176,10 @@ int batch_submit(emqxgm* h, const uint8_t* bytes, const uint32_t* offsets, uint3
     }
     // with the gather behind the pass the row pointers travel in its block (one copy less)
     p.rows_enq = !want_fb || h->host_out_mode == 1;
-    if ((rc = pass_submit(h, p.c, p.d_bytes, p.d_off, n, false, false)) ||
-        (p.rows_enq && (rc = host_pipe_copy_out(h, p))) ||
+    rc = pass_submit(h, p.c, p.d_bytes, p.d_off, n, false, false);
+    p.c.src_bytes = nullptr;  // (consumed by the enqueue; never left for a later pass)
+    p.c.src_off = nullptr;
+    if (rc || (p.rows_enq && (rc = host_pipe_copy_out(h, p))) ||
         (want_fb && (rc = host_pipe_enqueue_gather(h, p))))
       return rc;
     if (!p.fin) HIPCHK(h, hipEventCreateWithFlags(&p.fin, hipEventDisableTiming));
