@@ -433,7 +433,10 @@ def _window_sweep(Batcher, eng, w, sizes):
     call per window, ~tens of us), as a NIF batcher process would make the same three calls."""
     off = w.toff.astype(np.int64)
     out = {}
-    for W in sizes:
+    # every size with EMQXGM_HOST_PIPES windows in flight, and the two smallest also with one
+    # (the latency of a window that waits for no other)
+    runs = [(W, eng.HOST_PIPES) for W in sizes] + [(W, 1) for W in sorted(sizes)[:2]]
+    for W, depth in runs:
         W = min(W, w.nt)
         b = Batcher(eng, window_topics=W, window_bytes=64 * W)
         inflight, lat = [], []
@@ -456,7 +459,7 @@ def _window_sweep(Batcher, eng, w, sizes):
                 k = b.add_many(buf, rel, i)
                 state["pos"] += 1
                 added += k
-                if len(inflight) == eng.HOST_PIPES:
+                if len(inflight) == depth:
                     collect()
                 inflight.append(b.flush())
             while inflight:
@@ -470,14 +473,15 @@ def _window_sweep(Batcher, eng, w, sizes):
         el = time.perf_counter() - t0
         b.close()
         la = np.array(lat, np.float64) / 1e3
-        out[str(W)] = {"topics_per_s": round(state["done"] / el, 1), "windows": len(lat),
-                       "latency_us_p50": round(float(np.percentile(la, 50)), 1),
-                       "latency_us_p99": round(float(np.percentile(la, 99)), 1)}
+        key = str(W) if depth == eng.HOST_PIPES else f"{W}_inflight{depth}"
+        out[key] = {"topics_per_s": round(state["done"] / el, 1), "windows": len(lat),
+                    "latency_us_p50": round(float(np.percentile(la, 50)), 1),
+                    "latency_us_p99": round(float(np.percentile(la, 99)), 1)}
     out["includes"] = ("topics packed into pinned windows, H2D, the device pass, row pointers + "
                        "filter ids + exact ids and every pair's filter bytes (gathered on the "
-                       "device) in pinned host memory (emqxgm_batcher_*), 3 windows in flight; "
-                       "latency = flush -> collected; the caller's reading of the result (the "
-                       "NIF's term building) is not included")
+                       "device) in pinned host memory (emqxgm_batcher_*), 3 windows in flight "
+                       "(*_inflight1: one); latency = flush -> collected; the caller's reading of "
+                       "the result (the NIF's term building) is not included")
     return out
 
 
