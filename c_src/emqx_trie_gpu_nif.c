@@ -332,8 +332,9 @@ static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
 
 static ErlNifFunc funcs[] = {
     {"open", 5, nif_open, ERL_NIF_DIRTY_JOB_IO_BOUND},
-    {"route_set", 3, nif_route_set, 0},
-    {"sync_begin", 1, nif_sync_begin, 0},
+    /* the writer lock: held through a commit's full build (seconds at 10M filters) */
+    {"route_set", 3, nif_route_set, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"sync_begin", 1, nif_sync_begin, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"sync_end", 2, nif_sync_end, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"commit", 1, nif_commit, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"empty", 1, nif_empty, 0},
