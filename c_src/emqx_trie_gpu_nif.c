@@ -342,7 +342,7 @@ static ErlNifFunc funcs[] = {
     {"route_member", 2, nif_route_member, 0},
     {"match_async", 3, nif_match_async, 0},
     {"cancel", 2, nif_cancel, ERL_NIF_DIRTY_JOB_IO_BOUND},
-    {"tune", 3, nif_tune, 0},
+    {"tune", 3, nif_tune, ERL_NIF_DIRTY_JOB_IO_BOUND},  /* some keys drain the passes in flight */
     {"stats", 1, nif_stats, 0},
 };
 
