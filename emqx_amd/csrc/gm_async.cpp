@@ -40,13 +40,7 @@
 #include <vector>
 
 #include "../../include/emqx_gpumatch.h"
-
-// gm_engine.cpp: emqxgm_match_batch_submit_filters without its O(n) check that the offsets
-// increase (a window's are built increasing here)
-int gm_submit_window(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets, uint32_t n,
-                     uint64_t* ticket);
-// gm_engine.cpp: every host pipe of h sized for windows of n topics / nb bytes
-int gm_reserve_windows(emqxgm_t* h, uint32_t n, uint64_t nb);
+#include "gm_internal.h"
 
 namespace {
 

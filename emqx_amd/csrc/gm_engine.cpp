@@ -28,6 +28,7 @@
 
 #include "../../include/emqx_gpumatch.h"
 #include "gm_common.h"
+#include "gm_internal.h"
 #include "gm_kernels.h"
 #include "gm_roctx.h"
 
@@ -187,7 +188,7 @@ struct Epoch {
   std::atomic<uint32_t> walk_level{WALK_SHALLOW};
   std::atomic<uint32_t> census_level{WALK_SHALLOW};  // the same for diagnostic census passes
                                                       // (their unpruned walks stack deeper)
-  std::atomic<bool> ready_seen{false};  // `ready` has completed (a pass then skips its query)
+  mutable std::atomic<bool> ready_seen{false};  // `ready` has completed (passes skip the query)
   ~Epoch() {
     if (ready) (void)hipEventDestroy(ready);
   }
@@ -1728,7 +1729,7 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
   // the epoch's uploads / patches must have landed (a full build's have: its wait is skipped)
   if (!E.ready_seen.load(std::memory_order_relaxed)) {
     if (hipEventQuery(E.ready) == hipSuccess)
-      const_cast<Epoch&>(E).ready_seen.store(true, std::memory_order_relaxed);
+      E.ready_seen.store(true, std::memory_order_relaxed);
     else
       HIPCHK(h, hipStreamWaitEvent(st, E.ready, 0));
   }

@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "../../include/emqx_gpumatch.h"
+#include "../../emqx_amd/csrc/gm_internal.h"
 
 extern "C" {
 void* ref_create(int compact);
