@@ -792,7 +792,10 @@ hipError_t launch_scatter(Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_
   if (fuse_scan) {
     if (n > SCAN_TILE || !sc.ctl_host_dev) return hipErrorInvalidValue;
     a.ctl_host = sc.ctl_host_dev;
-    hipLaunchKernelGGL(k_scatter<true>, dim3(grid_for(sc.p_cap, g.cus * 8)), dim3(WG), 0, s, a);
+    // (a small batch's chunks are few: 128 blocks stride over them; the full grid was
+    // thousands of blocks with nothing to do)
+    hipLaunchKernelGGL(k_scatter<true>, dim3(std::min<uint32_t>(grid_for(sc.p_cap, g.cus * 8), 128u)),
+                       dim3(WG), 0, s, a);
   } else {
     hipLaunchKernelGGL(k_scatter<false>, dim3(grid_for(sc.p_cap, g.cus * 8)), dim3(WG), 0, s, a);
   }
