@@ -145,6 +145,10 @@ struct emqxgm_async {
   std::thread flusher;
   std::vector<std::thread> completers;
   std::atomic<uint64_t> st_direct{0}, st_busy{0}, st_too_big{0};
+  // EMQXGM_ASYNC_PUBLISH: per handle, the bytes of a window's route entries' filters
+  std::vector<std::vector<uint8_t>> rf_bytes;
+  std::vector<std::vector<uint64_t>> rf_off;
+  bool publish_mode() const { return (cfg.flags & EMQXGM_ASYNC_PUBLISH) != 0; }
   uint64_t st_windows = 0, st_cancelled = 0, st_errors = 0, st_delivered = 0;
 
   // Seals slot si (with mu held): no reservation after this one succeeds; the window goes to the
@@ -371,8 +375,9 @@ struct emqxgm_async {
         g.unlock();
         s.flush_ns = mono_ns();
         uint64_t tk = 0;
-        // the filter-byte gather and every result copy go behind the pass: one wait
-        const int rc = gm_submit_window(hs[k], s.bytes, s.off, s.n, &tk);
+        // the filter-byte gather and every result copy go behind the pass: one wait (a publish
+        // layer's completer runs the whole pass itself)
+        const int rc = publish_mode() ? 0 : gm_submit_window(hs[k], s.bytes, s.off, s.n, &tk);
         g.lock();
         s.ticket = tk;
         s.status = rc;
@@ -411,6 +416,19 @@ struct emqxgm_async {
     for (auto& c : cv_comp) c->notify_all();
   }
 
+  // The bytes of every route entry's To of a publish window (one registry copy per window).
+  int route_bytes(uint32_t k, const emqxgm_publish_out& po) {
+    auto& b = rf_bytes[k];
+    auto& o = rf_off[k];
+    o.resize(po.n_routes + 1);
+    if (b.empty()) b.resize(1u << 16);
+    for (;;) {
+      const int rc = emqxgm_filters_copy(hs[k], po.route_filter, po.n_routes, b.data(), b.size(), o.data());
+      if (rc != -ENOSPC) return rc;
+      b.resize(std::max<uint64_t>(o[po.n_routes], 2 * b.size()));
+    }
+  }
+
   void completer_loop(uint32_t k) {
     std::unique_lock<std::mutex> g(mu);
     for (;;) {
@@ -423,7 +441,13 @@ struct emqxgm_async {
       const uint32_t* foff = nullptr;
       const uint8_t* fb = nullptr;
       int rc = s.status;
-      if (rc == 0) rc = emqxgm_match_batch_wait_filters(hs[k], s.ticket, &bo, &foff, &fb);
+      emqxgm_publish_out po{};
+      if (rc == 0 && publish_mode()) {
+        rc = emqxgm_publish_batch(hs[k], s.bytes, s.off, s.n, &po);
+        if (rc == 0) rc = route_bytes(k, po);
+      } else if (rc == 0) {
+        rc = emqxgm_match_batch_wait_filters(hs[k], s.ticket, &bo, &foff, &fb);
+      }
       const uint64_t done = mono_ns();
       g.lock();
       inflight[k].pop_front();
@@ -434,7 +458,18 @@ struct emqxgm_async {
       w.n = s.n;
       w.tag = reinterpret_cast<const uint64_t*>(s.tag.get());
       w.owner = reinterpret_cast<const uint64_t*>(s.owner.get());
-      if (rc == 0) {
+      if (rc == 0 && publish_mode()) {
+        w.n_routes = po.n_routes;
+        w.n_deliveries = po.n_deliveries;
+        w.route_ptr = po.route_ptr;
+        w.route_filter = po.route_filter;
+        w.route_dest = po.route_dest;
+        w.deliver_ptr = po.deliver_ptr;
+        w.deliver_filter = po.deliver_filter;
+        w.deliver_sub = po.deliver_sub;
+        w.rfoff = rf_off[k].data();
+        w.rfbytes = rf_bytes[k].data();
+      } else if (rc == 0) {
         w.n_pairs = bo.n_pairs;
         w.row = bo.row_ptr;
         w.filter_id = bo.filter_id;
@@ -476,7 +511,8 @@ int emqxgm_async_create(emqxgm_t* const* hs, uint32_t n_handles, const emqxgm_as
   if (!a->cfg.window_bytes) a->cfg.window_bytes = 64u * a->cfg.window_topics;
   if (!a->cfg.window_us) a->cfg.window_us = 50;
   if (!a->cfg.queued_windows) a->cfg.queued_windows = 2;
-  if (a->cfg.window_topics >= SEAL || a->cfg.window_bytes >= SEAL) {
+  if (a->cfg.window_topics >= SEAL || a->cfg.window_bytes >= SEAL ||
+      (a->cfg.flags & ~EMQXGM_ASYNC_PUBLISH)) {
     delete a;
     return -EINVAL;
   }
@@ -506,8 +542,8 @@ int emqxgm_async_create(emqxgm_t* const* hs, uint32_t n_handles, const emqxgm_as
     a->free_slots.push_back((int)(n_slots - 1 - i));
   }
   // each engine's host pipes at the windows' size now (a reallocation later would stall every
-  // pass on the device)
-  for (uint32_t k = 0; k < n_handles && !rc; ++k)
+  // pass on the device; a publish layer's passes go through the handle's synchronous context)
+  for (uint32_t k = 0; k < n_handles && !rc && !(a->cfg.flags & EMQXGM_ASYNC_PUBLISH); ++k)
     rc = gm_reserve_windows(a->hs[k], a->cfg.window_topics, a->cfg.window_bytes);
   if (rc) {
     for (size_t i = 0; i < a->slots.size(); ++i) {
@@ -518,6 +554,8 @@ int emqxgm_async_create(emqxgm_t* const* hs, uint32_t n_handles, const emqxgm_as
     return rc;
   }
   a->inflight.resize(n_handles);
+  a->rf_bytes.resize(n_handles);
+  a->rf_off.resize(n_handles);
   a->outstanding.assign(n_handles, 0);
   for (uint32_t k = 0; k < n_handles; ++k) a->cv_comp.emplace_back(new std::condition_variable());
   {
@@ -572,7 +610,15 @@ int emqxgm_async_match(emqxgm_async_t* a, const uint8_t* topic, uint32_t len, ui
     x.first_ns = mono_ns();
     const int rc = a->place(x);
     if (rc == -EBUSY) a->st_busy.fetch_add(1, std::memory_order_relaxed);
-    if (rc == 0) a->st_direct.fetch_add(1, std::memory_order_relaxed);
+    if (rc == 0) {
+      a->st_direct.fetch_add(1, std::memory_order_relaxed);
+      // the window may have been empty and the flusher asleep with no deadline: it arms the
+      // window_us timer for this call, as a chunk's first call does
+      if (a->flusher_idle.load(std::memory_order_seq_cst)) {
+        std::lock_guard<std::mutex> g(a->mu);
+        a->cv_flush.notify_one();
+      }
+    }
     return rc;
   }
   Chunk* c = a->my_chunk();
@@ -633,10 +679,13 @@ int emqxgm_async_cancel(emqxgm_async_t* a, uint64_t tag, uint64_t owner) {
   for (size_t i = 0; i < a->slots.size() && delivering < 0; ++i) {
     Slot& s = *a->slots[i];
     if (s.state == FREE) continue;
-    // an open window's calls: those reserved so far (the caller's own call is complete)
-    const uint32_t m = s.state == OPEN || s.state == READY
-                           ? std::min<uint32_t>((uint32_t)(s.cursor.load() >> 32), a->cfg.window_topics)
-                           : s.n;
+    // an open window's calls: the reservations so far that fit (the caller's own call is
+    // complete); a sealed one's: those made before the seal that fit.  Places past them hold
+    // tags of earlier uses of the slot.
+    const uint32_t lim = std::min(s.limit.load(), a->cfg.window_topics);
+    const uint32_t m = s.state == OPEN    ? std::min<uint32_t>((uint32_t)(s.cursor.load() >> 32), lim)
+                       : s.state == READY ? std::min<uint32_t>(s.reserved, lim)
+                                          : s.n;
     for (uint32_t j = 0; j < m; ++j) {
       if (s.tag[j].load(std::memory_order_relaxed) != tag ||
           s.owner[j].load(std::memory_order_relaxed) != owner)

@@ -17,11 +17,13 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <new>
 #include <shared_mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -268,6 +270,7 @@ struct TrieModel {
   bool needs_verify = false;
   uint32_t max_depth = 0;
   uint64_t n_trie = 0, n_route = 0;
+  uint64_t n_nodes0 = 0, fv_words0 = 0;  // nodes / verify words at the build (headroom used since)
   // exact route keys: entry per committed key, bitmaps over entries.  Two regions of one
   // table: plain (non-wildcard) keys in buckets [0, xcap_p), wildcard keys in [xcap_p,
   // xcap_p + xcap_w); a name can only equal a key of its own kind (same bytes, same words).
@@ -361,6 +364,34 @@ struct FanModel {
   uint64_t rt_used = 0, rt_cap = 0, dl_used = 0, dl_cap = 0, garbage = 0;
   std::vector<uint4> ent;
   uint32_t *d_ent = nullptr, *d_rt = nullptr, *d_dl = nullptr;  // owned by emqxgm::o_fan
+};
+
+// What a full build reads and how (build_model / upload_tables).  A background build (bg) runs
+// on a thread of its own while writers keep changing the registry: it reads the registry in
+// slices (for_slices) and records per filter the membership it read (seen: bit 0 trie member,
+// bit 1 route key), from which its install replays every change made since (install_build).
+struct BuildIn {
+  bool bg = false;
+  uint64_t nf = 0;           // filters [0, nf) are read
+  uint64_t n_trie_hint = 0;  // expected trie members (edge map sizing)
+  uint64_t test_mask = 0, fmask = ~0ull;
+  uint32_t fat_mode = 1, keyed_mode = 1;
+  std::vector<uint8_t>* seen = nullptr;
+};
+
+// A full build running beside the writers (r05).  Until its install the readers keep the index
+// they have, and commits patch it (delta commits); the install swaps the build's tables in with
+// the changes since its start replayed onto them as one more delta.
+struct BuildJob {
+  BuildIn in;
+  std::vector<uint8_t> seen;
+  std::vector<uint32_t> covered;  // changes pending at the start: the build includes them
+  TrieModel m;
+  DevIndex nx;  // its table fields (upload_tables)
+  OwnerP o;     // and their buffers
+  int rc = 0;
+  std::chrono::steady_clock::time_point t0;
+  double build_ms = 0;
 };
 
 inline bool bit(const std::vector<uint64_t>& b, uint64_t i) { return (b[i >> 6] >> (i & 63)) & 1; }
@@ -542,9 +573,23 @@ struct emqxgm {
   uint64_t h_stage_bytes = 0;
   hipEvent_t patch_ev = nullptr;    // the last patch upload + launch
   uint32_t delta_mode = 1;        // 0: always rebuild, 1: delta when small, 2: delta if possible
+  uint64_t delta_max = 0;         // "small": changes per delta (tune "delta_max"; 0: max(4096, n/8))
   uint32_t fat_mode = 1;          // 1: fat buckets at full builds (gm_common.h FAT_ID), 0: none
   uint32_t keyed_mode = 1;        // token-keyed parents at full builds (select_keyed): 0 / 1 / 2
   bool roctx = false;             // roctx ranges / launch markers (gm_roctx.h)
+
+  // ---- background full builds (r05; wmu) ----
+  std::unique_ptr<BuildJob> job;   // in flight (installed by its own thread when done)
+  std::thread builder;             // its thread (joined before the next one starts)
+  std::condition_variable bcv;     // a job was installed
+  uint64_t builds_started = 0, builds_done = 0;
+  int build_rc = 0;                // the last install's result
+  std::vector<uint32_t> build_log; // filters whose membership changed since the job started
+  // full builds of registries of at least this many filters run in the background (tune
+  // "bg_build"; 0: never): a commit the current tables cannot take waits for the build, every
+  // other commit meanwhile is a delta on the index the readers have
+  uint64_t bg_min = 16384;
+  std::atomic<uint32_t> bg_delay_ms{0};  // tune "bg_delay_ms": a build holds its install back (tests)
 };
 
 namespace {
@@ -907,10 +952,30 @@ void commit_stats(emqxgm* h, double ms, bool delta) {
   (delta ? h->st.delta_commits : h->st.full_commits) += 1;
 }
 
+// f(i0, i1, filters, pool) over the registered filters [0, n) in slices.  A background build
+// (bg) reads the registry while writers change it: it holds the registry lock shared for one
+// slice at a time and, before each slice, takes and drops the writer lock, so that a writer
+// waiting for either gets in first -- a subscribe waits for at most one slice, never for the
+// build.  (A filter's bytes, offset and length never change once registered; its membership
+// flags only change under the registry lock held exclusively.)
+constexpr uint64_t REG_SLICE = 8192;
+template <class F>
+void for_slices(emqxgm* h, bool bg, uint64_t n, F f) {
+  for (uint64_t i0 = 0; i0 < n; i0 += REG_SLICE) {
+    std::shared_lock<std::shared_mutex> g(h->pmu, std::defer_lock);
+    if (bg) {
+      { std::lock_guard<std::mutex> w(h->wmu); }
+      g.lock();
+    }
+    f(i0, std::min<uint64_t>(n, i0 + REG_SLICE), h->filters.data(), h->pool.data());
+  }
+}
+
 // The device tables of a host model (its node slots, side array, verify bits, exact entries,
 // overflow bits, multi lists): generated from the model -- a full build and a snapshot load
-// share this -- uploaded into a new table set, and h->ix pointed at them.
-int upload_model(emqxgm* h, TrieModel& m) {
+// share this -- and uploaded into a new table set: nx's table fields, o its buffers (the caller
+// swaps them in; nx's pool and fan-out fields are left as they are).
+int upload_tables(emqxgm* h, const BuildIn& in, TrieModel& m, DevIndex& nx, OwnerP& o) {
   const uint64_t n_nodes = m.parent.size();
   std::vector<uint4> eslots(SLOT_U4 * m.ecap, make_uint4(0u, 0u, 0u, 0u));
   for (uint64_t i = 0; i < m.ecap; ++i)
@@ -919,19 +984,19 @@ int upload_model(emqxgm* h, TrieModel& m) {
     if (m.slot[c] != DEAD && m.slot[c] != ROOTH) m.node_slot(c, &eslots[SLOT_U4 * m.slot[c]]);
   std::vector<uint32_t> tn_of(m.tn_cap, NONE);
   for (size_t i = 0; i < n_nodes; ++i) tn_of[i] = m.tn[i];
-  const uint64_t fmask =
-      h->cfg.full_hash_bits >= 64 ? ~0ull : ((1ull << h->cfg.full_hash_bits) - 1ull);
+  const uint64_t fmask = in.fmask;
   const uint64_t xcap = m.xcap_p + m.xcap_w;
   std::vector<uint4> xslots(xcap * XBUCKET * XENT_U4, make_uint4(0u, 0u, 0u, 0u));
   for (uint64_t e = 0; e < xcap * XBUCKET; ++e) xslots[XENT_U4 * e].y = bit(m.xtomb, e) ? TOMB : NONE;
-  for (uint32_t id = 0; id < m.xpos.size(); ++id) {
-    if (m.xpos[id] == NONE) continue;
-    const Filter& f = h->filters[id];
-    const uint8_t* p = h->pool.data() + f.off;
-    xent(key_hash(p, f.len, fmask), id, p, f.len, &xslots[XENT_U4 * (uint64_t)m.xpos[id]]);
-  }
+  for_slices(h, in.bg, m.xpos.size(), [&](uint64_t i0, uint64_t i1, const Filter* F, const uint8_t* pool) {
+    for (uint64_t id = i0; id < i1; ++id) {
+      if (m.xpos[id] == NONE) continue;
+      const uint8_t* p = pool + F[id].off;
+      xent(key_hash(p, F[id].len, fmask), (uint32_t)id, p, F[id].len,
+           &xslots[XENT_U4 * (uint64_t)m.xpos[id]]);
+    }
+  });
   std::vector<DevBuf> nbufs;
-  DevIndex nx = h->ix;  // pool and fan-out pointers already set
   int rc = 0;
   if ((rc = dev_upload(h, nbufs, eslots, &nx.edges)) ||
       (rc = dev_upload(h, nbufs, m.multi, &nx.multi)) ||
@@ -958,14 +1023,50 @@ int upload_model(emqxgm* h, TrieModel& m) {
   nx.root_pcf = root_p ? m.pcf(root_p) : 0u;
   nx.root_phf = root_p ? m.phf(root_p) : NONE;
   m.root_half(nx);
-  nx.test_mask = h->test_mask;
+  nx.test_mask = in.test_mask;
   nx.needs_verify = m.needs_verify;
   nx.full_mask = fmask;
   nx.max_depth = m.max_depth;
   nx.trie_empty = (m.n_trie == 0);
   nx.plain_empty = (m.n_route_p == 0);
   nx.wild_empty = (m.n_route_w == 0);
-  h->o_tab = std::make_shared<DevOwner>(std::move(nbufs));  // old tables live on with their epochs
+  o = std::make_shared<DevOwner>(std::move(nbufs));
+  return 0;
+}
+
+// The table fields of `from` into `to` (its pool and fan-out fields stay).
+void set_tables(DevIndex& to, const DevIndex& from) {
+  DevIndex x = from;
+  x.fan = to.fan;
+  x.rt_dst = to.rt_dst;
+  x.dl_sub = to.dl_sub;
+  x.fan_nf = to.fan_nf;
+  x.fbytes = to.fbytes;
+  x.foff = to.foff;
+  x.fver = to.fver;
+  x.leafp_mask = to.leafp_mask;
+  to = x;
+}
+
+BuildIn build_in(emqxgm* h, bool bg) {
+  BuildIn in;
+  in.bg = bg;
+  in.nf = h->filters.size();
+  in.n_trie_hint = h->n_trie_pending;
+  in.test_mask = h->test_mask;
+  in.fmask = h->cfg.full_hash_bits >= 64 ? ~0ull : ((1ull << h->cfg.full_hash_bits) - 1ull);
+  in.fat_mode = h->fat_mode;
+  in.keyed_mode = h->keyed_mode;
+  return in;
+}
+
+// The tables of model m uploaded and swapped into the writer's index (the old ones live on with
+// the epochs that read them): a blocking full build and a snapshot load.
+int upload_model(emqxgm* h, TrieModel& m) {
+  DevIndex nx = h->ix;
+  OwnerP o;
+  if (int rc = upload_tables(h, build_in(h, false), m, nx, o)) return rc;
+  h->o_tab = std::move(o);
   h->ix = nx;
   return 0;
 }
@@ -1017,59 +1118,64 @@ void select_keyed(TrieModel& m, uint32_t mode) {
   for (uint32_t x = 1; x < nn; ++x) m.keyed[x] = ok[x] && n_crowded[x] * 16 <= m.nlit[x];
 }
 
-// Full build of the device index from the pending registry; swaps it in and rebuilds the host
-// model (TrieModel) that later delta commits patch.
-int commit_full(emqxgm* h) {
-  const uint64_t test_mask = h->test_mask;
-  const uint64_t fmask =
-      h->cfg.full_hash_bits >= 64 ? ~0ull : ((1ull << h->cfg.full_hash_bits) - 1ull);
-  const uint64_t nf = h->filters.size();
-  h->tm = TrieModel();  // frees the old model before the new one is built
-  TrieModel m;
+// The host model (TrieModel) of a full build of the registry's filters [0, in.nf): trie nodes,
+// edge-slot placement, exact-key placement.  No device work; a background build runs it beside
+// the writers (in.bg, for_slices).
+int build_model(emqxgm* h, const BuildIn& in, TrieModel& m) {
+  const uint64_t test_mask = in.test_mask;
+  const uint64_t fmask = in.fmask;
+  const uint64_t nf = in.nf;
 
   // ---- trie: nodes keyed by (parent, level token); root = node 0 ----
   m.new_node(NONE, 0);
-  m.emap.init(std::max<uint64_t>(1024, h->n_trie_pending * 2));
+  m.emap.init(std::max<uint64_t>(1024, in.n_trie_hint * 2));
   ListBuild lb;
   m.fvbits.assign((nf + 31) / 32 + 1, 0u);
   std::vector<uint64_t> toks;
   std::vector<uint8_t> is_plus, is_hash;
-  for (uint32_t id = 0; id < h->filters.size(); ++id) {
-    const Filter& f = h->filters[id];
-    if (!f.in_trie) continue;
-    ++m.n_trie;
-    bool hashed;
-    tokenize(h->pool.data() + f.off, f.len, test_mask, toks, is_plus, is_hash, hashed);
-    if (hashed) {
-      m.fvbits[id >> 5] |= 1u << (id & 31);
-      m.needs_verify = true;
-    }
-    const size_t nw = toks.size();
-    const bool hash_last = is_hash[nw - 1];
-    const size_t path_len = hash_last ? nw - 1 : nw;  // '#' last: attach to the parent node
-    uint32_t cur = 0;
-    for (size_t w = 0; w < path_len; ++w) {
-      const uint64_t tok = is_plus[w] ? PLUS_TOK : toks[w];
-      bool ins;
-      uint32_t* v = m.emap.get_or_insert(cur, tok, ins);
-      if (ins) {
-        if (m.parent.size() >= MAX_NODES) {
-          set_err(h, "trie exceeds 2^26-1 nodes");
-          return -E2BIG;
-        }
-        const uint32_t child = m.new_node(cur, tok);
-        *v = child;
-        if (is_plus[w])
-          m.pchild[cur] = child;
-        else
-          m.nlit[cur] += 1;
+  int rc = 0;
+  for_slices(h, in.bg, nf, [&](uint64_t i0, uint64_t i1, const Filter* F, const uint8_t* pool) {
+    for (uint64_t i = i0; i < i1 && !rc; ++i) {
+      const uint32_t id = (uint32_t)i;
+      const Filter& f = F[id];
+      if (in.seen) (*in.seen)[id] = f.in_trie ? 1 : 0;
+      if (!f.in_trie) continue;
+      ++m.n_trie;
+      bool hashed;
+      tokenize(pool + f.off, f.len, test_mask, toks, is_plus, is_hash, hashed);
+      if (hashed) {
+        m.fvbits[id >> 5] |= 1u << (id & 31);
+        m.needs_verify = true;
       }
-      cur = *v;
-      m.ref[cur] += 1;
+      const size_t nw = toks.size();
+      const bool hash_last = is_hash[nw - 1];
+      const size_t path_len = hash_last ? nw - 1 : nw;  // '#' last: attach to the parent node
+      uint32_t cur = 0;
+      for (size_t w = 0; w < path_len; ++w) {
+        const uint64_t tok = is_plus[w] ? PLUS_TOK : toks[w];
+        bool ins;
+        uint32_t* v = m.emap.get_or_insert(cur, tok, ins);
+        if (ins) {
+          if (m.parent.size() >= MAX_NODES) {
+            set_err(h, "trie exceeds 2^26-1 nodes");
+            rc = -E2BIG;
+            return;
+          }
+          const uint32_t child = m.new_node(cur, tok);
+          *v = child;
+          if (is_plus[w])
+            m.pchild[cur] = child;
+          else
+            m.nlit[cur] += 1;
+        }
+        cur = *v;
+        m.ref[cur] += 1;
+      }
+      m.max_depth = std::max<uint32_t>(m.max_depth, (uint32_t)path_len);
+      lb.add(hash_last ? m.hf[cur] : f.wild ? m.tw[cur] : m.tn[cur], id);
     }
-    m.max_depth = std::max<uint32_t>(m.max_depth, (uint32_t)path_len);
-    lb.add(hash_last ? m.hf[cur] : f.wild ? m.tw[cur] : m.tn[cur], id);
-  }
+  });
+  if (rc) return rc;
   // child signatures
   for (size_t y = 1; y < m.parent.size(); ++y)
     if (m.tok[y] != PLUS_TOK) m.sig[m.parent[y]] |= (uint8_t)sig_bit(m.tok[y]);
@@ -1121,8 +1227,8 @@ int commit_full(emqxgm* h) {
   // that still has a free slot (r03 A/B: TOMBing passed buckets lengthened cfg2's miss chains).
   m.fchild.assign(n_nodes, 0u);
   m.half.assign(n_nodes, 0u);
-  select_keyed(m, h->keyed_mode);
-  if (h->fat_mode) {
+  select_keyed(m, in.keyed_mode);
+  if (in.fat_mode) {
     std::vector<uint8_t> depth(n_nodes, 0);
     std::vector<uint32_t> lit(n_nodes, 0);
     for (uint32_t c = 1; c < n_nodes; ++c) {
@@ -1173,13 +1279,23 @@ int commit_full(emqxgm* h) {
   for (uint64_t w : m.occ) m.n_occ += (uint64_t)__builtin_popcountll(w);
   // node side array with headroom for delta-commit growth
   m.tn_cap = n_nodes + std::max<uint64_t>(4096, n_nodes / 4);
+  m.n_nodes0 = n_nodes;
+  m.fv_words0 = m.fvbits.size();
   m.fv_cap = m.fvbits.size() + std::max<uint64_t>(1024, m.fvbits.size() / 4);
   m.fvbits.resize(m.fv_cap, 0u);
 
   // ---- exact route keys: buckets of XBUCKET entries, load factor <= 1/2 per region, filled
   // in order; plain keys and wildcard keys in separate regions ----
-  for (const Filter& f : h->filters)
-    if (f.route_refs) m.nroute(f.wild) += 1;
+  std::vector<uint32_t> rids;  // the route keys, in id order (read once: a background build's
+                               // registry may change between two reads)
+  for_slices(h, in.bg, nf, [&](uint64_t i0, uint64_t i1, const Filter* F, const uint8_t*) {
+    for (uint64_t id = i0; id < i1; ++id) {
+      if (!F[id].route_refs) continue;
+      if (in.seen) (*in.seen)[id] |= 2;
+      rids.push_back((uint32_t)id);
+      m.nroute(F[id].wild) += 1;
+    }
+  });
   m.n_route = m.n_route_p + m.n_route_w;
   m.xcap_p = pow2_at_least(std::max<uint64_t>(16, (m.n_route_p * 2 + XBUCKET - 1) / XBUCKET));
   m.xcap_w = pow2_at_least(std::max<uint64_t>(16, (m.n_route_w * 2 + XBUCKET - 1) / XBUCKET));
@@ -1188,29 +1304,46 @@ int commit_full(emqxgm* h) {
   m.xtomb.assign(xcap * XBUCKET / 64 + 1, 0ull);
   m.xovf.assign(xcap / 64 + 1, 0ull);
   m.xpos.assign(nf, NONE);
-  for (uint32_t id = 0; id < h->filters.size(); ++id) {
-    const Filter& f = h->filters[id];
-    if (!f.route_refs) continue;
-    const uint64_t fh = key_hash(h->pool.data() + f.off, f.len, fmask);
-    const bool w = f.wild;
-    uint64_t b = m.xhome(w, fh);
-    for (;;) {
-      uint32_t j = 0;
-      while (j < XBUCKET && bit(m.xocc, b * XBUCKET + j)) ++j;
-      if (j < XBUCKET) {
-        const uint64_t e = b * XBUCKET + j;
-        bset(m.xocc, e);
-        m.xpos[id] = (uint32_t)e;
-        break;
+  for (uint64_t k0 = 0; k0 < rids.size(); k0 += REG_SLICE) {
+    const uint64_t k1 = std::min<uint64_t>(rids.size(), k0 + REG_SLICE);
+    // (bytes of registered filters never change: only the storage may move, under the lock)
+    for_slices(h, in.bg, 1, [&](uint64_t, uint64_t, const Filter* F, const uint8_t* pool) {
+      for (uint64_t k = k0; k < k1; ++k) {
+        const uint32_t id = rids[k];
+        const Filter& f = F[id];
+        const uint64_t fh = key_hash(pool + f.off, f.len, fmask);
+        const bool w = f.wild;
+        uint64_t b = m.xhome(w, fh);
+        for (;;) {
+          uint32_t j = 0;
+          while (j < XBUCKET && bit(m.xocc, b * XBUCKET + j)) ++j;
+          if (j < XBUCKET) {
+            const uint64_t e = b * XBUCKET + j;
+            bset(m.xocc, e);
+            m.xpos[id] = (uint32_t)e;
+            break;
+          }
+          bset(m.xovf, b);  // the key goes on past this full bucket
+          b = m.xnext(w, b);
+        }
       }
-      bset(m.xovf, b);  // the key goes on past this full bucket
-      b = m.xnext(w, b);
-    }
+    });
   }
   m.x_occ_p = m.n_route_p;
   m.x_occ_w = m.n_route_w;
+  return 0;
+}
+
+// Full build of the device index from the pending registry, in the caller's thread (wmu held:
+// no writer runs meanwhile); swaps it in and rebuilds the host model (TrieModel) that later delta
+// commits patch.
+int commit_full(emqxgm* h) {
+  const BuildIn in = build_in(h, false);
+  h->tm = TrieModel();  // frees the old model before the new one is built
+  TrieModel m;
+  int rc = build_model(h, in, m);
+  if (rc) return rc;
   if (hipSetDevice(h->cfg.device) != hipSuccess) return fail(h, hipErrorInvalidDevice, "hipSetDevice");
-  int rc = 0;
   if ((rc = upload_pool(h, nullptr)) || (rc = fan_full(h)) || (rc = upload_model(h, m))) return rc;
   m.valid = true;
   h->tm = std::move(m);
@@ -1224,7 +1357,14 @@ int commit_full(emqxgm* h) {
 // the caller then runs the full build, which also rebuilds the model.  The patches are only
 // staged here; publish_epoch applies them on the GPU after every pass already enqueued and before
 // every later one, so no match sees a half-applied delta.
-int commit_delta(emqxgm* h) {
+//
+// The model's state per filter is its committed flags -- or, for the catch-up of a background
+// build (install_build), `base`: the membership the build read (bit 0 trie, bit 1 route key;
+// ids past its end: none).  The declines for size and for table capacity come before anything
+// changes, so they leave the model valid (a background build then runs while later deltas still
+// patch it); only a delta that would need a multi[] list (level-token collisions) gives the model
+// up half-way.
+int commit_delta(emqxgm* h, const std::vector<uint8_t>* base = nullptr) {
   TrieModel& m = h->tm;
   if (!m.valid || h->delta_mode == 0) return 1;
   const uint64_t nf = h->filters.size();
@@ -1234,16 +1374,51 @@ int commit_delta(emqxgm* h) {
   std::vector<uint32_t> tadd, tdel, radd, rdel;
   for (uint32_t id : ch) {
     const Filter& f = h->filters[id];
-    if (f.in_trie != f.trie_committed) (f.in_trie ? tadd : tdel).push_back(id);
+    const uint8_t b = base ? (id < base->size() ? (*base)[id] : 0u)
+                           : (uint8_t)((f.trie_committed ? 1u : 0u) | (f.route_committed ? 2u : 0u));
+    if ((bool)f.in_trie != (bool)(b & 1)) (f.in_trie ? tadd : tdel).push_back(id);
     const bool r = f.route_refs > 0;
-    if (r != (bool)f.route_committed) (r ? radd : rdel).push_back(id);
+    if (r != (bool)(b & 2)) (r ? radd : rdel).push_back(id);
   }
   const uint64_t nchg = tadd.size() + tdel.size() + radd.size() + rdel.size();
-  if (h->delta_mode == 1 && nchg > std::max<uint64_t>(4096, (m.n_trie + m.n_route) / 8)) return 1;
+  if (h->delta_mode == 1 &&
+      nchg > (h->delta_max ? h->delta_max : std::max<uint64_t>(4096, (m.n_trie + m.n_route) / 8)))
+    return 1;
   if ((nf + 31) / 32 + 1 > m.fv_cap) return 1;
-  m.valid = false;  // from here a declined delta leaves the model to the full build
 
   const uint64_t test_mask = h->test_mask;
+  std::vector<uint64_t> toks;
+  std::vector<uint8_t> is_plus, is_hash;
+  {
+    // the nodes and slots the delta can take at most: each added filter's path levels that are
+    // not in the trie yet, plus every node a delete may free and an add re-create
+    uint64_t new_nodes = 0, xa[2] = {0, 0};
+    for (uint32_t id : tadd) {
+      const Filter& f = h->filters[id];
+      bool hashed;
+      tokenize(h->pool.data() + f.off, f.len, test_mask, toks, is_plus, is_hash, hashed);
+      const size_t path_len = is_hash.back() ? toks.size() - 1 : toks.size();
+      uint32_t cur = 0;
+      size_t w = 0;
+      for (; w < path_len; ++w) {
+        const uint32_t* v = m.emap.find(cur, is_plus[w] ? PLUS_TOK : toks[w]);
+        if (!v) break;
+        cur = *v;
+      }
+      new_nodes += path_len - w;
+    }
+    if (!tadd.empty())
+      for (uint32_t id : tdel) new_nodes += 1 + (uint64_t)std::count(
+          h->pool.data() + h->filters[id].off, h->pool.data() + h->filters[id].off + h->filters[id].len, '/');
+    if (m.parent.size() + new_nodes > std::min<uint64_t>(MAX_NODES, m.tn_cap) ||
+        (m.n_occ + 2 * new_nodes) * 2 > m.ecap)
+      return 1;
+    for (uint32_t id : radd) xa[h->filters[id].wild ? 1 : 0] += 1;
+    for (int w = 0; w < 2; ++w)
+      if (xa[w] && (m.xoccr(w != 0) + xa[w]) * 4 > m.xcapr(w != 0) * XBUCKET * 3) return 1;
+  }
+  m.valid = false;  // from here a declined delta leaves the model to the full build
+
   const uint64_t fmask =
       h->cfg.full_hash_bits >= 64 ? ~0ull : ((1ull << h->cfg.full_hash_bits) - 1ull);
   std::unordered_map<uint64_t, uint32_t> epatch;  // edge slot -> node (NONE: TOMB)
@@ -1254,8 +1429,6 @@ int commit_delta(emqxgm* h) {
   std::vector<uint32_t> dirty;                    // nodes whose slot / side entry changed
   std::vector<uint32_t> fv_words;  // changed words of the verify bitmap
   std::vector<uint32_t> ovf_words; // changed words of the exact table's overflow bitmap
-  std::vector<uint64_t> toks;
-  std::vector<uint8_t> is_plus, is_hash;
   std::vector<uint32_t> path;
 
   // ---- trie deletes: drop the key from its end node, free nodes no filter passes any more ----
@@ -1541,40 +1714,230 @@ void sweep_graveyard(emqxgm* h) {
   // dead epochs (and the device buffers only they owned) are freed here, outside emu
 }
 
-// Make the pending registry the committed index: a delta commit when it fits, else a full build.
-// Runs under wmu only: readers keep matching against the current epoch while a full build runs.
-int commit_locked(emqxgm* h) {
-  const auto t0 = std::chrono::steady_clock::now();
-  RoctxRange rr(h->roctx, "emqxgm.commit");
+double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// The registry's committed flags (trie_member, route_member, the next delta's base) follow the
+// published epoch: for the listed filters, or for all.
+void flip_committed(emqxgm* h, const std::vector<uint32_t>* ids) {
+  std::unique_lock<std::shared_mutex> g(h->pmu);
+  auto flip = [](Filter& f) {
+    f.trie_committed = f.in_trie;
+    f.route_committed = f.route_refs > 0;
+  };
+  if (ids) {
+    for (uint32_t id : *ids) flip(h->filters[id]);
+  } else {
+    for (Filter& f : h->filters) flip(f);
+  }
+}
+
+// A delta commit of the pending changes published, or 1 when it does not fit (nothing changed
+// then, unless the model gave way: tm.valid false).  During a background build its changes are
+// logged for the build's install.
+int try_delta(emqxgm* h, std::chrono::steady_clock::time_point t0) {
   sweep_graveyard(h);
   h->patches.clear();
   int rc = patch_wait(h);  // the previous commit's patches are applied before buffers change
   if (rc) return rc;
   rc = commit_delta(h);
-  const bool delta = rc == 0;
-  if (rc > 0) {
+  if (rc) {
     h->patches.clear();  // a declined delta stages nothing
-    rc = commit_full(h);
+    return rc;
   }
-  if (rc || (rc = publish_epoch(h, delta))) return rc;
-  {
-    // the registry's committed flags (trie_member, the next delta) follow the published epoch
-    std::unique_lock<std::shared_mutex> g(h->pmu);
-    auto flip = [](Filter& f) {
-      f.trie_committed = f.in_trie;
-      f.route_committed = f.route_refs > 0;
-    };
-    if (delta) {
-      for (uint32_t id : h->changed) flip(h->filters[id]);
-    } else {
-      for (Filter& f : h->filters) flip(f);
+  if ((rc = publish_epoch(h, true))) return rc;
+  flip_committed(h, &h->changed);
+  if (h->job) h->build_log.insert(h->build_log.end(), h->changed.begin(), h->changed.end());
+  h->changed.clear();
+  h->dirty = false;
+  commit_stats(h, ms_since(t0), true);
+  return 0;
+}
+
+// A blocking full build of the whole registry, published.
+int full_now(emqxgm* h, std::chrono::steady_clock::time_point t0) {
+  sweep_graveyard(h);
+  h->patches.clear();
+  int rc = patch_wait(h);
+  if (rc || (rc = commit_full(h)) || (rc = publish_epoch(h, false))) return rc;
+  flip_committed(h, nullptr);
+  h->changed.clear();
+  h->build_log.clear();
+  h->dirty = false;
+  const double ms = ms_since(t0);
+  commit_stats(h, ms, false);
+  std::lock_guard<std::mutex> g(h->stmu);
+  h->st.last_build_ms = ms;
+  return 0;
+}
+
+bool bg_allowed(const emqxgm* h) {
+  return h->bg_min != 0 && h->filters.size() >= h->bg_min && h->delta_mode != 0;
+}
+
+// A table of the current index well on its way to a delta bound (edge slots past 3/8 of 1/2,
+// an exact region past 5/8 of 3/4, half the node or verify-word headroom used): rebuilt in the
+// background while deltas still fit, so that a subscribe does not meet a full table.
+bool nearly_full(const emqxgm* h) {
+  const TrieModel& m = h->tm;
+  if (!m.valid) return false;
+  if (m.n_occ * 8 > m.ecap * 3) return true;
+  for (bool w : {false, true})
+    if (m.xcapr(w) > 16 && (w ? m.x_occ_w : m.x_occ_p) * 8 > m.xcapr(w) * XBUCKET * 5) return true;
+  if (m.parent.size() * 2 > m.tn_cap + m.n_nodes0) return true;
+  const uint64_t fvw = (h->filters.size() + 31) / 32 + 1;
+  return m.fv_words0 && fvw * 2 > m.fv_cap + m.fv_words0;
+}
+
+int install_build(emqxgm* h);
+
+// The background build's thread: build the model and upload its tables without the writer lock
+// (for_slices lets writers in between slices), then install it under the lock.
+void build_thread(emqxgm* h, BuildJob* J) {
+  int rc = 0;
+  if (hipSetDevice(h->cfg.device) != hipSuccess) rc = -EIO;
+  if (!rc) rc = build_model(h, J->in, J->m);
+  if (!rc) rc = upload_tables(h, J->in, J->m, J->nx, J->o);
+  J->rc = rc;
+  J->build_ms = ms_since(J->t0);
+  if (const uint32_t d = h->bg_delay_ms.load()) std::this_thread::sleep_for(std::chrono::milliseconds(d));
+  std::lock_guard<std::mutex> g(h->wmu);
+  h->build_rc = install_build(h);
+  h->builds_done += 1;
+  h->bcv.notify_all();
+}
+
+// Starts a background full build of the registry as it is now (wmu held): the changes pending now
+// are the build's to publish (`covered`); the index readers have stays until the install.
+int start_build(emqxgm* h) {
+  if (h->builder.joinable()) h->builder.join();  // the previous one is installed and gone
+  std::unique_ptr<BuildJob> J(new (std::nothrow) BuildJob());
+  if (!J) return -ENOMEM;
+  J->in = build_in(h, true);
+  J->seen.assign(J->in.nf, 0);
+  J->in.seen = &J->seen;
+  J->covered.swap(h->changed);
+  J->t0 = std::chrono::steady_clock::now();
+  h->build_log.clear();
+  h->dirty = false;
+  BuildJob* jp = J.get();
+  h->job = std::move(J);
+  h->builds_started += 1;
+  try {
+    h->builder = std::thread([h, jp] { build_thread(h, jp); });
+  } catch (...) {
+    h->changed.swap(jp->covered);
+    h->job.reset();
+    h->builds_started -= 1;
+    h->dirty = true;
+    return -ENOMEM;
+  }
+  std::lock_guard<std::mutex> g(h->stmu);
+  h->st.bg_builds += 1;
+  return 0;
+}
+
+// Waits (releasing the writer lock) until the build in flight is installed.
+int wait_build(emqxgm* h, std::unique_lock<std::mutex>& lk) {
+  const uint64_t target = h->builds_started;
+  h->bcv.wait(lk, [&] { return h->builds_done >= target; });
+  return h->build_rc;
+}
+
+// Swaps the finished background build in (wmu held, by its thread): its tables replace the
+// writer's index, the changes made since it read the registry (the log of the deltas committed
+// meanwhile and whatever is pending) are replayed onto its model as one delta against the
+// membership it read, and the result is published.  A failed build, or a catch-up too large for
+// a delta, ends in a blocking full build.
+int install_build(emqxgm* h) {
+  std::unique_ptr<BuildJob> J = std::move(h->job);
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<uint32_t> ch = std::move(h->build_log);
+  h->build_log.clear();
+  ch.insert(ch.end(), h->changed.begin(), h->changed.end());
+  int rc = J->rc;
+  if (rc == 0) {
+    sweep_graveyard(h);
+    h->patches.clear();
+    rc = patch_wait(h);
+  }
+  if (rc == 0) {
+    J->m.valid = true;
+    h->tm = std::move(J->m);
+    h->o_tab = std::move(J->o);
+    set_tables(h->ix, J->nx);
+    h->changed = ch;
+    rc = commit_delta(h, &J->seen);
+    if (rc > 0) {
+      h->patches.clear();
+      rc = commit_full(h);  // (the catch-up did not fit: every filter, now)
+      ch.clear();
+      J->covered.clear();
+      if (rc == 0) J->covered.push_back(NONE);  // flip every flag below
     }
+    if (rc == 0) rc = publish_epoch(h, false);
+  } else {
+    h->changed = ch;
+    set_err(h, "background build failed: a blocking full build follows");
+    rc = full_now(h, t0);
+    J->covered.clear();
+    ch.clear();
+    if (rc == 0) return 0;
+  }
+  if (rc) {
+    h->tm.valid = false;  // the next commit rebuilds
+    h->dirty = true;
+    return rc;
+  }
+  if (!J->covered.empty() && J->covered[0] == NONE) {
+    flip_committed(h, nullptr);
+  } else {
+    ch.insert(ch.end(), J->covered.begin(), J->covered.end());
+    flip_committed(h, &ch);
   }
   h->changed.clear();
   h->dirty = false;
-  commit_stats(h, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
-               delta);
+  commit_stats(h, ms_since(t0), false);
+  std::lock_guard<std::mutex> g(h->stmu);
+  h->st.last_build_ms = J->build_ms;
+  h->st.catchup_changes = ch.size();
   return 0;
+}
+
+// Make the pending registry the committed index (wmu held; lk: the caller's lock on it, which
+// waiting for a background build releases -- nullptr: never build in the background).
+//   * No build in flight: a delta commit when it fits; else a full build -- in the background
+//     when the registry is large enough (bg_allowed), the caller waiting for its install.
+//   * A build in flight: the pending changes go into the index readers have now as a delta
+//     commit (and are replayed onto the build at its install).  wait_all (emqxgm_commit) then
+//     waits for the install too, since changes made before the build started -- possibly this
+//     caller's -- become visible only with it; the synchronous subscribe path
+//     (EMQXGM_SET_COMMIT, whose changes are made under the same lock hold) returns at once.
+//     A delta the current tables cannot take waits for the install, which includes it.
+int commit_locked(emqxgm* h, std::unique_lock<std::mutex>* lk, bool wait_all) {
+  const auto t0 = std::chrono::steady_clock::now();
+  RoctxRange rr(h->roctx, "emqxgm.commit");
+  if (h->job) {
+    if (!lk) return -EBUSY;
+    int rc = h->dirty ? try_delta(h, t0) : 0;
+    if (rc < 0) return rc;
+    if (rc == 0 && !wait_all) return 0;
+    if (rc > 0) {
+      std::lock_guard<std::mutex> g(h->stmu);
+      h->st.bg_waits += 1;
+    }
+    return wait_build(h, *lk);
+  }
+  if (!h->dirty) return 0;
+  int rc = try_delta(h, t0);
+  if (rc == 0) {
+    if (lk && bg_allowed(h) && nearly_full(h)) (void)start_build(h);  // not waited for
+    return 0;
+  }
+  if (rc < 0) return rc;
+  if (lk && bg_allowed(h) && start_build(h) == 0) return wait_build(h, *lk);
+  return full_now(h, t0);
 }
 
 int dev_alloc(emqxgm* h, PassCtx& c, void** p, size_t bytes) {
@@ -2324,7 +2687,8 @@ int emqxgm_create(const emqxgm_cfg* cfg, emqxgm_t** out) {
   h->geom = walk_geometry(h->cfg.device, h->cfg.walk_wg_per_cu);
   h->geom.xrange_bytes = h->xrange_bytes;
   set_pipe_geometry(h);
-  int rc = commit_locked(h);  // empty index: epoch 1
+  h->dirty = true;
+  int rc = commit_locked(h, nullptr, true);  // empty index: epoch 1
   if (rc) {
     emqxgm_destroy(h);
     return rc;
@@ -2335,6 +2699,11 @@ int emqxgm_create(const emqxgm_cfg* cfg, emqxgm_t** out) {
 
 void emqxgm_destroy(emqxgm_t* h) {
   if (!h) return;
+  {
+    std::unique_lock<std::mutex> lk(h->wmu);
+    if (h->job) (void)wait_build(h, lk);
+  }
+  if (h->builder.joinable()) h->builder.join();
   (void)hipSetDevice(h->cfg.device);
   for (auto& p : h->pipes) ctx_free(p.c);
   for (auto& p : h->hpipes) host_pipe_free(p);
@@ -2635,9 +3004,117 @@ int emqxgm_route_ref_many(emqxgm_t* h, const uint8_t* bytes, const uint64_t* off
 
 int emqxgm_commit(emqxgm_t* h, uint64_t* epoch) {
   if (!h) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->wmu);
+  std::unique_lock<std::mutex> lk(h->wmu);
+  const int rc = commit_locked(h, &lk, true);
+  if (epoch) *epoch = h->epoch;
+  return rc;
+}
+
+int emqxgm_route_set_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets,
+                           const uint8_t* present, uint64_t n, uint32_t flags, uint64_t* epoch) {
+  if (!h || !offsets || (!bytes && n) || (flags & ~EMQXGM_SET_COMMIT)) return -EINVAL;
+  for (uint64_t i = 0; i < n; ++i)
+    if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > 65535) return -EINVAL;
+  std::unique_lock<std::mutex> lk(h->wmu);
+  {
+    std::unique_lock<std::shared_mutex> g(h->pmu);
+    for (uint64_t i = 0; i < n; ++i) {
+      const bool pr = !present || present[i];
+      const uint8_t* p = bytes + offsets[i];
+      const uint32_t len = (uint32_t)(offsets[i + 1] - offsets[i]);
+      if (pr && h->filters.size() >= 0x7FFFFFFFu) return -E2BIG;
+      const uint32_t id = find_id(h, p, len, pr);
+      if (id != NONE) route_set_locked(h, id, pr);
+    }
+  }
   int rc = 0;
-  if (h->dirty) rc = commit_locked(h);
+  if (flags & EMQXGM_SET_COMMIT) rc = commit_locked(h, &lk, false);
+  if (epoch) *epoch = h->epoch;
+  return rc;
+}
+
+int emqxgm_route_dests_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                             const uint32_t* dptr, const uint32_t* node, const uint32_t* group,
+                             uint32_t flags, uint64_t* epoch) {
+  if (!h || !offsets || !dptr || (!bytes && n) || (flags & ~EMQXGM_SET_COMMIT)) return -EINVAL;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > 65535 || dptr[i + 1] < dptr[i])
+      return -EINVAL;
+    for (uint32_t j = dptr[i]; j < dptr[i + 1]; ++j)
+      if (!node || !group || node[j] == NONE || (group[j] != NONE && (group[j] & EMQXGM_DEST_GROUP)))
+        return -EINVAL;
+  }
+  std::unique_lock<std::mutex> lk(h->wmu);
+  {
+    std::unique_lock<std::shared_mutex> g(h->pmu);
+    std::vector<std::pair<uint32_t, uint32_t>> ds;
+    for (uint64_t i = 0; i < n; ++i) {
+      ds.clear();
+      for (uint32_t j = dptr[i]; j < dptr[i + 1]; ++j) ds.emplace_back(node[j], group[j]);
+      std::sort(ds.begin(), ds.end());
+      ds.erase(std::unique(ds.begin(), ds.end()), ds.end());
+      const uint8_t* p = bytes + offsets[i];
+      const uint32_t len = (uint32_t)(offsets[i + 1] - offsets[i]);
+      if (!ds.empty() && h->filters.size() >= 0x7FFFFFFFu) return -E2BIG;
+      const uint32_t id = find_id(h, p, len, !ds.empty());
+      if (id == NONE) continue;  // absent and unknown: nothing to remove
+      auto it = h->rdest.find(id);
+      std::vector<std::pair<uint32_t, uint32_t>> old;
+      if (it != h->rdest.end()) old = it->second;
+      std::sort(old.begin(), old.end());
+      if (old != ds) {
+        if (ds.empty())
+          h->rdest.erase(id);
+        else
+          h->rdest[id] = ds;
+        h->fan_changed.push_back(id);
+        h->dirty = true;
+      }
+      route_set_locked(h, id, !ds.empty());
+    }
+  }
+  int rc = 0;
+  if (flags & EMQXGM_SET_COMMIT) rc = commit_locked(h, &lk, false);
+  if (epoch) *epoch = h->epoch;
+  return rc;
+}
+
+int emqxgm_subscribers_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                             const uint32_t* sptr, const uint32_t* subs, uint32_t flags,
+                             uint64_t* epoch) {
+  if (!h || !offsets || !sptr || (!bytes && n) || (flags & ~EMQXGM_SET_COMMIT)) return -EINVAL;
+  for (uint64_t i = 0; i < n; ++i)
+    if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > 65535 || sptr[i + 1] < sptr[i] ||
+        (sptr[i + 1] > sptr[i] && !subs))
+      return -EINVAL;
+  std::unique_lock<std::mutex> lk(h->wmu);
+  {
+    std::unique_lock<std::shared_mutex> g(h->pmu);
+    std::vector<uint32_t> ss;
+    for (uint64_t i = 0; i < n; ++i) {
+      ss.assign(subs + sptr[i], subs + sptr[i + 1]);
+      std::sort(ss.begin(), ss.end());
+      ss.erase(std::unique(ss.begin(), ss.end()), ss.end());
+      const uint8_t* p = bytes + offsets[i];
+      const uint32_t len = (uint32_t)(offsets[i + 1] - offsets[i]);
+      if (!ss.empty() && h->filters.size() >= 0x7FFFFFFFu) return -E2BIG;
+      const uint32_t id = find_id(h, p, len, !ss.empty());
+      if (id == NONE) continue;
+      auto it = h->lsubs.find(id);
+      std::vector<uint32_t> old;
+      if (it != h->lsubs.end()) old = it->second;
+      std::sort(old.begin(), old.end());
+      if (old == ss) continue;
+      if (ss.empty())
+        h->lsubs.erase(id);
+      else
+        h->lsubs[id] = ss;
+      h->fan_changed.push_back(id);
+      h->dirty = true;
+    }
+  }
+  int rc = 0;
+  if (flags & EMQXGM_SET_COMMIT) rc = commit_locked(h, &lk, false);
   if (epoch) *epoch = h->epoch;
   return rc;
 }
@@ -2839,9 +3316,11 @@ extern "C" {
 
 int emqxgm_snapshot_save(emqxgm_t* h, const char* path) {
   if (!h || !path) return -EINVAL;
-  std::lock_guard<std::mutex> g(h->wmu);
+  std::unique_lock<std::mutex> lk(h->wmu);
   int rc = 0;
-  if (h->dirty && (rc = commit_locked(h))) return rc;  // the file holds committed state only
+  // the file holds committed state only (and the model of the index readers have)
+  if ((h->dirty || h->job) && (rc = commit_locked(h, &lk, true))) return rc;
+  if (h->job && (rc = wait_build(h, lk))) return rc;
   if (!h->tm.valid) {
     set_err(h, "no host model to save");
     return -EINVAL;
@@ -2947,6 +3426,8 @@ int emqxgm_snapshot_load(emqxgm_t* h, const char* path) {
     return rc;
   }
   m.valid = true;
+  m.n_nodes0 = m.parent.size();  // (headroom counted from the restored index on)
+  m.fv_words0 = std::min<uint64_t>(m.fv_cap, (h->filters.size() + 31) / 32 + 1);
   h->tm = std::move(m);
   h->changed.clear();
   h->fan_changed.clear();
@@ -3788,6 +4269,30 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
     h->delta_mode = (uint32_t)value;
     return 0;
   }
+  if (strcmp(key, "delta_max") == 0) {  // changes a delta commit takes (0: max(4096, keys / 8))
+    if (value < 0) return -EINVAL;
+    std::lock_guard<std::mutex> g(h->wmu);
+    h->delta_max = (uint64_t)value;
+    return 0;
+  }
+  if (strcmp(key, "bg_build") == 0) {  // full builds of >= v filters in the background (0: never)
+    if (value < 0) return -EINVAL;
+    std::lock_guard<std::mutex> g(h->wmu);
+    h->bg_min = (uint64_t)value;
+    return 0;
+  }
+  if (strcmp(key, "bg_delay_ms") == 0) {  // tests: a background build holds its install back
+    if (value < 0 || value > 600000) return -EINVAL;
+    h->bg_delay_ms.store((uint32_t)value);
+    return 0;
+  }
+  if (strcmp(key, "rebuild") == 0) {  // 1: a full build in the background now (not waited for)
+    if (value != 1) return -EINVAL;
+    std::lock_guard<std::mutex> g(h->wmu);
+    if (h->job) return -EBUSY;
+    if (!bg_allowed(h) || !h->tm.valid) return -EINVAL;
+    return start_build(h);
+  }
   if (strcmp(key, "roctx") == 0) {  // 1: roctx ranges / launch markers (gm_roctx.h)
     if (value < 0 || value > 1) return -EINVAL;
     h->roctx = value != 0;
@@ -3795,7 +4300,8 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
   }
   if (strcmp(key, "keyed") == 0) {  // token-keyed parents (select_keyed), next full build on
     if (value < 0 || value > 2) return -EINVAL;
-    std::lock_guard<std::mutex> g(h->wmu);
+    std::unique_lock<std::mutex> g(h->wmu);
+    if (h->job) (void)wait_build(h, g);  // (it builds with the old setting)
     if (h->keyed_mode != (uint32_t)value && !h->filters.empty()) {
       h->tm.valid = false;  // the next commit is a full build
       h->dirty = true;
@@ -3805,7 +4311,8 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
   }
   if (strcmp(key, "fat_buckets") == 0) {  // 1 (default) / 0: from the next full build on
     if (value < 0 || value > 1) return -EINVAL;
-    std::lock_guard<std::mutex> g(h->wmu);
+    std::unique_lock<std::mutex> g(h->wmu);
+    if (h->job) (void)wait_build(h, g);
     h->fat_mode = (uint32_t)value;
     h->tm.valid = false;  // the next commit is a full build
     h->dirty = true;

@@ -17,7 +17,8 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libemqx_gpumatch.so")
 NONE = 0xFFFFFFFF
-ABI_VERSION = 3  # include/emqx_gpumatch.h EMQXGM_ABI_VERSION
+ABI_VERSION = 4  # include/emqx_gpumatch.h EMQXGM_ABI_VERSION
+SET_COMMIT = 1  # EMQXGM_SET_COMMIT
 TAG_CANCELLED = 0xFFFFFFFFFFFFFFFF  # EMQXGM_TAG_CANCELLED
 
 
@@ -72,7 +73,11 @@ class _WindowOut(C.Structure):
 class _AsyncCfg(C.Structure):
     _fields_ = [("window_topics", C.c_uint32), ("window_bytes", C.c_uint32),
                 ("window_us", C.c_uint32), ("max_levels", C.c_uint32),
-                ("queued_windows", C.c_uint32), ("reserved", C.c_uint32 * 3)]
+                ("queued_windows", C.c_uint32), ("flags", C.c_uint32),
+                ("reserved", C.c_uint32 * 2)]
+
+
+ASYNC_PUBLISH = 1  # EMQXGM_ASYNC_PUBLISH
 
 
 class _AsyncWindow(C.Structure):
@@ -81,7 +86,12 @@ class _AsyncWindow(C.Structure):
                 ("owner", C.POINTER(C.c_uint64)), ("row", C.POINTER(C.c_uint32)),
                 ("filter_id", C.POINTER(C.c_uint32)), ("foff", C.POINTER(C.c_uint32)),
                 ("fbytes", C.POINTER(C.c_uint8)), ("exact_id", C.POINTER(C.c_uint32)),
-                ("first_ns", C.c_uint64), ("flush_ns", C.c_uint64), ("done_ns", C.c_uint64)]
+                ("first_ns", C.c_uint64), ("flush_ns", C.c_uint64), ("done_ns", C.c_uint64),
+                ("n_routes", C.c_uint64), ("n_deliveries", C.c_uint64),
+                ("route_ptr", C.POINTER(C.c_uint64)), ("route_filter", C.POINTER(C.c_uint32)),
+                ("route_dest", C.POINTER(C.c_uint32)), ("deliver_ptr", C.POINTER(C.c_uint64)),
+                ("deliver_filter", C.POINTER(C.c_uint32)), ("deliver_sub", C.POINTER(C.c_uint32)),
+                ("rfoff", C.POINTER(C.c_uint64)), ("rfbytes", C.POINTER(C.c_uint8))]
 
 
 ASYNC_CB = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(_AsyncWindow))
@@ -104,7 +114,9 @@ class _Stats(C.Structure):
                 ("delta_commits", C.c_uint64), ("last_commit_ms", C.c_double),
                 ("tok_ms", C.c_double), ("tok_launches", C.c_uint64),
                 ("exact_ms", C.c_double), ("keyed_nodes", C.c_uint64),
-                ("buffer_grows", C.c_uint64), ("sync_gathers", C.c_uint64)]
+                ("buffer_grows", C.c_uint64), ("sync_gathers", C.c_uint64),
+                ("bg_builds", C.c_uint64), ("bg_waits", C.c_uint64),
+                ("last_build_ms", C.c_double), ("catchup_changes", C.c_uint64)]
 
 
 # name -> (restype, argtypes): exactly the entry points declared in include/emqx_gpumatch.h
@@ -125,6 +137,9 @@ SYMBOLS = {
     "emqxgm_route_ref_many": (C.c_int, [_P, _P, _P, C.c_uint64, _P]),
     "emqxgm_route_set": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_int]),
     "emqxgm_route_set_many": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_int]),
+    "emqxgm_route_set_batch": (C.c_int, [_P, _P, _P, _P, C.c_uint64, C.c_uint32, _U64P]),
+    "emqxgm_route_dests_batch": (C.c_int, [_P, _P, _P, C.c_uint64, _P, _P, _P, C.c_uint32, _U64P]),
+    "emqxgm_subscribers_batch": (C.c_int, [_P, _P, _P, C.c_uint64, _P, _P, C.c_uint32, _U64P]),
     "emqxgm_route_sync_begin": (C.c_int, [_P, _U32P]),
     "emqxgm_route_sync_end": (C.c_int, [_P, C.c_uint32, _U64P]),
     "emqxgm_route_member": (C.c_int, [_P, C.c_char_p, C.c_uint32]),
@@ -349,6 +364,47 @@ class Engine:
         buf = np.ascontiguousarray(buf, dtype=np.uint8)
         self._check(self._lib.emqxgm_route_set_many(self._h, _ptr(buf), _ptr(off), len(off) - 1,
                                                      1 if present else 0), "route_set_many")
+
+    def route_set_batch(self, items: Sequence[Tuple[bytes, bool]], commit: bool = True) -> int:
+        """emqxgm_route_set_batch: the membership of several filters, and (commit) visible to
+        every match started after the return -- never waiting for a background full build
+        unless the current tables cannot take the delta.  Returns the epoch."""
+        buf, off = pack([f for f, _ in items], np.uint64)
+        pr = np.fromiter((1 if p else 0 for _, p in items), dtype=np.uint8, count=len(items))
+        e = C.c_uint64()
+        self._check(self._lib.emqxgm_route_set_batch(self._h, _ptr(buf), _ptr(off), _ptr(pr),
+                                                      len(items), SET_COMMIT if commit else 0,
+                                                      C.byref(e)), "route_set_batch")
+        return e.value
+
+    def route_dests_batch(self, items: Sequence[Tuple[bytes, Sequence[Tuple[int, int]]]],
+                          commit: bool = True) -> int:
+        """emqxgm_route_dests_batch: each filter gets exactly these (node, group) dest handles
+        (group NONE: a node dest) -- its rows of the route bag -- and its route key / trie
+        membership while it has any; (commit) visible on return.  Returns the epoch."""
+        buf, off = pack([f for f, _ in items], np.uint64)
+        dptr = np.zeros(len(items) + 1, np.uint32)
+        np.cumsum([len(d) for _, d in items], out=dptr[1:])
+        node = np.array([n for _, d in items for n, _ in d], np.uint32)
+        group = np.array([g for _, d in items for _, g in d], np.uint32)
+        e = C.c_uint64()
+        self._check(self._lib.emqxgm_route_dests_batch(
+            self._h, _ptr(buf), _ptr(off), len(items), _ptr(dptr), _ptr(node), _ptr(group),
+            SET_COMMIT if commit else 0, C.byref(e)), "route_dests_batch")
+        return e.value
+
+    def subscribers_batch(self, items: Sequence[Tuple[bytes, Sequence[int]]],
+                          commit: bool = True) -> int:
+        """emqxgm_subscribers_batch: each filter gets exactly these local subscriber handles."""
+        buf, off = pack([f for f, _ in items], np.uint64)
+        sptr = np.zeros(len(items) + 1, np.uint32)
+        np.cumsum([len(x) for _, x in items], out=sptr[1:])
+        subs = np.array([v for _, x in items for v in x], np.uint32)
+        e = C.c_uint64()
+        self._check(self._lib.emqxgm_subscribers_batch(
+            self._h, _ptr(buf), _ptr(off), len(items), _ptr(sptr), _ptr(subs),
+            SET_COMMIT if commit else 0, C.byref(e)), "subscribers_batch")
+        return e.value
 
     def sync_begin(self) -> int:
         g = C.c_uint32()
@@ -752,7 +808,8 @@ class Batcher:
 @dataclass
 class AsyncResult:
     """One reported call of the concurrent entry: its trie filters' bytes (None: the window
-    failed, status < 0) and its exact route key id."""
+    failed, status < 0) and its exact route key id; a publish layer's call its aggre/1 entries
+    [(To bytes, dest handle)] and local dispatches [(To bytes, subscriber handle)]."""
     tag: int
     owner: int
     status: int
@@ -760,6 +817,8 @@ class AsyncResult:
     exact_id: int
     device_index: int
     latency_ns: int  # first call of its window -> its window's result complete
+    routes: Optional[List[Tuple[bytes, int]]] = None
+    deliveries: Optional[List[Tuple[bytes, int]]] = None
 
 
 class AsyncMatcher:
@@ -770,7 +829,7 @@ class AsyncMatcher:
 
     def __init__(self, engines: Sequence[Engine], callback=None, window_topics: int = 0,
                  window_bytes: int = 0, window_us: int = 0, max_levels: int = 0,
-                 queued_windows: int = 0):
+                 queued_windows: int = 0, publish: bool = False):
         import threading
         self._engines = list(engines)  # kept alive: the layer uses their handles
         self._lib = self._engines[0]._lib
@@ -785,15 +844,27 @@ class AsyncMatcher:
                 tag = w.tag[i]
                 if tag == TAG_CANCELLED:
                     continue
+                rt = dl = None
                 if w.status:
                     fl, ex = None, NONE
+                elif publish:
+                    fl, ex = None, NONE
+
+                    def to(j):
+                        a, b = w.rfoff[j], w.rfoff[j + 1]
+                        return C.string_at(C.addressof(w.rfbytes.contents) + a, b - a) if b > a else b""
+                    a, b = w.route_ptr[i], w.route_ptr[i + 1]
+                    rt = [(to(j), w.route_dest[j]) for j in range(a, b)]
+                    names = {w.route_filter[j]: to(j) for j in range(a, b)}
+                    dl = [(names[w.deliver_filter[j]], w.deliver_sub[j])
+                          for j in range(w.deliver_ptr[i], w.deliver_ptr[i + 1])]
                 else:
                     fl = [C.string_at(C.addressof(w.fbytes.contents) + w.foff[j],
                                       w.foff[j + 1] - w.foff[j]) if w.foff[j + 1] > w.foff[j] else b""
                           for j in range(w.row[i], w.row[i + 1])]
                     ex = w.exact_id[i]
                 out.append(AsyncResult(tag, w.owner[i], w.status, fl, ex, w.device_index,
-                                       w.done_ns - w.first_ns))
+                                       w.done_ns - w.first_ns, rt, dl))
             if self._user_cb is not None:
                 self._user_cb(out)
             else:
@@ -802,7 +873,8 @@ class AsyncMatcher:
                         self.results[(r.tag, r.owner)] = r
                     self._cv.notify_all()
         self._cb = ASYNC_CB(on_window)  # kept alive as long as the layer
-        cfg = _AsyncCfg(window_topics, window_bytes, window_us, max_levels, queued_windows)
+        cfg = _AsyncCfg(window_topics, window_bytes, window_us, max_levels, queued_windows,
+                        ASYNC_PUBLISH if publish else 0)
         arr = (C.c_void_p * len(self._engines))(*[e._h for e in self._engines])
         a = C.c_void_p()
         self._engines[0]._check(self._lib.emqxgm_async_create(arr, len(self._engines), C.byref(cfg),

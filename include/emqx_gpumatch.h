@@ -53,7 +53,10 @@
  * Threading (the reference reads with read_concurrency while writers commit in mria
  * transactions, emqx_trie.erl:70-75, emqx_router_utils.erl:74-135):
  *   - writers (insert/delete/route/subscriber calls, emqxgm_commit) are serialised by one writer
- *     lock;
+ *     lock; a full build of a large registry runs in a background thread without it (r05):
+ *     meanwhile commits are delta patches of the current index, emqxgm_commit returns once the
+ *     build is installed (changes made before it started show with it), and
+ *     emqxgm_route_set_batch(.., EMQXGM_SET_COMMIT) returns as soon as its own changes show;
  *   - every match call reads the last committed epoch and never waits for a writer: a commit
  *     builds the next index beside the current one (a full build: seconds at 10M filters) and
  *     swaps it in atomically; a small delta is patched in place on the device, ordered on the GPU
@@ -76,7 +79,8 @@ extern "C" {
 #define EMQXGM_DEST_GROUP 0x80000000u /* dest handle bit: a shared-subscription group */
 #define EMQXGM_RULE_EQ 1u    /* rule flag: {eq, Filter} -- the name must equal the filter */
 #define EMQXGM_RULE_WORDS 2u /* rule flag: match/2 on word lists (no '$' clauses) */
-#define EMQXGM_ABI_VERSION 3
+#define EMQXGM_ABI_VERSION 4
+#define EMQXGM_SET_COMMIT 1u /* emqxgm_route_set_batch: visible before the call returns */
 
 typedef struct emqxgm emqxgm_t;
 
@@ -137,6 +141,11 @@ typedef struct emqxgm_stats {
   uint64_t buffer_grows;    /* pass scratch / host-pipe buffers reallocated (each a stall) */
   uint64_t sync_gathers;    /* host windows whose filter block outgrew its estimate (finished
                                synchronously in the wait) */
+  uint64_t bg_builds;       /* full builds run in the background, beside the writers (r05) */
+  uint64_t bg_waits;        /* commits that waited for one: the current tables could not take
+                               their delta */
+  double last_build_ms;     /* wall time of the last full build (background: start to ready) */
+  uint64_t catchup_changes; /* filters replayed onto the last background build at its install */
 } emqxgm_stats;
 
 int emqxgm_abi_version(void);
@@ -173,6 +182,18 @@ int emqxgm_snapshot_load(emqxgm_t* h, const char* path);
 int emqxgm_route_set(emqxgm_t* h, const uint8_t* filter, uint32_t len, int present);
 int emqxgm_route_set_many(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
                           int present);
+/* The same for n filters at once, each with its own state (present[i] != 0; present == NULL: all
+ * present), and with flags EMQXGM_SET_COMMIT a commit that makes them visible to every match
+ * started after the call returns: the writing node's subscribe / unsubscribe path (SURVEY 8b's
+ * post-maybe_trans hook: the reference's subscriber has its route before SUBACK,
+ * emqx_broker.erl:163-168, 484-486 -> emqx_router.erl:124-138) and the mirror's batched events.
+ * It never waits for a full build: while one runs in the background, the changes are patched
+ * into the index the readers have now (a delta commit) and replayed onto the new index when it
+ * is installed.  It waits only when the current tables cannot take the delta (a table at its
+ * load bound while the rebuild that grows it runs; emqxgm_stats.bg_waits counts them).  Full
+ * builds of registries of at least emqxgm_tune("bg_build") filters run in the background. */
+int emqxgm_route_set_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets,
+                           const uint8_t* present, uint64_t n, uint32_t flags, uint64_t* epoch);
 /* A full resync (the mirror's start and its periodic anti-entropy pass): _begin starts generation
  * *gen; every emqxgm_route_set(.., 1) until _end marks its filter; _end(gen) sets every route key
  * that was not marked absent (*removed of them).  -ESTALE if another _begin came in between. */
@@ -293,6 +314,20 @@ int emqxgm_set_local_node(emqxgm_t* h, uint32_t node);
 /* The local subscriber bag (filter -> subscriber handle); duplicates / absent deletes: no-op. */
 int emqxgm_subscriber_add(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t sub);
 int emqxgm_subscriber_delete(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t sub);
+/* Level-triggered forms for a mirror of the committed tables (the NIF's sync process and the
+ * writing node's hook, r05): filter i = bytes[offsets[i] .. offsets[i+1]) gets exactly the dests
+ * (node[j], group[j]) for j in [dptr[i], dptr[i+1]) -- its rows of the emqx_route bag,
+ * emqx_router.erl:72-92: group = EMQXGM_NONE for a node dest, else the {Group, Node} dest --
+ * and its route key / wildcard trie membership while it has any (emqxgm_route_set's rule);
+ * or exactly the local subscribers subs[sptr[i] .. sptr[i+1]) (the emqx_subscriber bag,
+ * emqx_broker.erl:150-214, 546-552).  Duplicates are ignored.  flags EMQXGM_SET_COMMIT: visible
+ * before the call returns, as emqxgm_route_set_batch. */
+int emqxgm_route_dests_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                             const uint32_t* dptr, const uint32_t* node, const uint32_t* group,
+                             uint32_t flags, uint64_t* epoch);
+int emqxgm_subscribers_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                             const uint32_t* sptr, const uint32_t* subs, uint32_t flags,
+                             uint64_t* epoch);
 
 typedef struct emqxgm_publish_out { /* host-resident result of emqxgm_publish_batch */
   uint32_t n;
@@ -437,7 +472,12 @@ int emqxgm_batcher_collect(emqxgm_batcher_t* b, uint64_t window, emqxgm_window_o
  * (from that thread; the windows of different handles concurrently).  The window passed to `cb`
  * is valid during the call only.  Every accepted call is reported exactly once, unless cancelled
  * first.  Errors of emqxgm_async_match: -E2BIG (longer than a window, or more than max_levels
- * levels), -EBUSY (every window full or in flight), -EINVAL: the caller answers those itself. */
+ * levels), -EBUSY (every window full or in flight), -EINVAL: the caller answers those itself.
+ * A layer created with EMQXGM_ASYNC_PUBLISH answers each call with emqx_broker:publish/1's
+ * routing instead (emqx_broker.erl:218-300: the aggre/1 entries of match_routes(Topic) and the
+ * local dispatches, dispatch/2 :326-355, from the engine's fan-out tables): the completer runs
+ * emqxgm_publish_batch for the window (the handle's publish results are then reused by it, so a
+ * handle serves one publish layer). */
 #define EMQXGM_TAG_CANCELLED 0xFFFFFFFFFFFFFFFFull /* never a caller's tag */
 typedef struct emqxgm_async emqxgm_async_t;
 typedef struct emqxgm_async_cfg {
@@ -446,8 +486,11 @@ typedef struct emqxgm_async_cfg {
   uint32_t window_us;      /* a window is submitted at most this long after its first topic (0 = 50) */
   uint32_t max_levels;     /* calls for topics with more levels: -E2BIG (0 = no limit) */
   uint32_t queued_windows; /* full windows that may wait for a pipe (0 = 2) */
-  uint32_t reserved[3];
+  uint32_t flags;          /* EMQXGM_ASYNC_PUBLISH: windows are answered with the publish
+                              fan-out (emqxgm_publish_batch) instead of trie rows */
+  uint32_t reserved[2];
 } emqxgm_async_cfg;
+#define EMQXGM_ASYNC_PUBLISH 1u
 typedef struct emqxgm_async_window {
   int status;               /* 0, or the negative errno the window's pass failed with (no result) */
   uint32_t n;               /* calls in the window, in the order they were made */
@@ -461,6 +504,20 @@ typedef struct emqxgm_async_window {
   const uint8_t* fbytes;
   const uint32_t* exact_id; /* [n] route key equal to the topic, or EMQXGM_NONE */
   uint64_t first_ns, flush_ns, done_ns; /* CLOCK_MONOTONIC: first call, submit, result complete */
+  /* EMQXGM_ASYNC_PUBLISH layers (row .. exact_id are then unset): the window's
+   * emqxgm_publish_batch result -- call i's aggre/1 entries are [route_ptr[i], route_ptr[i+1])
+   * (filter id To, dest handle), its local dispatches [deliver_ptr[i], deliver_ptr[i+1])
+   * (filter id To, subscriber handle) -- and the bytes of each entry's To:
+   * rfbytes[rfoff[j] .. rfoff[j+1]) (rfoff has n_routes + 1 entries) */
+  uint64_t n_routes, n_deliveries;
+  const uint64_t* route_ptr;
+  const uint32_t* route_filter;
+  const uint32_t* route_dest;
+  const uint64_t* deliver_ptr;
+  const uint32_t* deliver_filter;
+  const uint32_t* deliver_sub;
+  const uint64_t* rfoff;
+  const uint8_t* rfbytes;
 } emqxgm_async_window;
 typedef void (*emqxgm_async_cb)(void* user, const emqxgm_async_window* w);
 int emqxgm_async_create(emqxgm_t* const* hs, uint32_t n_handles, const emqxgm_async_cfg* cfg,
@@ -532,7 +589,9 @@ int emqxgm_set_profiling(emqxgm_t* h, int on);
  * "exact_range_kb" (0 default: one route-key probe pass over the whole table; > 0: the probe
  * runs in passes over bucket ranges of that many KiB, so that the lines in flight share page
  * translations -- measured slower on a 100M-key table, kept as an option); "delta_commit": 0 = every commit rebuilds the index, 1 = small deltas are patched in place
- * (default), 2 = every delta that fits the tables' load bounds is patched in place;
+ * (default), 2 = every delta that fits the tables' load bounds is patched in place; "delta_max":
+ * the changes a delta commit takes in mode 1 (0 default = max(4096, (trie members + route keys)
+ * / 8));
  * "fat_buckets": 1 (default) = single-literal-child nodes keep their child in their own bucket
  * line, 0 = none (A/B runs), from the next full build on (the next commit);
  * "roctx": 1 = roctx ranges around passes, waits and commits and a marker at each kernel launch
@@ -541,7 +600,12 @@ int emqxgm_set_profiling(emqxgm_t* h, int on);
  * automatic, 0 = none, 2 = every eligible node (tests); "zc_topics": the largest pinned window
  * of _submit_filters that goes without DMA copies (65536 default, 0 = always copies); "spin_us":
  * host pipes' waits poll the pass's completion for up to this long before they block (200
- * default, 0 = block at once). */
+ * default, 0 = block at once); "bg_build": full builds of registries of at least this many
+ * filters run in a background thread while commits keep patching the current index (16384
+ * default, 0 = every full build blocks the writers, as before r05); "bg_delay_ms": a background
+ * build holds its install back this long (tests: a build in flight on demand); "rebuild" (1):
+ * start a background full build of the registry now without waiting for it (-EBUSY: one is in
+ * flight; it also compacts the tables' deleted slots). */
 int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value);
 int emqxgm_get_stats(emqxgm_t* h, emqxgm_stats* st);
 /* Last HIP error string seen by the handle (for diagnostics). */

@@ -131,6 +131,14 @@ int gm_submit_window(emqxgm_t* h, const uint8_t* bytes, const uint32_t* off, uin
 }
 extern "C" {
 
+// publish-mode layers (EMQXGM_ASYNC_PUBLISH) are checked on the GPU (tests/test_gpu_async.py)
+int emqxgm_publish_batch(emqxgm_t*, const uint8_t*, const uint32_t*, uint32_t, emqxgm_publish_out*) {
+  return -EIO;
+}
+int emqxgm_filters_copy(emqxgm_t*, const uint32_t*, uint64_t, uint8_t*, uint64_t, uint64_t*) {
+  return -EIO;
+}
+
 int emqxgm_match_batch_wait_filters(emqxgm_t* h, uint64_t ticket, emqxgm_batch_out* out,
                                     const uint32_t** foff, const uint8_t** fbytes) {
   // the "device" takes a while; the layer must not hold its own lock meanwhile

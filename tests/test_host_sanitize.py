@@ -8,7 +8,14 @@ one, every commit's device tables walked on the CPU as k_walk walks them and com
 oracle (oracle/ref_trie.cpp, restating emqx_trie.erl:113-144, 242-260, 282-348), the exact table
 probed as k_exact probes it, every fan-out entry compared with the registry; halfway through,
 the delta-committing engine is saved to a snapshot and replaced by a fresh engine loaded from it.
-Any sanitizer report or mismatch fails the run."""
+Any sanitizer report or mismatch fails the run.
+
+tests/host_harness/bg_harness.cpp (r05) is the subscribe-then-publish visibility check while full
+builds run in the background: single subscribes / unsubscribes through
+emqxgm_route_set_batch(.., EMQXGM_SET_COMMIT) during a bulk commit's build, during a build the
+tables' load started, and a batch too large for a delta during a build -- each checked on the
+epoch readers have right after the call (the reference's subscriber has its route before SUBACK,
+emqx_broker.erl:163-168, emqx_router.erl:124-138) -- under ThreadSanitizer and ASan + UBSan."""
 import os
 import subprocess
 
@@ -19,21 +26,29 @@ H = os.path.join(ROOT, "tests", "host_harness")
 OUT = os.path.join(H, "build", "harness_asan")
 SRCS = [os.path.join(H, "harness.cpp"), os.path.join(H, "fake_hip.cpp"),
         os.path.join(ROOT, "oracle", "ref_trie.cpp")]
-DEPS = SRCS + [os.path.join(H, "fakehip", "hip", "hip_runtime.h")] + [
+DEPS = SRCS + [os.path.join(H, "fakehip", "hip", "hip_runtime.h"), os.path.join(H, "harness_walk.h")] + [
     os.path.join(ROOT, "emqx_amd", "csrc", f) for f in ("gm_engine.cpp", "gm_common.h", "gm_kernels.h")
 ] + [os.path.join(ROOT, "include", "emqx_gpumatch.h")]
 
 
-def _build():
-    if os.path.exists(OUT) and all(os.path.getmtime(d) <= os.path.getmtime(OUT) for d in DEPS):
-        return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
-           "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer", "-Wno-subobject-linkage",
-           "-I", os.path.join(H, "fakehip")] + SRCS + ["-pthread", "-o", OUT]
+SAN = {"asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
+                "-fno-omit-frame-pointer"],
+       "tsan": ["-fsanitize=thread"]}
+
+
+def _build(main="harness.cpp", san="asan"):
+    out = OUT if (main, san) == ("harness.cpp", "asan") else os.path.join(
+        H, "build", main.replace(".cpp", "") + "_" + san)
+    srcs = [os.path.join(H, main)] + SRCS[1:]
+    deps = DEPS + [srcs[0]]
+    if os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = ["g++", "-std=c++17", "-O1", "-g"] + SAN[san] + [
+        "-Wno-subobject-linkage", "-I", os.path.join(H, "fakehip")] + srcs + ["-pthread", "-o", out]
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     assert r.returncode == 0, r.stdout[-4000:]
-    return OUT
+    return out
 
 
 @pytest.mark.timeout(600)
@@ -55,3 +70,26 @@ def test_engine_host_code_under_asan_ubsan(seed, rounds, hash_bits, keyed, tmp_p
     assert commits > 0 and checks > 0  # (the counts are the restored engine's: it replaced the first)
     if hash_bits == 0:
         assert delta > 0 and full > 0  # both commit paths ran
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("san,seed,delta_max", [("tsan", 21, 300), ("asan", 22, 400)])
+def test_subscribe_visible_during_background_builds(san, seed, delta_max):
+    """Each single subscribe / unsubscribe committed with EMQXGM_SET_COMMIT is visible on the
+    next match while a full build runs in the background; the bulk that started the build is
+    visible exactly from its install on; a batch the current tables cannot take waits for the
+    install and is visible after it.  The printed latency is the single subscribes' during
+    builds (fake HIP runtime: host-side cost only).  delta_max: the changes a delta takes
+    (tune "delta_max"; 0 = the default bound, 4096 at these sizes) -- small under TSan to keep
+    the bulk small."""
+    exe = _build("bg_harness.cpp", san)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1",
+               TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1")
+    r = subprocess.run([exe, str(seed), str(delta_max)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                       text=True, env=env, timeout=840)
+    assert r.returncode == 0, r.stdout[-6000:]
+    last = r.stdout.strip().splitlines()[-1].split()
+    assert last[0] == "OK", r.stdout[-2000:]
+    checks, builds, waits = map(int, last[1:4])
+    assert checks > 500 and builds >= 3 and waits >= 1
