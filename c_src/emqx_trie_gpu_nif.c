@@ -1,21 +1,28 @@
 /*
  * emqx_trie_gpu_nif.c -- the Erlang NIF over libemqx_gpumatch.so (include/emqx_gpumatch.h).
  *
- * Loaded by src/emqx_trie_gpu_nif.erl.  It replaces the publish-time match path of EMQX
- * 5.0.14: emqx_trie:match/1 and match_session/1 (apps/emqx/src/emqx_trie.erl:147-169) as called
- * by emqx_router:match_routes/1 (apps/emqx/src/emqx_router.erl:141-157) and
- * emqx_session_router:match_routes/1 (emqx_session_router.erl:145-159) from
- * emqx_broker:publish/1 (apps/emqx/src/emqx_broker.erl:218-232).
+ * Loaded by src/emqx_trie_gpu_nif.erl.  It replaces the publish-time routing path of EMQX
+ * 5.0.14: emqx_trie:match/1 and match_session/1 (apps/emqx/src/emqx_trie.erl:147-169), the route
+ * lookups of emqx_router:match_routes/1 (apps/emqx/src/emqx_router.erl:141-157) and the aggre /
+ * local dispatch of emqx_broker:publish/1 (apps/emqx/src/emqx_broker.erl:218-300, 546-579).
  *
- * One resource = one index (the route table's trie + route keys, or the session router's) held
- * by one engine per GPU of broker.perf.gpu_match.devices (every engine the whole index: the
- * replica layout of DESIGN.md 5) plus the concurrent publish entry over them
- * (emqxgm_async_*).  Publisher processes call match_async/3 themselves, concurrently, on their
- * own schedulers; the engine's completer threads send each caller
- *     {emqx_trie_gpu, Id, [Filter]}  or  {emqx_trie_gpu, Id, {error, Reason}}
- * (src/emqx_trie_gpu.erl waits for it, and falls back to the reference's own emqx_trie:match/1
- * on an error or a timeout).  The mirror of the committed route table
- * (src/emqx_trie_gpu_sync.erl) calls route_set/3, sync_begin/1, sync_end/2 and commit/1.
+ * One resource = one index (the route table's trie, route keys, dests and local subscribers, or
+ * the session router's) held by one engine per GPU of broker.perf.gpu_match.devices (every engine
+ * the whole index: the replica layout of DESIGN.md 5) plus the concurrent entries over them
+ * (emqxgm_async_*).  Publisher processes call match_async/3 or publish_async/3 themselves,
+ * concurrently, on their own schedulers, with a fresh reference (make_ref/0, so the receive
+ * skips the mailbox), and get back {ok, Call}; an engine completer thread sends each caller
+ *     {emqx_trie_gpu, Ref, Filters, ExactHit}                  (match_async)
+ *     {emqx_trie_gpu, Ref, {routes, Entries, Deliveries}}      (publish_async)
+ *     {emqx_trie_gpu, Ref, {error, Reason}}
+ * (src/emqx_trie_gpu.erl waits for it and takes the reference's own path on an error or a
+ * timeout, after cancel/2).  Each accepted call is a small resource holding its own environment
+ * with the caller's reference: it lives until the call is answered or cancelled.
+ *
+ * The mirror of the committed tables (src/emqx_trie_gpu_sync.erl and the writing node's hook in
+ * emqx_trie_gpu) calls route_sync/2 (membership, committed before it returns), route_dests/3,
+ * subscribers/3, register/3 and set_local_node/2 (the fan-out tables, the terms behind their
+ * handles), and route_set_many/3 + sync_begin/1 + sync_end/2 + commit/1 for a resync.
  *
  * Compiled only where erl_nif.h exists (c_src/Makefile); this image has no Erlang runtime, so
  * the C-ABI below it is tested through ctypes and the C harness of tests/host_harness
@@ -23,32 +30,85 @@
  */
 #include <erl_nif.h>
 #include <errno.h>
+#include <stdint.h>
 #include <string.h>
 
 #include "emqx_gpumatch.h"
 
 #define GM_MAX_DEVICES 16
+#define GM_MAX_TOPIC 65535 /* emqx_topic.erl:47 ?MAX_TOPIC_LEN */
+
+/* The terms the engine's 32-bit handles stand for (node atoms, shared-subscription groups,
+ * subscriber pids), registered by the mirror: the engine's fan-out answers in handles, a
+ * publisher gets the terms. */
+typedef struct {
+  ErlNifRWLock* lk;
+  ErlNifEnv* env; /* holds the copies (a re-registered handle's old copy stays until unload) */
+  ERL_NIF_TERM* v;
+  unsigned n;     /* handles [0, n) have a slot; v[i] == 0: none */
+} term_tab;
 
 typedef struct {
   unsigned nh;
   emqxgm_t* h[GM_MAX_DEVICES];
-  emqxgm_async_t* a;
+  emqxgm_async_t* a;  /* match_async */
+  emqxgm_async_t* ap; /* publish_async (open option publish) */
+  uint64_t next_tag;  /* call tags: unique per resource, so a stale one never matches a cancel */
+  term_tab nodes, groups, subs;
 } gm_res;
 
-static ErlNifResourceType* RT;
-static ERL_NIF_TERM A_OK, A_ERROR, A_TRUE, A_FALSE, A_MOD;
+/* One accepted call until its answer is sent or it is cancelled. */
+typedef struct {
+  ErlNifEnv* env; /* the message is built here and sent from the completer thread */
+  ERL_NIF_TERM ref;
+  ErlNifPid pid;
+  uint64_t tag;
+  int publish;
+} gm_call;
 
-/* An ErlNifPid is one term word: it travels through the engine as the call's owner. */
-typedef char gm_pid_fits_owner[sizeof(ErlNifPid) <= sizeof(uint64_t) ? 1 : -1];
+static ErlNifResourceType *RT, *CALL_RT;
+static ERL_NIF_TERM A_OK, A_ERROR, A_TRUE, A_FALSE, A_MOD, A_ROUTES, A_NONE, A_NODE, A_GROUP, A_SUB,
+    A_SPIN_US, A_BG_BUILD, A_PUBLISH, A_UNDEFINED;
+
+static int tab_init(term_tab* t, char* name) {
+  t->lk = enif_rwlock_create(name);
+  t->env = enif_alloc_env();
+  t->v = NULL;
+  t->n = 0;
+  return t->lk && t->env;
+}
+
+static void tab_free(term_tab* t) {
+  if (t->lk) enif_rwlock_destroy(t->lk);
+  if (t->env) enif_free_env(t->env);
+  enif_free(t->v);
+  memset(t, 0, sizeof *t);
+}
+
+/* the term behind handle h copied into env, or `undefined` (caller holds the read lock) */
+static ERL_NIF_TERM tab_get(ErlNifEnv* env, const term_tab* t, uint32_t h) {
+  return (h < t->n && t->v[h]) ? enif_make_copy(env, t->v[h]) : A_UNDEFINED;
+}
 
 static void gm_res_dtor(ErlNifEnv* env, void* obj) {
   gm_res* r = (gm_res*)obj;
   (void)env;
   if (r->a) emqxgm_async_destroy(r->a); /* reports every accepted call first */
+  if (r->ap) emqxgm_async_destroy(r->ap);
   for (unsigned k = 0; k < r->nh; ++k)
     if (r->h[k]) emqxgm_destroy(r->h[k]);
-  r->a = NULL;
+  tab_free(&r->nodes);
+  tab_free(&r->groups);
+  tab_free(&r->subs);
+  r->a = r->ap = NULL;
   r->nh = 0;
+}
+
+static void gm_call_dtor(ErlNifEnv* env, void* obj) {
+  gm_call* c = (gm_call*)obj;
+  (void)env;
+  if (c->env) enif_free_env(c->env);
+  c->env = NULL;
 }
 
 static ERL_NIF_TERM errno_atom(ErlNifEnv* env, int rc) {
@@ -75,48 +135,115 @@ static int get_res(ErlNifEnv* env, ERL_NIF_TERM t, gm_res** r) {
   return enif_get_resource(env, t, RT, (void**)r) && (*r)->nh > 0;
 }
 
+/* Sends call c its message (built in its own environment) and lets the call go. */
+static void answer(gm_call* c, ERL_NIF_TERM result) {
+  ERL_NIF_TERM msg = enif_make_tuple3(c->env, A_MOD, c->ref, result);
+  enif_send(NULL, &c->pid, c->env, msg);
+  enif_free_env(c->env);
+  c->env = NULL;
+  enif_release_resource(c); /* the in-flight reference */
+}
+
+static ERL_NIF_TERM bytes_term(ErlNifEnv* env, const uint8_t* p, size_t len) {
+  ERL_NIF_TERM b;
+  unsigned char* d = enif_make_new_binary(env, len, &b);
+  if (len) memcpy(d, p, len);
+  return b;
+}
+
 /* The completer thread of one engine handle: every caller of a completed window gets its
- * message.  One process-independent environment per window (enif_send clears it each time). */
+ * message (cancelled calls were released by their cancel). */
 static void on_window(void* user, const emqxgm_async_window* w) {
-  (void)user;
-  ErlNifEnv* env = enif_alloc_env();
-  if (!env) return;
+  gm_res* r = (gm_res*)user;
   for (uint32_t i = 0; i < w->n; ++i) {
-    if (w->tag[i] == EMQXGM_TAG_CANCELLED) continue; /* the caller timed out and cancelled */
-    ErlNifPid pid;
-    memcpy(&pid, &w->owner[i], sizeof pid);
+    if (w->tag[i] == EMQXGM_TAG_CANCELLED) continue;
+    gm_call* c = (gm_call*)(uintptr_t)w->owner[i];
+    ErlNifEnv* env = c->env;
     ERL_NIF_TERM res;
     if (w->status) {
       res = err_term(env, w->status);
+    } else if (!c->publish) {
+      ERL_NIF_TERM fl = enif_make_list(env, 0);
+      for (uint32_t j = w->row[i + 1]; j-- > w->row[i];)
+        fl = enif_make_list_cell(env, bytes_term(env, w->fbytes + w->foff[j], w->foff[j + 1] - w->foff[j]), fl);
+      /* the topic itself is a route key: match_routes/1 looks it up (emqx_router.erl:143-144) */
+      const ERL_NIF_TERM hit = w->exact_id[i] != EMQXGM_NONE ? A_TRUE : A_FALSE;
+      ERL_NIF_TERM msg = enif_make_tuple4(env, A_MOD, c->ref, fl, hit);
+      enif_send(NULL, &c->pid, env, msg);
+      enif_free_env(env);
+      c->env = NULL;
+      enif_release_resource(c);
+      continue;
     } else {
-      res = enif_make_list(env, 0);
-      for (uint32_t j = w->row[i + 1]; j-- > w->row[i];) {
-        const size_t len = (size_t)(w->foff[j + 1] - w->foff[j]);
-        ERL_NIF_TERM b;
-        unsigned char* p = enif_make_new_binary(env, len, &b);
-        if (len) memcpy(p, w->fbytes + w->foff[j], len);
-        res = enif_make_list_cell(env, b, res);
+      /* aggre/1 entries {To, Node} | {To, Group} (emqx_broker.erl:284-300) and the local
+       * dispatches {To, SubPid} of the {To, node()} entries (dispatch/2, :326-355) */
+      const uint64_t a = w->route_ptr[i], b = w->route_ptr[i + 1];
+      ERL_NIF_TERM ents = enif_make_list(env, 0), dels = enif_make_list(env, 0);
+      ERL_NIF_TERM to_small[16];
+      ERL_NIF_TERM* to = b - a <= 16 ? to_small : enif_alloc(sizeof(ERL_NIF_TERM) * (size_t)(b - a));
+      if (!to) {
+        answer(c, err_term(env, -ENOMEM));
+        continue;
       }
+      enif_rwlock_rlock(r->nodes.lk);
+      enif_rwlock_rlock(r->groups.lk);
+      for (uint64_t j = a; j < b; ++j) {
+        to[j - a] = bytes_term(env, w->rfbytes + w->rfoff[j], (size_t)(w->rfoff[j + 1] - w->rfoff[j]));
+        const uint32_t d = w->route_dest[j];
+        const ERL_NIF_TERM dt = (d & EMQXGM_DEST_GROUP) ? tab_get(env, &r->groups, d & ~EMQXGM_DEST_GROUP)
+                                                        : tab_get(env, &r->nodes, d);
+        ents = enif_make_list_cell(env, enif_make_tuple2(env, to[j - a], dt), ents);
+      }
+      enif_rwlock_runlock(r->groups.lk);
+      enif_rwlock_runlock(r->nodes.lk);
+      enif_rwlock_rlock(r->subs.lk);
+      for (uint64_t j = w->deliver_ptr[i]; j < w->deliver_ptr[i + 1]; ++j) {
+        ERL_NIF_TERM t = A_UNDEFINED;
+        for (uint64_t q = a; q < b; ++q)
+          if (w->route_filter[q] == w->deliver_filter[j]) {
+            t = to[q - a];
+            break;
+          }
+        dels = enif_make_list_cell(env, enif_make_tuple2(env, t, tab_get(env, &r->subs, w->deliver_sub[j])), dels);
+      }
+      enif_rwlock_runlock(r->subs.lk);
+      if (to != to_small) enif_free(to);
+      res = enif_make_tuple3(env, A_ROUTES, ents, dels);
     }
-    ERL_NIF_TERM msg = enif_make_tuple3(env, A_MOD, enif_make_uint64(env, w->tag[i]), res);
-    enif_send(NULL, &pid, env, msg);
+    answer(c, res);
   }
-  enif_free_env(env);
 }
 
-/* open(Devices, WindowTopics, WindowBytes, WindowUs, MaxLevels) -> {ok, Res} | {error, Reason}
- * broker.perf.gpu_match.{devices, batch_max, batch_window_us, max_levels}
- * (src/emqx_trie_gpu_schema.erl): one engine per device, windows of WindowTopics topics */
+static int opt_uint(ErlNifEnv* env, ERL_NIF_TERM map, ERL_NIF_TERM key, ErlNifSInt64 dflt, ErlNifSInt64* v) {
+  ERL_NIF_TERM t;
+  *v = dflt;
+  return !enif_get_map_value(env, map, key, &t) || enif_get_int64(env, t, v);
+}
+
+/* open(Devices, WindowTopics, WindowBytes, WindowUs, MaxLevels, Opts) -> {ok, Res} | {error, R}
+ * broker.perf.gpu_match.{devices, batch_max, batch_window_us, max_levels} (src/
+ * emqx_trie_gpu_schema.erl): one engine per device, windows of WindowTopics topics.  Opts:
+ * #{spin_us => N (0: a completer blocks at once instead of polling; the default),
+ *   bg_build => N (emqxgm_tune "bg_build"), publish => boolean() (a publish_async layer too)} */
 static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   unsigned ndev, wt, wb, wus, ml;
-  ERL_NIF_TERM list = argv[0], head;
+  ERL_NIF_TERM list = argv[0], head, pub;
+  ErlNifSInt64 spin, bg;
   (void)argc;
   if (!enif_get_list_length(env, list, &ndev) || ndev == 0 || ndev > GM_MAX_DEVICES ||
       !enif_get_uint(env, argv[1], &wt) || !enif_get_uint(env, argv[2], &wb) ||
-      !enif_get_uint(env, argv[3], &wus) || !enif_get_uint(env, argv[4], &ml))
+      !enif_get_uint(env, argv[3], &wus) || !enif_get_uint(env, argv[4], &ml) ||
+      !opt_uint(env, argv[5], A_SPIN_US, 0, &spin) || !opt_uint(env, argv[5], A_BG_BUILD, 16384, &bg))
     return enif_make_badarg(env);
+  const int publish = enif_get_map_value(env, argv[5], A_PUBLISH, &pub) && pub == A_TRUE;
   gm_res* r = enif_alloc_resource(RT, sizeof(gm_res));
   memset(r, 0, sizeof *r);
+  if (!tab_init(&r->nodes, "emqx_trie_gpu.nodes") || !tab_init(&r->groups, "emqx_trie_gpu.groups") ||
+      !tab_init(&r->subs, "emqx_trie_gpu.subs")) {
+    enif_release_resource(r);
+    return err_term(env, -ENOMEM);
+  }
+  r->next_tag = 1;
   int rc = 0;
   for (unsigned k = 0; k < ndev && !rc; ++k) {
     int dev;
@@ -130,16 +257,22 @@ static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
     cfg.full_hash_bits = 64;
     cfg.batch_max = wt; /* one window is one engine batch */
     rc = emqxgm_create(&cfg, &r->h[k]);
-    if (!rc) r->nh = k + 1;
+    if (!rc) {
+      r->nh = k + 1;
+      rc = emqxgm_tune(r->h[k], "spin_us", spin);
+      if (!rc) rc = emqxgm_tune(r->h[k], "bg_build", bg);
+    }
   }
-  if (!rc) {
-    emqxgm_async_cfg ac;
-    memset(&ac, 0, sizeof ac);
-    ac.window_topics = wt;
-    ac.window_bytes = wb;
-    ac.window_us = wus;
-    ac.max_levels = ml;
-    rc = emqxgm_async_create(r->h, r->nh, &ac, on_window, NULL, &r->a);
+  emqxgm_async_cfg ac;
+  memset(&ac, 0, sizeof ac);
+  ac.window_topics = wt;
+  ac.window_bytes = wb;
+  ac.window_us = wus;
+  ac.max_levels = ml;
+  if (!rc) rc = emqxgm_async_create(r->h, r->nh, &ac, on_window, r, &r->a);
+  if (!rc && publish) {
+    ac.flags = EMQXGM_ASYNC_PUBLISH;
+    rc = emqxgm_async_create(r->h, r->nh, &ac, on_window, r, &r->ap);
   }
   if (rc) {
     enif_release_resource(r); /* the destructor frees what was made */
@@ -150,16 +283,290 @@ static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
   return enif_make_tuple2(env, A_OK, t);
 }
 
-/* route_set(Res, Filter, Present) -> ok | {error, Reason}: the route-key / trie membership of
- * Filter in every engine (emqxgm_route_set: a state, not a count; emqx_router_utils.erl:34-71).
- * Visible after commit/1. */
+/* Packs a list of binaries (or of tuples whose first element is one) for a batch call:
+ * bytes / offsets allocated with enif_alloc.  Filters longer than a topic can be
+ * (emqx_topic.erl:47) are never routes: 0, or -E2BIG. */
+typedef struct {
+  unsigned n;
+  uint8_t* bytes;
+  uint64_t* off;
+} packed;
+
+static void packed_free(packed* p) {
+  enif_free(p->bytes);
+  enif_free(p->off);
+  memset(p, 0, sizeof *p);
+}
+
+/* elem: the binary of each list item (item itself, or element 1 of a tuple when tuples) */
+static int pack_list(ErlNifEnv* env, ERL_NIF_TERM list, int tuples, packed* p) {
+  ERL_NIF_TERM head, l = list;
+  size_t total = 0;
+  memset(p, 0, sizeof *p);
+  if (!enif_get_list_length(env, list, &p->n)) return -EINVAL;
+  p->off = enif_alloc(sizeof(uint64_t) * ((size_t)p->n + 1));
+  if (!p->off) return -ENOMEM;
+  p->off[0] = 0;
+  for (unsigned i = 0; i < p->n; ++i) { /* first pass: sizes */
+    ErlNifBinary b;
+    int ar;
+    const ERL_NIF_TERM* el;
+    if (!enif_get_list_cell(env, l, &head, &l)) return -EINVAL;
+    if (tuples) {
+      if (!enif_get_tuple(env, head, &ar, &el) || ar < 2) return -EINVAL;
+      head = el[0];
+    }
+    if (!enif_inspect_binary(env, head, &b)) return -EINVAL;
+    if (b.size > GM_MAX_TOPIC) return -E2BIG;
+    total += b.size;
+    p->off[i + 1] = total;
+  }
+  p->bytes = enif_alloc(total ? total : 1);
+  if (!p->bytes) return -ENOMEM;
+  l = list;
+  for (unsigned i = 0; i < p->n; ++i) {
+    ErlNifBinary b;
+    int ar;
+    const ERL_NIF_TERM* el;
+    enif_get_list_cell(env, l, &head, &l);
+    if (tuples) {
+      enif_get_tuple(env, head, &ar, &el);
+      head = el[0];
+    }
+    enif_inspect_binary(env, head, &b);
+    if (b.size) memcpy(p->bytes + p->off[i], b.data, b.size);
+  }
+  return 0;
+}
+
+/* route_sync(Res, [{Filter, Present :: boolean()}]) -> {ok, Epoch} | {error, R}: the writing node's
+ * hook after emqx_router:do_add_route/2, do_delete_route/2 (emqx_router.erl:124-138, 171-179) and
+ * the mirror's batched table events: membership set AND committed before the return
+ * (emqxgm_route_set_batch with EMQXGM_SET_COMMIT: never a wait for a background full build). */
+static ERL_NIF_TERM nif_route_sync(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_res* r;
+  packed p;
+  (void)argc;
+  if (!get_res(env, argv[0], &r)) return enif_make_badarg(env);
+  int rc = pack_list(env, argv[1], 1, &p);
+  uint8_t* pr = rc ? NULL : enif_alloc(p.n ? p.n : 1);
+  if (!rc && !pr) rc = -ENOMEM;
+  if (!rc) {
+    ERL_NIF_TERM head, l = argv[1];
+    for (unsigned i = 0; i < p.n && !rc; ++i) {
+      int ar;
+      const ERL_NIF_TERM* el;
+      enif_get_list_cell(env, l, &head, &l);
+      enif_get_tuple(env, head, &ar, &el);
+      if (el[1] != A_TRUE && el[1] != A_FALSE) rc = -EINVAL;
+      pr[i] = el[1] == A_TRUE;
+    }
+  }
+  uint64_t epoch = 0;
+  for (unsigned k = 0; k < r->nh && !rc; ++k)
+    rc = emqxgm_route_set_batch(r->h[k], p.bytes, p.off, pr, p.n, EMQXGM_SET_COMMIT, k ? NULL : &epoch);
+  enif_free(pr);
+  packed_free(&p);
+  if (rc == -EINVAL) return enif_make_badarg(env);
+  return rc ? err_term(env, rc) : enif_make_tuple2(env, A_OK, enif_make_uint64(env, epoch));
+}
+
+/* route_set_many(Res, [Filter], Present) -> ok | {error, R}: a resync chunk (emqxgm_route_set_many
+ * on every engine; committed by commit/1 after sync_end/2). */
+static ERL_NIF_TERM nif_route_set_many(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_res* r;
+  packed p;
+  (void)argc;
+  if (!get_res(env, argv[0], &r) || (argv[2] != A_TRUE && argv[2] != A_FALSE)) return enif_make_badarg(env);
+  int rc = pack_list(env, argv[1], 0, &p);
+  for (unsigned k = 0; k < r->nh && !rc; ++k)
+    rc = emqxgm_route_set_many(r->h[k], p.bytes, p.off, p.n, argv[2] == A_TRUE);
+  packed_free(&p);
+  if (rc == -EINVAL) return enif_make_badarg(env);
+  return rc ? err_term(env, rc) : A_OK;
+}
+
+static int get_commit(ERL_NIF_TERM t, uint32_t* flags) {
+  if (t != A_TRUE && t != A_FALSE) return 0;
+  *flags = t == A_TRUE ? EMQXGM_SET_COMMIT : 0;
+  return 1;
+}
+
+/* route_dests(Res, [{Filter, [{NodeH, GroupH | none}]}], Commit) -> {ok, Epoch} | {error, R}: each
+ * filter's rows of the emqx_route bag (emqx_router.erl:72-92) as dest handles (register/3 maps
+ * them to the dest terms): emqxgm_route_dests_batch. */
+static ERL_NIF_TERM nif_route_dests(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_res* r;
+  packed p;
+  uint32_t flags;
+  (void)argc;
+  if (!get_res(env, argv[0], &r) || !get_commit(argv[2], &flags)) return enif_make_badarg(env);
+  int rc = pack_list(env, argv[1], 1, &p);
+  uint32_t *dptr = NULL, *node = NULL, *group = NULL;
+  unsigned nd = 0;
+  if (!rc) {
+    ERL_NIF_TERM head, l = argv[1];
+    dptr = enif_alloc(sizeof(uint32_t) * ((size_t)p.n + 1));
+    if (!dptr) rc = -ENOMEM;
+    for (unsigned i = 0; i < p.n && !rc; ++i) { /* count */
+      int ar;
+      const ERL_NIF_TERM* el;
+      unsigned k;
+      enif_get_list_cell(env, l, &head, &l);
+      enif_get_tuple(env, head, &ar, &el);
+      if (!enif_get_list_length(env, el[1], &k)) rc = -EINVAL;
+      nd += k;
+    }
+    if (!rc) {
+      node = enif_alloc(sizeof(uint32_t) * (nd ? nd : 1));
+      group = enif_alloc(sizeof(uint32_t) * (nd ? nd : 1));
+      if (!node || !group) rc = -ENOMEM;
+    }
+    l = argv[1];
+    unsigned j = 0;
+    for (unsigned i = 0; i < p.n && !rc; ++i) {
+      int ar, dar;
+      const ERL_NIF_TERM *el, *de;
+      ERL_NIF_TERM dh, dl;
+      enif_get_list_cell(env, l, &head, &l);
+      enif_get_tuple(env, head, &ar, &el);
+      dptr[i] = j;
+      for (dl = el[1]; !rc && enif_get_list_cell(env, dl, &dh, &dl); ++j) {
+        unsigned nv = 0, gv = EMQXGM_NONE;
+        if (!enif_get_tuple(env, dh, &dar, &de) || dar != 2 || !enif_get_uint(env, de[0], &nv) ||
+            (de[1] != A_NONE && !enif_get_uint(env, de[1], &gv)))
+          rc = -EINVAL;
+        node[j] = nv;
+        group[j] = gv;
+      }
+    }
+    if (!rc) dptr[p.n] = j;
+  }
+  uint64_t epoch = 0;
+  for (unsigned k = 0; k < r->nh && !rc; ++k)
+    rc = emqxgm_route_dests_batch(r->h[k], p.bytes, p.off, p.n, dptr, node, group, flags, k ? NULL : &epoch);
+  enif_free(dptr);
+  enif_free(node);
+  enif_free(group);
+  packed_free(&p);
+  if (rc == -EINVAL) return enif_make_badarg(env);
+  return rc ? err_term(env, rc) : enif_make_tuple2(env, A_OK, enif_make_uint64(env, epoch));
+}
+
+/* subscribers(Res, [{Filter, [SubH]}], Commit) -> {ok, Epoch} | {error, R}: each filter's local
+ * subscribers (the emqx_subscriber bag, emqx_broker.erl:546-552; shard rows flattened) as
+ * handles: emqxgm_subscribers_batch. */
+static ERL_NIF_TERM nif_subscribers(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_res* r;
+  packed p;
+  uint32_t flags;
+  (void)argc;
+  if (!get_res(env, argv[0], &r) || !get_commit(argv[2], &flags)) return enif_make_badarg(env);
+  int rc = pack_list(env, argv[1], 1, &p);
+  uint32_t *sptr = NULL, *subs = NULL;
+  unsigned ns = 0;
+  if (!rc) {
+    ERL_NIF_TERM head, l = argv[1];
+    sptr = enif_alloc(sizeof(uint32_t) * ((size_t)p.n + 1));
+    if (!sptr) rc = -ENOMEM;
+    for (unsigned i = 0; i < p.n && !rc; ++i) {
+      int ar;
+      const ERL_NIF_TERM* el;
+      unsigned k;
+      enif_get_list_cell(env, l, &head, &l);
+      enif_get_tuple(env, head, &ar, &el);
+      if (!enif_get_list_length(env, el[1], &k)) rc = -EINVAL;
+      ns += k;
+    }
+    if (!rc && !(subs = enif_alloc(sizeof(uint32_t) * (ns ? ns : 1)))) rc = -ENOMEM;
+    l = argv[1];
+    unsigned j = 0;
+    for (unsigned i = 0; i < p.n && !rc; ++i) {
+      int ar;
+      const ERL_NIF_TERM* el;
+      ERL_NIF_TERM sh, sl;
+      enif_get_list_cell(env, l, &head, &l);
+      enif_get_tuple(env, head, &ar, &el);
+      sptr[i] = j;
+      for (sl = el[1]; !rc && enif_get_list_cell(env, sl, &sh, &sl); ++j) {
+        unsigned v;
+        if (!enif_get_uint(env, sh, &v)) rc = -EINVAL;
+        subs[j] = v;
+      }
+    }
+    if (!rc) sptr[p.n] = j;
+  }
+  uint64_t epoch = 0;
+  for (unsigned k = 0; k < r->nh && !rc; ++k)
+    rc = emqxgm_subscribers_batch(r->h[k], p.bytes, p.off, p.n, sptr, subs, flags, k ? NULL : &epoch);
+  enif_free(sptr);
+  enif_free(subs);
+  packed_free(&p);
+  if (rc == -EINVAL) return enif_make_badarg(env);
+  return rc ? err_term(env, rc) : enif_make_tuple2(env, A_OK, enif_make_uint64(env, epoch));
+}
+
+/* register(Res, node | group | sub, [{Handle, Term}]) -> ok: the terms publish_async answers with */
+static ERL_NIF_TERM nif_register(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_res* r;
+  ERL_NIF_TERM head, l = argv[2];
+  (void)argc;
+  if (!get_res(env, argv[0], &r) || !enif_is_list(env, argv[2])) return enif_make_badarg(env);
+  term_tab* t = argv[1] == A_NODE ? &r->nodes : argv[1] == A_GROUP ? &r->groups : argv[1] == A_SUB ? &r->subs : NULL;
+  if (!t) return enif_make_badarg(env);
+  int bad = 0;
+  enif_rwlock_rwlock(t->lk);
+  while (!bad && enif_get_list_cell(env, l, &head, &l)) {
+    int ar;
+    const ERL_NIF_TERM* el;
+    unsigned hv;
+    if (!enif_get_tuple(env, head, &ar, &el) || ar != 2 || !enif_get_uint(env, el[0], &hv) ||
+        hv >= 0x7FFFFFFFu) {
+      bad = 1;
+      break;
+    }
+    if (hv >= t->n) {
+      unsigned n2 = t->n ? t->n : 64;
+      while (n2 <= hv) n2 *= 2;
+      ERL_NIF_TERM* v = enif_realloc(t->v, sizeof(ERL_NIF_TERM) * n2);
+      if (!v) {
+        bad = 2;
+        break;
+      }
+      memset(v + t->n, 0, sizeof(ERL_NIF_TERM) * (n2 - t->n));
+      t->v = v;
+      t->n = n2;
+    }
+    t->v[hv] = enif_make_copy(t->env, el[1]);
+  }
+  enif_rwlock_rwunlock(t->lk);
+  if (bad == 1) return enif_make_badarg(env);
+  return bad ? err_term(env, -ENOMEM) : A_OK;
+}
+
+/* set_local_node(Res, NodeH) -> ok: node()'s dest handle (emqxgm_set_local_node) */
+static ERL_NIF_TERM nif_set_local_node(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_res* r;
+  unsigned v;
+  (void)argc;
+  if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &v)) return enif_make_badarg(env);
+  for (unsigned k = 0; k < r->nh; ++k) {
+    const int rc = emqxgm_set_local_node(r->h[k], v);
+    if (rc) return err_term(env, rc);
+  }
+  return A_OK;
+}
+
+/* route_set(Res, Filter, Present) -> ok | {error, Reason}: one filter's membership in every engine
+ * (no commit: the resync's and the mirror's unbatched form) */
 static ERL_NIF_TERM nif_route_set(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   gm_res* r;
   ErlNifBinary bin;
   (void)argc;
-  if (!get_res(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &bin) || bin.size > 65535 ||
+  if (!get_res(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &bin) ||
       (argv[2] != A_TRUE && argv[2] != A_FALSE))
     return enif_make_badarg(env);
+  if (bin.size > GM_MAX_TOPIC) return err_term(env, -E2BIG);
   for (unsigned k = 0; k < r->nh; ++k) {
     const int rc = emqxgm_route_set(r->h[k], bin.data, (uint32_t)bin.size, argv[2] == A_TRUE);
     if (rc) return err_term(env, rc);
@@ -201,8 +608,8 @@ static ERL_NIF_TERM nif_sync_end(ErlNifEnv* env, int argc, const ERL_NIF_TERM ar
   return enif_make_tuple2(env, A_OK, enif_make_uint64(env, removed));
 }
 
-/* commit(Res) -> {ok, Epoch}: the atomic epoch swap on every engine (a delta patch or a full
- * build; dirty CPU) */
+/* commit(Res) -> {ok, Epoch}: everything pending visible on every engine (a delta patch, or a full
+ * build -- in the background for a large registry, this call waiting for its install; dirty CPU) */
 static ERL_NIF_TERM nif_commit(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   gm_res* r;
   uint64_t epoch = 0;
@@ -232,8 +639,8 @@ typedef int (*member_fn)(emqxgm_t*, const uint8_t*, uint32_t);
 static ERL_NIF_TERM do_member(ErlNifEnv* env, const ERL_NIF_TERM argv[], member_fn f) {
   gm_res* r;
   ErlNifBinary bin;
-  if (!get_res(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &bin) || bin.size > 65535)
-    return enif_make_badarg(env);
+  if (!get_res(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &bin)) return enif_make_badarg(env);
+  if (bin.size > GM_MAX_TOPIC) return A_FALSE; /* never a filter (emqx_topic.erl:47) */
   const int rc = f(r->h[0], bin.data, (uint32_t)bin.size);
   return rc < 0 ? err_term(env, rc) : (rc ? A_TRUE : A_FALSE);
 }
@@ -250,39 +657,65 @@ static ERL_NIF_TERM nif_route_member(ErlNifEnv* env, int argc, const ERL_NIF_TER
   return do_member(env, argv, emqxgm_route_member);
 }
 
-/* match_async(Res, Topic, Id) -> ok | {error, e2big | ebusy | eshutdown}: Topic joins the open
- * window; the caller (self()) later receives {emqx_trie_gpu, Id, Result}.  Id: a unique
- * non-negative integer (erlang:unique_integer([positive])).  Runs on the caller's own scheduler
- * (a copy into pinned memory under a short lock). */
-static ERL_NIF_TERM nif_match_async(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+/* match_async(Res, Topic, Ref) / publish_async(Res, Topic, Ref) -> {ok, Call} | {error, R}: Topic
+ * joins the open window of the layer on the caller's own scheduler (a copy into pinned memory);
+ * the caller (self()) later receives {emqx_trie_gpu, Ref, ...}.  e2big: deeper than max_levels or
+ * longer than a topic can be (the caller takes emqx_trie:match/1 then); ebusy: every window full;
+ * einval: no publish layer. */
+static ERL_NIF_TERM do_async(ErlNifEnv* env, const ERL_NIF_TERM argv[], int publish) {
   gm_res* r;
   ErlNifBinary bin;
-  ErlNifUInt64 id;
   ErlNifPid self;
-  uint64_t owner = 0;
-  (void)argc;
   if (!get_res(env, argv[0], &r) || !enif_inspect_binary(env, argv[1], &bin) ||
-      !enif_get_uint64(env, argv[2], &id) || id == EMQXGM_TAG_CANCELLED || bin.size > 65535 ||
-      !enif_self(env, &self))
+      !enif_is_ref(env, argv[2]) || !enif_self(env, &self))
     return enif_make_badarg(env);
-  memcpy(&owner, &self, sizeof self);
-  const int rc = emqxgm_async_match(r->a, bin.data, (uint32_t)bin.size, id, owner);
-  return rc ? err_term(env, rc) : A_OK;
+  emqxgm_async_t* a = publish ? r->ap : r->a;
+  if (!a) return err_term(env, -EINVAL);
+  if (bin.size > GM_MAX_TOPIC) return err_term(env, -E2BIG);
+  gm_call* c = enif_alloc_resource(CALL_RT, sizeof(gm_call));
+  if (!c) return err_term(env, -ENOMEM);
+  memset(c, 0, sizeof *c);
+  ERL_NIF_TERM t = enif_make_resource(env, c); /* the caller's handle (cancel/2) */
+  enif_release_resource(c);                    /* ... owns the allocation now */
+  if (!(c->env = enif_alloc_env())) return err_term(env, -ENOMEM);
+  c->ref = enif_make_copy(c->env, argv[2]);
+  c->pid = self;
+  c->publish = publish;
+  c->tag = __atomic_fetch_add(&r->next_tag, 1, __ATOMIC_RELAXED);
+  enif_keep_resource(c); /* the in-flight reference: released by its answer or its cancel */
+  const int rc = emqxgm_async_match(a, bin.data, (uint32_t)bin.size, c->tag, (uint64_t)(uintptr_t)c);
+  if (rc) {
+    enif_release_resource(c);
+    return err_term(env, rc);
+  }
+  return enif_make_tuple2(env, A_OK, t);
 }
 
-/* cancel(Res, Id) -> true | false: true = the call will never be answered; false = its answer
+static ERL_NIF_TERM nif_match_async(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  return do_async(env, argv, 0);
+}
+
+static ERL_NIF_TERM nif_publish_async(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  return do_async(env, argv, 1);
+}
+
+/* cancel(Res, Call) -> true | false: true = the call will never be answered; false = its answer
  * is already in the caller's mailbox.  Dirty IO: may wait while the call's window is reported. */
 static ERL_NIF_TERM nif_cancel(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   gm_res* r;
-  ErlNifUInt64 id;
-  ErlNifPid self;
-  uint64_t owner = 0;
+  gm_call* c;
   (void)argc;
-  if (!get_res(env, argv[0], &r) || !enif_get_uint64(env, argv[1], &id) || !enif_self(env, &self))
+  if (!get_res(env, argv[0], &r) || !enif_get_resource(env, argv[1], CALL_RT, (void**)&c))
     return enif_make_badarg(env);
-  memcpy(&owner, &self, sizeof self);
-  const int rc = emqxgm_async_cancel(r->a, id, owner);
-  return rc < 0 ? err_term(env, rc) : (rc ? A_TRUE : A_FALSE);
+  emqxgm_async_t* a = c->publish ? r->ap : r->a;
+  if (!a || c->tag == 0) return A_FALSE;
+  const int rc = emqxgm_async_cancel(a, c->tag, (uint64_t)(uintptr_t)c);
+  if (rc < 0) return err_term(env, rc);
+  if (rc == 0) return A_FALSE;
+  enif_release_resource(c); /* never answered: the in-flight reference goes here */
+  return A_TRUE;
 }
 
 /* tune(Res, Key, Value) -> ok | {error, einval}: emqxgm_tune knobs on every engine */
@@ -301,19 +734,25 @@ static ERL_NIF_TERM nif_tune(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
   return A_OK;
 }
 
-/* stats(Res) -> #{calls, windows, reported, busy, cancelled, too_deep, failed, outstanding} */
+/* stats(Res) -> #{calls, windows, reported, busy, cancelled, too_deep, failed, outstanding,
+ * bg_builds, bg_waits, last_build_ms} */
 static ERL_NIF_TERM nif_stats(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   static const char* keys[8] = {"calls", "windows", "reported", "busy",
                                 "cancelled", "too_deep", "failed", "outstanding"};
   gm_res* r;
   uint64_t v[8];
+  emqxgm_stats st;
   (void)argc;
   if (!get_res(env, argv[0], &r)) return enif_make_badarg(env);
-  const int rc = emqxgm_async_stats(r->a, v);
+  int rc = emqxgm_async_stats(r->a, v);
+  if (!rc) rc = emqxgm_get_stats(r->h[0], &st);
   if (rc) return err_term(env, rc);
   ERL_NIF_TERM m = enif_make_new_map(env);
   for (int i = 0; i < 8; ++i)
     enif_make_map_put(env, m, enif_make_atom(env, keys[i]), enif_make_uint64(env, v[i]), &m);
+  enif_make_map_put(env, m, enif_make_atom(env, "bg_builds"), enif_make_uint64(env, st.bg_builds), &m);
+  enif_make_map_put(env, m, enif_make_atom(env, "bg_waits"), enif_make_uint64(env, st.bg_waits), &m);
+  enif_make_map_put(env, m, enif_make_atom(env, "last_build_ms"), enif_make_double(env, st.last_build_ms), &m);
   return m;
 }
 
@@ -321,19 +760,35 @@ static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   (void)priv;
   (void)info;
   RT = enif_open_resource_type(env, NULL, "emqx_trie_gpu", gm_res_dtor, ERL_NIF_RT_CREATE, NULL);
-  if (!RT || emqxgm_abi_version() != EMQXGM_ABI_VERSION) return -1;
+  CALL_RT = enif_open_resource_type(env, NULL, "emqx_trie_gpu_call", gm_call_dtor, ERL_NIF_RT_CREATE, NULL);
+  if (!RT || !CALL_RT || emqxgm_abi_version() != EMQXGM_ABI_VERSION) return -1;
   A_OK = enif_make_atom(env, "ok");
   A_ERROR = enif_make_atom(env, "error");
   A_TRUE = enif_make_atom(env, "true");
   A_FALSE = enif_make_atom(env, "false");
   A_MOD = enif_make_atom(env, "emqx_trie_gpu");
+  A_ROUTES = enif_make_atom(env, "routes");
+  A_NONE = enif_make_atom(env, "none");
+  A_NODE = enif_make_atom(env, "node");
+  A_GROUP = enif_make_atom(env, "group");
+  A_SUB = enif_make_atom(env, "sub");
+  A_SPIN_US = enif_make_atom(env, "spin_us");
+  A_BG_BUILD = enif_make_atom(env, "bg_build");
+  A_PUBLISH = enif_make_atom(env, "publish");
+  A_UNDEFINED = enif_make_atom(env, "undefined");
   return 0;
 }
 
 static ErlNifFunc funcs[] = {
-    {"open", 5, nif_open, ERL_NIF_DIRTY_JOB_IO_BOUND},
-    /* the writer lock: held through a commit's full build (seconds at 10M filters) */
+    {"open", 6, nif_open, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    /* the writer lock: a commit that must wait for a background build holds a dirty scheduler */
+    {"route_sync", 2, nif_route_sync, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"route_set", 3, nif_route_set, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"route_set_many", 3, nif_route_set_many, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"route_dests", 3, nif_route_dests, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"subscribers", 3, nif_subscribers, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"register", 3, nif_register, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"set_local_node", 2, nif_set_local_node, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"sync_begin", 1, nif_sync_begin, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"sync_end", 2, nif_sync_end, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"commit", 1, nif_commit, ERL_NIF_DIRTY_JOB_CPU_BOUND},
@@ -341,8 +796,9 @@ static ErlNifFunc funcs[] = {
     {"trie_member", 2, nif_trie_member, 0},
     {"route_member", 2, nif_route_member, 0},
     {"match_async", 3, nif_match_async, 0},
+    {"publish_async", 3, nif_publish_async, 0},
     {"cancel", 2, nif_cancel, ERL_NIF_DIRTY_JOB_IO_BOUND},
-    {"tune", 3, nif_tune, ERL_NIF_DIRTY_JOB_IO_BOUND},  /* some keys drain the passes in flight */
+    {"tune", 3, nif_tune, ERL_NIF_DIRTY_JOB_IO_BOUND}, /* some keys drain the passes in flight */
     {"stats", 1, nif_stats, 0},
 };
 

@@ -17,16 +17,20 @@ max_levels         128                ``emqxgm_async_cfg.max_levels``: deeper to
                                       reference's ``emqx_trie:match/1`` (``mqtt.max_topic_levels``,
                                       emqx_schema.erl:405-412)
 delta_commit       small              ``emqxgm_tune("delta_commit", never 0 / small 1 / always 2)``
+bg_build           16384              ``emqxgm_tune("bg_build")``: full builds of registries of at
+                                      least this many filters run in the background (r05)
+publish            true               a publish layer (``EMQXGM_ASYNC_PUBLISH``) beside the match one
+spin_us            0                  ``emqxgm_tune("spin_us")``: completer threads block at once
 timeout_ms         5000               a publisher's wait before it cancels and takes the
                                       reference's match (src/emqx_trie_gpu.erl)
-resync_interval_ms 30000              period of the mirror's full resync
-                                      (``emqxgm_route_sync_begin`` / ``_end``)
+resync_interval_ms (role)             period of the mirror's full resync (``emqxgm_route_sync_begin``
+                                      / ``_end``): none (0) on a core node, 30000 on a replicant
 ================== ================== ======================================================
 """
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Dict, List, Mapping
+from typing import Dict, List, Mapping, Optional
 
 DELTA_COMMIT = {"never": 0, "small": 1, "always": 2}
 
@@ -39,8 +43,11 @@ class GpuMatchConfig:
     batch_window_us: int = 50
     max_levels: int = 128
     delta_commit: str = "small"
+    bg_build: int = 16384
+    publish: bool = True
+    spin_us: int = 0
     timeout_ms: int = 5000
-    resync_interval_ms: int = 30000
+    resync_interval_ms: Optional[int] = None  # None: by the node's mria role
 
     @classmethod
     def from_map(cls, conf: Mapping) -> "GpuMatchConfig":
@@ -68,7 +75,12 @@ class GpuMatchConfig:
         rng("batch_window_us", self.batch_window_us, 1, 1_000_000)
         rng("max_levels", self.max_levels, 1, 65535)
         rng("timeout_ms", self.timeout_ms, 1, 600_000)
-        rng("resync_interval_ms", self.resync_interval_ms, 100, 86_400_000)
+        if self.resync_interval_ms is not None:
+            rng("resync_interval_ms", self.resync_interval_ms, 0, 86_400_000)
+        rng("bg_build", self.bg_build, 0, 1 << 62)
+        rng("spin_us", self.spin_us, 0, 1_000_000)
+        if not isinstance(self.publish, bool):
+            raise ValueError("broker.perf.gpu_match.publish: expected a boolean")
         if self.delta_commit not in DELTA_COMMIT:
             raise ValueError(f"broker.perf.gpu_match.delta_commit: one of {sorted(DELTA_COMMIT)}")
 
@@ -89,10 +101,17 @@ class GpuMatchConfig:
 
     def tunes(self) -> Dict[str, int]:
         """``emqxgm_tune`` knobs."""
-        return {"delta_commit": DELTA_COMMIT[self.delta_commit]}
+        return {"delta_commit": DELTA_COMMIT[self.delta_commit], "bg_build": self.bg_build,
+                "spin_us": self.spin_us}
+
+    def resync_ms(self, role: str = "core") -> int:
+        """The mirror's resync period on a node of this mria role (0: none)."""
+        if self.resync_interval_ms is not None:
+            return self.resync_interval_ms
+        return 30000 if role == "replicant" else 0
 
     def open(self, callback):
-        """The engines and their concurrent entry as the NIF's open/5 makes them
+        """The engines and their concurrent entry as the NIF's open/6 makes them
         (emqx_trie_gpu_sync:init/1): one Engine per device, tuned, and an AsyncMatcher over them
         reporting completed windows to `callback`."""
         from .engine import AsyncMatcher, Engine

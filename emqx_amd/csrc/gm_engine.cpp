@@ -565,6 +565,7 @@ struct emqxgm {
   std::vector<uint32_t> fan_changed;  // filter ids whose fan-out lists may differ
   bool fan_rebuild = false;           // every filter's lists may differ (local node changed)
   OwnerP o_fan;                       // the fan-out tables
+  OwnerP o_fv;                        // a regrown verify-bit array (grow_fv; until a full build)
   PatchList patches;
   DevBuf d_patch;                   // device copy of the staged patch list
   DevBuf d_rules;                   // emqxgm_match_rules inputs and output
@@ -1067,6 +1068,7 @@ int upload_model(emqxgm* h, TrieModel& m) {
   OwnerP o;
   if (int rc = upload_tables(h, build_in(h, false), m, nx, o)) return rc;
   h->o_tab = std::move(o);
+  h->o_fv.reset();  // (the new tables have their own verify bits)
   h->ix = nx;
   return 0;
 }
@@ -1364,6 +1366,26 @@ int commit_full(emqxgm* h) {
 // changes, so they leave the model valid (a background build then runs while later deltas still
 // patch it); only a delta that would need a multi[] list (level-token collisions) gives the model
 // up half-way.
+// The verify-bit array of the writer's index regrown to `need` words plus headroom: a new
+// buffer (owner o_fv until the next full build brings its own) filled from the host model; the
+// epochs reading the old array keep it.
+int grow_fv(emqxgm* h, TrieModel& m, uint64_t need) {
+  const uint64_t cap = need + std::max<uint64_t>(1024, need / 4);
+  if (int rc = patch_wait(h)) return rc;  // (patches to the old array have landed)
+  auto o = std::make_shared<DevOwner>();
+  DevBuf nb;
+  nb.bytes = cap * 4;
+  HIPCHK(h, hipMalloc(&nb.p, nb.bytes));
+  o->bufs.push_back(nb);
+  m.fvbits.resize(cap, 0u);
+  HIPCHK(h, hipMemcpy(nb.p, m.fvbits.data(), cap * 4, hipMemcpyHostToDevice));
+  m.fv_cap = cap;
+  m.d_fv = (uint32_t*)nb.p;
+  h->ix.fvbits = (const uint32_t*)nb.p;
+  h->o_fv = std::move(o);
+  return 0;
+}
+
 int commit_delta(emqxgm* h, const std::vector<uint8_t>* base = nullptr) {
   TrieModel& m = h->tm;
   if (!m.valid || h->delta_mode == 0) return 1;
@@ -1384,7 +1406,11 @@ int commit_delta(emqxgm* h, const std::vector<uint8_t>* base = nullptr) {
   if (h->delta_mode == 1 &&
       nchg > (h->delta_max ? h->delta_max : std::max<uint64_t>(4096, (m.n_trie + m.n_route) / 8)))
     return 1;
-  if ((nf + 31) / 32 + 1 > m.fv_cap) return 1;
+  if ((nf + 31) / 32 + 1 > m.fv_cap) {
+    // filter ids registered past the verify bits' headroom (a bulk registration, whose build
+    // runs in the background): a larger array, from the host model
+    if (int rc = grow_fv(h, m, (nf + 31) / 32 + 1)) return rc;
+  }
 
   const uint64_t test_mask = h->test_mask;
   std::vector<uint64_t> toks;
@@ -1392,8 +1418,11 @@ int commit_delta(emqxgm* h, const std::vector<uint8_t>* base = nullptr) {
   {
     // the nodes and slots the delta can take at most: each added filter's path levels that are
     // not in the trie yet, plus every node a delete may free and an add re-create
-    uint64_t new_nodes = 0, xa[2] = {0, 0};
-    for (uint32_t id : tadd) {
+    // (and a fat half moved out of its parent's bucket where the first new node is a second
+    // literal child: one more slot)
+    uint64_t new_nodes = 0, moved = 0, xa[2] = {0, 0};
+    std::unordered_map<uint32_t, uint32_t> dpass;  // node -> deleted filters passing it
+    auto walk = [&](uint32_t id, auto&& on_node) {
       const Filter& f = h->filters[id];
       bool hashed;
       tokenize(h->pool.data() + f.off, f.len, test_mask, toks, is_plus, is_hash, hashed);
@@ -1404,14 +1433,21 @@ int commit_delta(emqxgm* h, const std::vector<uint8_t>* base = nullptr) {
         const uint32_t* v = m.emap.find(cur, is_plus[w] ? PLUS_TOK : toks[w]);
         if (!v) break;
         cur = *v;
+        on_node(cur);
       }
       new_nodes += path_len - w;
-    }
+      if (w < path_len && !is_plus[w] && m.fchild[cur]) moved += 1;
+    };
     if (!tadd.empty())
-      for (uint32_t id : tdel) new_nodes += 1 + (uint64_t)std::count(
-          h->pool.data() + h->filters[id].off, h->pool.data() + h->filters[id].off + h->filters[id].len, '/');
+      for (uint32_t id : tdel) walk(id, [&](uint32_t n) { dpass[n] += 1; });
+    new_nodes = moved = 0;
+    for (uint32_t id : tadd)
+      walk(id, [&](uint32_t n) {  // a node the deletes free is created again
+        auto it = dpass.find(n);
+        if (it != dpass.end() && it->second >= m.ref[n]) new_nodes += 1;
+      });
     if (m.parent.size() + new_nodes > std::min<uint64_t>(MAX_NODES, m.tn_cap) ||
-        (m.n_occ + 2 * new_nodes) * 2 > m.ecap)
+        (m.n_occ + new_nodes + moved) * 2 > m.ecap)
       return 1;
     for (uint32_t id : radd) xa[h->filters[id].wild ? 1 : 0] += 1;
     for (int w = 0; w < 2; ++w)
@@ -1668,7 +1704,7 @@ int publish_epoch(emqxgm* h, bool delta) {
   auto E = std::make_shared<Epoch>();
   E->id = h->epoch + 1;
   E->ix = h->ix;
-  E->owners = {h->o_tab, h->o_fan, h->m_pool.o, h->m_foff.o, h->m_fver.o};
+  E->owners = {h->o_tab, h->o_fan, h->m_pool.o, h->m_foff.o, h->m_fver.o, h->o_fv};
   HIPCHK(h, hipEventCreateWithFlags(&E->ready, hipEventDisableTiming));
   std::lock_guard<std::mutex> g(h->emu);
   if (delta && h->cur) {
@@ -1866,6 +1902,7 @@ int install_build(emqxgm* h) {
     J->m.valid = true;
     h->tm = std::move(J->m);
     h->o_tab = std::move(J->o);
+    h->o_fv.reset();
     set_tables(h->ix, J->nx);
     h->changed = ch;
     rc = commit_delta(h, &J->seen);
@@ -1890,6 +1927,7 @@ int install_build(emqxgm* h) {
     h->dirty = true;
     return rc;
   }
+  const uint64_t n_catchup = ch.size();
   if (!J->covered.empty() && J->covered[0] == NONE) {
     flip_committed(h, nullptr);
   } else {
@@ -1901,7 +1939,7 @@ int install_build(emqxgm* h) {
   commit_stats(h, ms_since(t0), false);
   std::lock_guard<std::mutex> g(h->stmu);
   h->st.last_build_ms = J->build_ms;
-  h->st.catchup_changes = ch.size();
+  h->st.catchup_changes = n_catchup;
   return 0;
 }
 
@@ -3012,7 +3050,7 @@ int emqxgm_commit(emqxgm_t* h, uint64_t* epoch) {
 
 int emqxgm_route_set_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets,
                            const uint8_t* present, uint64_t n, uint32_t flags, uint64_t* epoch) {
-  if (!h || !offsets || (!bytes && n) || (flags & ~EMQXGM_SET_COMMIT)) return -EINVAL;
+  if (!h || !offsets || (!bytes && n && offsets[n]) || (flags & ~EMQXGM_SET_COMMIT)) return -EINVAL;
   for (uint64_t i = 0; i < n; ++i)
     if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > 65535) return -EINVAL;
   std::unique_lock<std::mutex> lk(h->wmu);
@@ -3036,7 +3074,7 @@ int emqxgm_route_set_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* of
 int emqxgm_route_dests_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
                              const uint32_t* dptr, const uint32_t* node, const uint32_t* group,
                              uint32_t flags, uint64_t* epoch) {
-  if (!h || !offsets || !dptr || (!bytes && n) || (flags & ~EMQXGM_SET_COMMIT)) return -EINVAL;
+  if (!h || !offsets || !dptr || (!bytes && n && offsets[n]) || (flags & ~EMQXGM_SET_COMMIT)) return -EINVAL;
   for (uint64_t i = 0; i < n; ++i) {
     if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > 65535 || dptr[i + 1] < dptr[i])
       return -EINVAL;
@@ -3082,7 +3120,7 @@ int emqxgm_route_dests_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* 
 int emqxgm_subscribers_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
                              const uint32_t* sptr, const uint32_t* subs, uint32_t flags,
                              uint64_t* epoch) {
-  if (!h || !offsets || !sptr || (!bytes && n) || (flags & ~EMQXGM_SET_COMMIT)) return -EINVAL;
+  if (!h || !offsets || !sptr || (!bytes && n && offsets[n]) || (flags & ~EMQXGM_SET_COMMIT)) return -EINVAL;
   for (uint64_t i = 0; i < n; ++i)
     if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > 65535 || sptr[i + 1] < sptr[i] ||
         (sptr[i + 1] > sptr[i] && !subs))

@@ -1,30 +1,68 @@
-"""``emqx_trie_gpu_sync`` (src/emqx_trie_gpu_sync.erl) restated over the engine's C-ABI: the
-level-triggered mirror of a committed route table into the device index.
+"""``emqx_trie_gpu_sync`` and the writing node's hooks (src/emqx_trie_gpu_sync.erl,
+src/emqx_trie_gpu.erl) restated over the engine's C-ABI: the level-triggered mirror of the
+committed route table (and the local subscriber bag) into the device index.
 
 The reference keeps a route key while its filter has a route and a wildcard filter in the trie
 while it has one (emqx_router_utils.erl:34-39, 57-71).  The mirror follows that as a STATE:
 whatever event arrives for topic T -- a write, a delete_object, a delete of the key, in any
-number and order -- it reads the table as it is now and calls ``emqxgm_route_set(T,
-has_routes(T))``.  A full resync (at start and then periodically) is ``sync_begin``, every topic
-of the table set present, ``sync_end``, which removes the route keys the scan did not see.
-Events queued while a resync runs are handled after it, against the table as it is then.
+number and order -- it reads the table as it is now and sets T's dests on the device
+(``emqxgm_route_dests_batch``: the route key and the trie membership follow from them).
 
-``table`` is anything with ``has_routes(topic)`` and ``topics()`` -- ``oracle.emqx_ref.Router``
-in the tests (the route bag ``emqx_route``, emqx_router.erl:155-161, 186-188).  ``engines``: one
-or more engines holding the same index (the NIF's resource: one engine per GPU).
+* ``handle_events``: the queued events become ONE device call committed before it returns
+  (``EMQXGM_SET_COMMIT``) -- no tick; a full build running in the background is not waited for.
+* ``route_changed(T)`` / ``subscribers_changed(T)``: the writing node's hooks after
+  emqx_router:do_add_route/2, do_delete_route/2 and emqx_broker's subscribe / unsubscribe
+  (emqx_router.erl:124-138, 171-179; emqx_broker.erl:160-212): committed before they return, so
+  the node's next publish sees the change (emqx_broker.erl:163-168).
+* ``resync``: ``sync_begin``, every topic of the table in chunks of ``chunk`` distinct topics per
+  call, ``sync_end`` (removes every route key the scan did not see), then the subscriber lists.
+
+``table`` is anything with ``lookup_routes(topic)`` ([(topic, dest)]; a dest is a node name or a
+``(group, node)`` tuple) and ``topics()`` -- ``oracle.emqx_ref.Router`` in the tests (the route bag
+``emqx_route``, emqx_router.erl:155-161, 186-188).  ``subscribers``: topic -> local subscriber
+names (the ``emqx_subscriber`` bag), optional.  ``engines``: one or more engines holding the
+same index (the NIF's resource: one engine per GPU).
 """
 from __future__ import annotations
 
 from collections import deque
-from typing import Deque, Sequence, Tuple
+from typing import Deque, Dict, Hashable, List, Optional, Sequence, Tuple
+
+from .engine import NONE
+
+
+class Handles:
+    """The engine's 32-bit names of dests (nodes, groups) and subscribers (emqx_trie_gpu's
+    handles table; the NIF maps them back to terms)."""
+
+    def __init__(self):
+        self.ids: Dict[Tuple[str, Hashable], int] = {}
+        self.names: Dict[str, List[Hashable]] = {"node": [], "group": [], "sub": []}
+
+    def __call__(self, kind: str, name: Hashable) -> int:
+        k = (kind, name)
+        if k not in self.ids:
+            self.ids[k] = len(self.names[kind])
+            self.names[kind].append(name)
+        return self.ids[k]
+
+    def dest(self, d) -> Tuple[int, int]:
+        if isinstance(d, tuple):  # {Group, Node}
+            return self("node", d[1]), self("group", d[0])
+        return self("node", d), NONE
 
 
 class RouteTableMirror:
-    def __init__(self, engines: Sequence, table):
+    def __init__(self, engines: Sequence, table, subscribers: Optional[Dict] = None,
+                 local_node: Hashable = "n1", chunk: int = 65536):
         self.engines = list(engines)
         self.table = table
+        self.subscribers = subscribers
+        self.handles = Handles()
+        self.chunk = chunk
         self.queue: Deque[Tuple[str, bytes]] = deque()  # the process's mailbox of table events
-        self.dirty = False
+        for e in self.engines:
+            e.set_local_node(self.handles("node", local_node))
 
     # -- mnesia table events: {write, Route, _} / {delete_object, Route, _} / {delete, {Tab, T}, _}
     def event(self, kind: str, topic: bytes) -> None:
@@ -33,39 +71,52 @@ class RouteTableMirror:
         self.queue.append((kind, topic))
 
     def handle_events(self, limit: int = -1) -> int:
-        """Handles up to `limit` queued events (all: -1), as handle_info/2 does: each sets its
-        topic's membership from the table's CURRENT state."""
+        """Handles up to `limit` queued events (all: -1) as handle_info/2 + collect/2 do: one
+        batch, each topic's dests read from the table's CURRENT state, committed at once."""
+        topics = set()
         k = 0
         while self.queue and k != limit:
-            _kind, topic = self.queue.popleft()
-            self.set(topic)
+            topics.add(self.queue.popleft()[1])
             k += 1
+        if topics:
+            self.sync(sorted(topics))
         return k
 
-    def set(self, topic: bytes) -> None:
-        present = bool(self.table.has_routes(topic))
+    def items(self, topics) -> list:
+        return [(t, [self.handles.dest(d) for _, d in self.table.lookup_routes(t)]) for t in topics]
+
+    def sync(self, topics, commit: bool = True) -> None:
+        items = self.items(topics)
         for e in self.engines:
-            e.route_set(topic, present)
-        self.dirty = True
+            e.route_dests_batch(items, commit=commit)
+
+    # -- the writing node's hooks (src/emqx_trie_gpu.erl route_changed/1, subscribers_changed/1)
+    def route_changed(self, topic: bytes) -> None:
+        self.sync([topic])
+
+    def subscribers_changed(self, topic: bytes, commit: bool = True) -> None:
+        subs = [self.handles("sub", s) for s in (self.subscribers or {}).get(topic, [])]
+        for e in self.engines:
+            e.subscribers_batch([(topic, subs)], commit=commit)
 
     def resync(self) -> int:
-        """A full resync: every topic of the table set present, every other route key removed.
-        Returns how many route keys the sweep removed (engine 0's count)."""
+        """A full resync: every topic of the table in chunks, every other route key removed,
+        every subscriber list set.  Returns how many route keys the sweep removed."""
         gens = [e.sync_begin() for e in self.engines]
-        for t in self.table.topics():
-            for e in self.engines:
-                e.route_set(t, True)
+        topics = list(self.table.topics())
+        for i in range(0, len(topics), self.chunk):
+            self.sync(topics[i:i + self.chunk], commit=False)
         removed = [e.sync_end(g) for e, g in zip(self.engines, gens)]
-        self.dirty = True
+        for t in sorted(self.subscribers or {}):
+            self.subscribers_changed(t, commit=False)
         return removed[0] if removed else 0
 
     def commit(self) -> None:
         for e in self.engines:
             e.commit()
-        self.dirty = False
 
     def init(self) -> None:
-        """init/1: (subscribed first,) one full resync, then the first commit; the index is
-        published only after it."""
+        """handle_continue(open): (subscribed first,) one full resync, then the first commit;
+        the index is published only after it."""
         self.resync()
         self.commit()

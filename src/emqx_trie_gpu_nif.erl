@@ -5,8 +5,14 @@
 -module(emqx_trie_gpu_nif).
 
 -export([
-    open/5,
+    open/6,
+    route_sync/2,
     route_set/3,
+    route_set_many/3,
+    route_dests/3,
+    subscribers/3,
+    register/3,
+    set_local_node/2,
     sync_begin/1,
     sync_end/2,
     commit/1,
@@ -14,6 +20,7 @@
     trie_member/2,
     route_member/2,
     match_async/3,
+    publish_async/3,
     cancel/2,
     tune/3,
     stats/1
@@ -31,10 +38,24 @@ init() ->
 
 -define(NOT_LOADED, erlang:nif_error(nif_not_loaded)).
 
-%% open(Devices, WindowTopics, WindowBytes, WindowUs, MaxLevels) -> {ok, Res} | {error, Reason}
-open(_Devices, _WindowTopics, _WindowBytes, _WindowUs, _MaxLevels) -> ?NOT_LOADED.
-%% route_set(Res, Filter, Present :: boolean()) -> ok | {error, Reason}
+%% open(Devices, WindowTopics, WindowBytes, WindowUs, MaxLevels,
+%%      #{spin_us => N, bg_build => N, publish => boolean()}) -> {ok, Res} | {error, Reason}
+open(_Devices, _WindowTopics, _WindowBytes, _WindowUs, _MaxLevels, _Opts) -> ?NOT_LOADED.
+%% route_sync(Res, [{Filter, Present :: boolean()}]) -> {ok, Epoch}: set and committed (visible to
+%% every later publish) before it returns; never waits for a background full build
+route_sync(_Res, _Items) -> ?NOT_LOADED.
+%% route_set(Res, Filter, Present :: boolean()) -> ok | {error, Reason} (pending until commit/1)
 route_set(_Res, _Filter, _Present) -> ?NOT_LOADED.
+%% route_set_many(Res, [Filter], Present) -> ok | {error, Reason} (a resync chunk, pending)
+route_set_many(_Res, _Filters, _Present) -> ?NOT_LOADED.
+%% route_dests(Res, [{Filter, [{NodeH, GroupH | none}]}], Commit :: boolean()) -> {ok, Epoch}
+route_dests(_Res, _Items, _Commit) -> ?NOT_LOADED.
+%% subscribers(Res, [{Filter, [SubH]}], Commit :: boolean()) -> {ok, Epoch}
+subscribers(_Res, _Items, _Commit) -> ?NOT_LOADED.
+%% register(Res, node | group | sub, [{Handle, Term}]) -> ok
+register(_Res, _Kind, _Items) -> ?NOT_LOADED.
+%% set_local_node(Res, NodeH) -> ok
+set_local_node(_Res, _NodeH) -> ?NOT_LOADED.
 %% sync_begin(Res) -> {ok, Gen}
 sync_begin(_Res) -> ?NOT_LOADED.
 %% sync_end(Res, Gen) -> {ok, Removed}
@@ -44,10 +65,13 @@ commit(_Res) -> ?NOT_LOADED.
 empty(_Res) -> ?NOT_LOADED.
 trie_member(_Res, _Filter) -> ?NOT_LOADED.
 route_member(_Res, _Filter) -> ?NOT_LOADED.
-%% match_async(Res, Topic, Id) -> ok | {error, e2big | ebusy | eshutdown}; later the caller gets
-%% {emqx_trie_gpu, Id, [Filter] | {error, Reason}}
-match_async(_Res, _Topic, _Id) -> ?NOT_LOADED.
-%% cancel(Res, Id) -> true (never answered) | false (the answer is in the mailbox)
-cancel(_Res, _Id) -> ?NOT_LOADED.
+%% match_async(Res, Topic, Ref) -> {ok, Call} | {error, e2big | ebusy | eshutdown}; later the
+%% caller gets {emqx_trie_gpu, Ref, [Filter], ExactHit :: boolean()} | {emqx_trie_gpu, Ref, {error, R}}
+match_async(_Res, _Topic, _Ref) -> ?NOT_LOADED.
+%% publish_async(Res, Topic, Ref) -> {ok, Call} | {error, R}; later
+%% {emqx_trie_gpu, Ref, {routes, [{To, Node | Group}], [{To, SubPid}]}} | {emqx_trie_gpu, Ref, {error, R}}
+publish_async(_Res, _Topic, _Ref) -> ?NOT_LOADED.
+%% cancel(Res, Call) -> true (never answered) | false (the answer is in the mailbox)
+cancel(_Res, _Call) -> ?NOT_LOADED.
 tune(_Res, _Key, _Value) -> ?NOT_LOADED.
 stats(_Res) -> ?NOT_LOADED.

@@ -14,9 +14,17 @@
 %%   max_levels          -> emqxgm_async_cfg.max_levels: deeper topics take emqx_trie:match/1
 %%                          (the zone's mqtt.max_topic_levels, emqx_schema.erl:405-412)
 %%   delta_commit        -> emqxgm_tune(h, "delta_commit", never 0 | small 1 | always 2)
+%%   bg_build            -> emqxgm_tune(h, "bg_build"): full builds of registries of at least this
+%%                          many filters run in the background while commits patch the index
+%%   publish             -> a publish_async layer (EMQXGM_ASYNC_PUBLISH) for emqx_trie_gpu:route/2
+%%   spin_us             -> emqxgm_tune(h, "spin_us"): a completer thread polls a window's pass
+%%                          this long before it blocks (0: block at once -- no core taken from the
+%%                          schedulers; ADVICE r04)
 %%   timeout_ms          -> how long a publisher waits for the device before it cancels and takes
-%%                          emqx_trie:match/1
-%%   resync_interval_ms  -> period of emqx_trie_gpu_sync's full resync (emqxgm_route_sync_*)
+%%                          the reference's path
+%%   resync_interval_ms  -> period of emqx_trie_gpu_sync's full resync (emqxgm_route_sync_*);
+%%                          default 0 (none) on a core node, whose table events all arrive, and
+%%                          30000 on a replicant
 %% emqx_amd/config.py is the same table for the Python mirror (tests/test_config.py).
 %%--------------------------------------------------------------------
 -module(emqx_trie_gpu_schema).
@@ -35,6 +43,9 @@ fields("gpu_match") ->
         {"batch_window_us", hoconsc:mk(range(1, 1000000), #{default => 50})},
         {"max_levels", hoconsc:mk(range(1, 65535), #{default => 128})},
         {"delta_commit", hoconsc:mk(hoconsc:enum([never, small, always]), #{default => small})},
+        {"bg_build", hoconsc:mk(non_neg_integer(), #{default => 16384})},
+        {"publish", hoconsc:mk(boolean(), #{default => true})},
+        {"spin_us", hoconsc:mk(range(0, 1000000), #{default => 0})},
         {"timeout_ms", hoconsc:mk(range(1, 600000), #{default => 5000})},
-        {"resync_interval_ms", hoconsc:mk(range(100, 86400000), #{default => 30000})}
+        {"resync_interval_ms", hoconsc:mk(range(0, 86400000), #{required => false})}
     ].

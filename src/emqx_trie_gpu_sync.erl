@@ -1,35 +1,44 @@
 %%--------------------------------------------------------------------
-%% emqx_trie_gpu_sync -- mirrors one committed route table into its device index.
+%% emqx_trie_gpu_sync -- mirrors one committed table set into its device index.
 %%
-%% Index route   : the route table emqx_route (emqx_router.erl:72-92) -> emqx_trie's trie;
+%% Index route   : the route table emqx_route (emqx_router.erl:72-92) -> emqx_trie's trie, the
+%%                 route keys and every route's dests; the local subscriber bag emqx_subscriber
+%%                 (emqx_broker.erl:546-579) -> the fan-out's local dispatch lists;
 %% Index session : the session router's table (emqx_session_router.erl:64-65, 312-316) -> the
 %%                 session trie (emqx_trie.erl:117-119, 135-137, 151-153).
 %%
 %% emqx_trie:insert/delete run inside mria transactions that may abort and retry
 %% (emqx_router_utils.erl:74-135), so the device follows committed state only.  The mirror is
 %% LEVEL-triggered: whatever event arrives for a topic T, it reads the table as it is now and
-%% sets T's membership to match it (emqxgm_route_set: a route key while T has a route, a trie
-%% member while a wildcard T has one -- the rule of emqx_router_utils.erl:34-39, 57-71).  The
-%% number and order of events therefore never matter: two dests added before the first event is
-%% handled, paired deletes, events queued while init/1 scans the table, a restart -- each ends in
-%% the table's state.  Changes are committed (one atomic epoch swap) on a short tick; matches
-%% never wait for it.
+%% sets T's state on the device to it (its dests -- and with them the route key and, for a
+%% wildcard T, the trie membership: the rule of emqx_router_utils.erl:34-39, 57-71 as a state).
+%% The number and order of events therefore never matter.
 %%
-%% Full resyncs (init/1, then every resync_interval_ms): sync_begin, every topic of the table set
-%% present, sync_end -- which removes every route key the scan did not see.  Events that arrive
-%% during a scan are handled after it, against the table as it is then, so they win.  The
-%% periodic resync is what keeps a node that never sees the table's mnesia events in step: on a
-%% mria replicant the route shard is replayed from the core nodes' rlog (emqx_router.erl:78-92)
-%% and mnesia table events may not fire there, so such a node lags by at most one interval.
+%% Table events are handled in batches: every event queued when the process gets to them becomes
+%% one device call that is committed before it returns (emqxgm_route_dests_batch with
+%% EMQXGM_SET_COMMIT), with no tick.  It never waits for a full build: a build (the first one, or
+%% one the tables' load starts) runs in the background while these commits patch the index the
+%% publishers read.  The writing node's own changes do not wait for this process at all: its hooks
+%% (emqx_trie_gpu:route_changed/1, subscribers_changed/1) commit them before SUBACK.
+%%
+%% Full resyncs: at start (handle_continue, so the supervisor is not held) and, where table events
+%% may be missed -- a mria replicant, whose route shard is replayed from the core nodes' rlog
+%% (emqx_router.erl:78-92) -- every resync_interval_ms.  sync_begin, every topic of the table in
+%% chunks of ?CHUNK distinct topics per dirty NIF call, sync_end (removes every route key the
+%% scan did not see), commit.  Events that arrive during a scan are handled after it, against the
+%% table as it is then, so they win.
 %%--------------------------------------------------------------------
 -module(emqx_trie_gpu_sync).
 
 -behaviour(gen_server).
 
--export([start_link/1]).
--export([init/1, handle_call/3, handle_cast/2, handle_info/2]).
+-include_lib("emqx/include/emqx.hrl").
 
--define(TICK_MS, 2).
+-export([start_link/1, table/1, repair/1]).
+-export([init/1, handle_continue/2, handle_call/3, handle_cast/2, handle_info/2]).
+
+-define(CHUNK, 65536).       %% distinct topics per resync call
+-define(BATCH, 65536).       %% table events per device call
 -define(CONF(K, D), emqx_config:get([broker, perf, gpu_match, K], D)).
 
 start_link(Index) ->
@@ -47,97 +56,199 @@ table(session) ->
         ram -> emqx_session_route_ram
     end.
 
+%% a device call was refused (out of memory): resync
+repair(Index) ->
+    gen_server:cast(name(Index), resync).
+
 init(Index) ->
-    Tab = table(Index),
+    %% a restarted mirror: publishers take the reference's path until its resync is committed
+    %% (the handles table died with the old process)
+    ok = emqx_trie_gpu:publish(Index, undefined),
+    {ok, #{index => Index, h => undefined, tab => table(Index)}, {continue, open}}.
+
+handle_continue(open, S = #{index := Index, tab := Tab}) ->
     case open(Index) of
         {ok, H} ->
             {ok, _} = mnesia:subscribe({table, Tab, simple}),
-            ok = tune(H),
-            S = #{index => Index, h => H, tab => Tab, dirty => false},
-            ok = resync(S),
+            S1 = S#{h := H},
+            ok = prepare(Index, H),
+            ok = resync(S1),
             {ok, _Epoch} = emqx_trie_gpu_nif:commit(H),
             %% only now may publishers use it (before, they take the reference's path)
-            emqx_trie_gpu:publish(Index, H),
+            ok = emqx_trie_gpu:publish(Index, H),
             schedule_resync(),
-            {ok, S};
+            {noreply, S1};
         {error, Reason} ->
-            {stop, {gpu_match_open, Reason}}
+            {stop, {gpu_match_open, Reason}, S}
     end.
 
 %% a restart keeps the engines (and their index) it published: the resync repairs whatever
 %% changed meanwhile
 open(Index) ->
-    case emqx_trie_gpu:handle(Index) of
+    case persistent_term:get({emqx_trie_gpu, {engines, Index}}, undefined) of
         undefined ->
-            emqx_trie_gpu_nif:open(
-                ?CONF(devices, [0]),
-                ?CONF(batch_max, 65536),
-                64 * ?CONF(batch_max, 65536),
-                ?CONF(batch_window_us, 50),
-                ?CONF(max_levels, 128)
-            );
+            Opts = #{
+                spin_us => ?CONF(spin_us, 0),
+                bg_build => ?CONF(bg_build, 16384),
+                publish => Index =:= route andalso ?CONF(publish, true)
+            },
+            case
+                emqx_trie_gpu_nif:open(
+                    ?CONF(devices, [0]),
+                    ?CONF(batch_max, 65536),
+                    64 * ?CONF(batch_max, 65536),
+                    ?CONF(batch_window_us, 50),
+                    ?CONF(max_levels, 128),
+                    Opts
+                )
+            of
+                {ok, H} ->
+                    persistent_term:put({emqx_trie_gpu, {engines, Index}}, H),
+                    {ok, H};
+                Error ->
+                    Error
+            end;
         H ->
             {ok, H}
     end.
 
-tune(H) ->
+%% the engines' knobs; for the route index the handle registry (node(), the dest and subscriber
+%% handles made so far) -- from here on every new handle is registered as it is made
+prepare(Index, H) ->
     Delta =
         case ?CONF(delta_commit, small) of
             never -> 0;
             small -> 1;
             always -> 2
         end,
-    emqx_trie_gpu_nif:tune(H, delta_commit, Delta).
+    ok = emqx_trie_gpu_nif:tune(H, delta_commit, Delta),
+    case Index of
+        session ->
+            ok;
+        route ->
+            Tab = emqx_trie_gpu:handles_table(),
+            _ = ets:info(Tab, name) =:= undefined andalso
+                ets:new(Tab, [named_table, public, set, {read_concurrency, true}]),
+            ok = emqx_trie_gpu:publish(registry, H),
+            {NodeH, none} = hd(emqx_trie_gpu:dest_handles([node()])),
+            lists:foreach(
+                fun(Kind) ->
+                    Hs = ets:select(Tab, [{{{Kind, '$1'}, '$2'}, [], [{{'$2', '$1'}}]}]),
+                    ok = emqx_trie_gpu_nif:register(H, Kind, Hs)
+                end,
+                [node, group, sub]
+            ),
+            emqx_trie_gpu_nif:set_local_node(H, NodeH)
+    end.
 
 handle_call(_Req, _From, S) ->
     {reply, ignored, S}.
 
+handle_cast(resync, S) ->
+    ok = resync(S),
+    {ok, _} = emqx_trie_gpu_nif:commit(maps:get(h, S)),
+    {noreply, S};
 handle_cast(_Msg, S) ->
     {noreply, S}.
 
-%% simple table events: the record's first field is the topic, whatever its tag
-handle_info({mnesia_table_event, {write, Route, _}}, S) ->
-    {noreply, set(element(2, Route), S)};
-handle_info({mnesia_table_event, {delete_object, Route, _}}, S) ->
-    {noreply, set(element(2, Route), S)};
-handle_info({mnesia_table_event, {delete, {_Tab, Topic}, _}}, S) ->
-    {noreply, set(Topic, S)};
-handle_info(commit, S = #{h := H}) ->
-    {ok, _Epoch} = emqx_trie_gpu_nif:commit(H),
-    {noreply, S#{dirty := false}};
+%% simple table events: the record's first field is the topic, whatever its tag.  Every event
+%% queued now joins one batch.
+handle_info({mnesia_table_event, _} = E, S) ->
+    Topics = collect([event_topic(E)], ?BATCH),
+    {noreply, sync(Topics, S)};
 handle_info(resync, S) ->
     ok = resync(S),
+    {ok, _Epoch} = emqx_trie_gpu_nif:commit(maps:get(h, S)),
     schedule_resync(),
-    {noreply, tick(S)};
+    {noreply, S};
 handle_info(_Info, S) ->
     {noreply, S}.
 
-%% T's membership := whether the table holds a route for T now
-set(Topic, S = #{h := H, tab := Tab}) ->
-    case emqx_trie_gpu_nif:route_set(H, Topic, ets:member(Tab, Topic)) of
-        ok ->
-            tick(S);
-        {error, _} ->
-            %% the engine refused (out of memory): a full resync retries every key
-            self() ! resync,
-            S
+event_topic({mnesia_table_event, {write, Route, _}}) -> element(2, Route);
+event_topic({mnesia_table_event, {delete_object, Route, _}}) -> element(2, Route);
+event_topic({mnesia_table_event, {delete, {_Tab, Topic}, _}}) -> Topic.
+
+collect(Acc, 0) ->
+    lists:usort(Acc);
+collect(Acc, N) ->
+    receive
+        {mnesia_table_event, _} = E -> collect([event_topic(E) | Acc], N - 1)
+    after 0 -> lists:usort(Acc)
     end.
 
-resync(#{h := H, tab := Tab}) ->
+%% the topics' state := the table's now, committed before the call returns
+sync(Topics, S = #{index := route, h := H, tab := Tab}) ->
+    check(emqx_trie_gpu_nif:route_dests(H, emqx_trie_gpu:route_items(Tab, Topics), true), S);
+sync(Topics, S = #{index := session, h := H, tab := Tab}) ->
+    check(emqx_trie_gpu_nif:route_sync(H, [{T, ets:member(Tab, T)} || T <- Topics]), S).
+
+check({ok, _Epoch}, S) ->
+    S;
+check({error, _}, S) ->
+    %% the engine refused (out of memory): a full resync retries every key
+    gen_server:cast(self(), resync),
+    S.
+
+%% every topic of the table (and for the route index every local subscriber list), in chunks of
+%% ?CHUNK distinct topics per dirty NIF call; then every route key the scan did not see goes.
+%% A bag's rows of one key come together in the scan: the key is read once, with all its rows.
+resync(#{index := Index, h := H, tab := Tab}) ->
     {ok, Gen} = emqx_trie_gpu_nif:sync_begin(H),
-    ets:foldl(
-        fun(Route, ok) -> emqx_trie_gpu_nif:route_set(H, element(2, Route), true) end,
-        ok,
+    Flush = fun(Topics) -> flush(Index, H, Tab, Topics) end,
+    {_, Last, _} = ets:foldl(
+        fun(Row, {Prev, Acc, N}) ->
+            case element(2, Row) of
+                Prev ->
+                    {Prev, Acc, N};
+                T when N + 1 >= ?CHUNK ->
+                    ok = Flush([T | Acc]),
+                    {T, [], 0};
+                T ->
+                    {T, [T | Acc], N + 1}
+            end
+        end,
+        {undefined, [], 0},
         Tab
     ),
+    ok = Flush(Last),
     {ok, _Removed} = emqx_trie_gpu_nif:sync_end(H, Gen),
-    ok.
+    case Index of
+        route -> resync_subscribers(H);
+        session -> ok
+    end.
 
+flush(_Index, _H, _Tab, []) ->
+    ok;
+flush(route, H, Tab, Topics) ->
+    {ok, _} = emqx_trie_gpu_nif:route_dests(H, emqx_trie_gpu:route_items(Tab, Topics), false),
+    ok;
+flush(session, H, _Tab, Topics) ->
+    emqx_trie_gpu_nif:route_set_many(H, Topics, true).
+
+%% the local subscriber bag: every topic's list (its shard rows expanded)
+resync_subscribers(H) ->
+    Topics = lists:usort([T || {T, _} <- ets:tab2list(emqx_subscriber), is_binary(T)]),
+    lists:foreach(
+        fun(Chunk) ->
+            {ok, _} = emqx_trie_gpu_nif:subscribers(H, emqx_trie_gpu:subscriber_items(Chunk), false)
+        end,
+        chunks(Topics, ?CHUNK)
+    ).
+
+chunks([], _N) -> [];
+chunks(L, N) when length(L) =< N -> [L];
+chunks(L, N) ->
+    {A, B} = lists:split(N, L),
+    [A | chunks(B, N)].
+
+%% periodic resyncs only where table events may be missed (a replicant), unless configured
 schedule_resync() ->
-    erlang:send_after(?CONF(resync_interval_ms, 30000), self(), resync).
-
-tick(S = #{dirty := true}) ->
-    S;
-tick(S) ->
-    erlang:send_after(?TICK_MS, self(), commit),
-    S#{dirty := true}.
+    Default =
+        case mria_rlog:role() of
+            replicant -> 30000;
+            core -> 0
+        end,
+    case ?CONF(resync_interval_ms, Default) of
+        0 -> ok;
+        Ms -> _ = erlang:send_after(Ms, self(), resync), ok
+    end.

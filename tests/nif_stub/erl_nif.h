@@ -42,3 +42,13 @@ int enif_get_uint64(ErlNifEnv*, ERL_NIF_TERM, ErlNifUInt64*); int enif_get_int64
 int enif_is_list(ErlNifEnv*, ERL_NIF_TERM); ERL_NIF_TERM enif_make_list_from_array(ErlNifEnv*, const ERL_NIF_TERM*, unsigned);
 ERL_NIF_TERM enif_make_double(ErlNifEnv*, double);
 void* enif_alloc(size_t); void enif_free(void*);
+int enif_keep_resource(void*); ERL_NIF_TERM enif_make_copy(ErlNifEnv*, ERL_NIF_TERM);
+int enif_is_ref(ErlNifEnv*, ERL_NIF_TERM); int enif_is_atom(ErlNifEnv*, ERL_NIF_TERM);
+int enif_is_identical(ERL_NIF_TERM, ERL_NIF_TERM);
+int enif_get_tuple(ErlNifEnv*, ERL_NIF_TERM, int*, const ERL_NIF_TERM**);
+int enif_get_map_value(ErlNifEnv*, ERL_NIF_TERM, ERL_NIF_TERM, ERL_NIF_TERM*);
+typedef struct ErlNifRWLock ErlNifRWLock;
+ErlNifRWLock* enif_rwlock_create(char*); void enif_rwlock_destroy(ErlNifRWLock*);
+void enif_rwlock_rlock(ErlNifRWLock*); void enif_rwlock_runlock(ErlNifRWLock*);
+void enif_rwlock_rwlock(ErlNifRWLock*); void enif_rwlock_rwunlock(ErlNifRWLock*);
+void* enif_realloc(void*, size_t);

@@ -11,8 +11,8 @@ def test_defaults_map_onto_the_engine():
     assert c.engine_kwargs() == [{"device": 0, "batch_max": 65536}]
     assert c.async_kwargs() == {"window_topics": 65536, "window_bytes": 64 * 65536,
                                 "window_us": 50, "max_levels": 128}
-    assert c.timeout_ms == 5000 and c.resync_interval_ms == 30000
-    assert c.tunes() == {"delta_commit": 1}
+    assert c.timeout_ms == 5000 and c.resync_ms("core") == 0 and c.resync_ms("replicant") == 30000
+    assert c.tunes() == {"delta_commit": 1, "bg_build": 16384, "spin_us": 0} and c.publish
 
 
 def test_values_and_ranges():
@@ -23,7 +23,8 @@ def test_values_and_ranges():
     for bad in ({"batch_max": 0}, {"batch_max": 5 << 20}, {"batch_window_us": 0},
                 {"max_levels": 0}, {"devices": []}, {"devices": [-1]}, {"enable": 1},
                 {"delta_commit": "sometimes"}, {"batch_size": 3}, {"batch_max": True},
-                {"timeout_ms": 0}, {"resync_interval_ms": 10}):
+                {"timeout_ms": 0}, {"resync_interval_ms": -1}, {"spin_us": -1},
+                {"publish": 1}, {"bg_build": -5}):
         with pytest.raises(ValueError):
             GpuMatchConfig.from_map(bad)
 

@@ -88,7 +88,8 @@ def test_subscribe_visible_on_the_next_match(emqx):
         # the route key itself: an exact hit exactly while present (match_routes of the name)
         assert (int(res.exact_id[3]) != 0xFFFFFFFF) == present, (f, present)
     st = eng.stats()
-    assert st["delta_commits"] >= 200 and st["bg_waits"] == 0
+    # (a subscribe of a filter the cfg1 index already routes changes nothing: no commit)
+    assert st["delta_commits"] >= 100 and len(lat) >= 150 and st["bg_waits"] == 0
     print(f"subscribe + commit: p50 {np.median(lat) * 1e6:.0f} us, p99 "
           f"{np.percentile(lat, 99) * 1e6:.0f} us over {len(lat)}")
     eng.close()
@@ -103,7 +104,9 @@ def test_subscribe_visible_while_a_1m_filter_build_runs(emqx):
     w = workloads.generate(2, 1_000_000, 20_000)
     eng = emqx.Engine()
     eng.tune("bg_build", 1)
-    base = [b"zz/b%d/+" % i for i in range(500)]
+    # (the index readers have until the install takes the subscribes as delta patches: sized for
+    # 20k filters, its tables hold the ~4k nodes of 2000 more)
+    base = [b"zz/b%d/+" % i for i in range(20000)]
     eng.route_set_batch([(f, True) for f in base])
     eng.route_set_many(w.fbytes, w.foff, True)  # the bulk: pending, committed on another thread
     eng.tune("bg_delay_ms", 1500)
@@ -136,7 +139,7 @@ def test_subscribe_visible_while_a_1m_filter_build_runs(emqx):
         lat.append(time.perf_counter() - t0)
         mine.append(f)
         trie.insert(f)
-        topics = [_instantiate(f, rng), b"zz/b%d/q" % rng.integers(0, 500)]
+        topics = [_instantiate(f, rng), b"zz/b%d/q" % rng.integers(0, 20000)]
         res = eng.match(topics)
         for i, t in enumerate(topics):
             assert _row(eng, res, i) == sorted(trie.match(t)), (f, t)
