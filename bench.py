@@ -65,12 +65,17 @@ def main():
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="emqxgm_tune before the index is built (A/B runs), e.g. fat_buckets=0")
     ap.add_argument("--filter-shard", action="store_true",
-                    help="N>1: also measure the filter-sharded layout beside the replicas (its "
-                         "RCCL branch has run under gloo only, so the default N>1 run -- the "
-                         "scaling measurement -- leaves it out; --shard filters makes it the "
-                         "headline)")
+                    help="(default since r05) N>1: the filter-sharded layout is measured beside "
+                         "the replicas, after their figure is final, under a watchdog")
+    ap.add_argument("--no-filter-shard", action="store_true",
+                    help="N>1: leave the filter-sharded layout out")
+    ap.add_argument("--filter-shard-timeout", type=float, default=240.0,
+                    help="N>1: seconds the filter-sharded run may take before the watchdog prints "
+                         "the line with config.filter_sharded = {error: timeout} and ends the rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-in/host-out timing")
+    ap.add_argument("--no-subscribe", action="store_true",
+                    help="skip the subscribe-to-visible latency (idle and during a background rebuild)")
     ap.add_argument("--windows", default="16384,65536,262144,1048576",
                     help="NIF batcher window sizes (topics) for the operating-point sweep "
                          "('' = skip); rank 0, N=1, with the host-in/host-out timing")
@@ -237,7 +242,7 @@ def main():
     # N > 1: the north-star layout beside the replicas, on the same ranks (filters split by hash,
     # rank 0's batch broadcast, results gathered and merged on rank 0 every step)
     fsh = None
-    if world > 1 and (args.shard == "filters" or args.filter_shard):
+    if world > 1 and args.shard == "filters":  # the north-star layout as the headline
         fsh = _filter_sharded_run(Engine, D, args, w, dbat, rank, world, dev, local)
     # kernel timing with HIP events on the engine's stream, in extra passes after the timed
     # region (the events themselves add gaps between launches), one pass at a time so that a
@@ -341,6 +346,11 @@ def main():
         from emqx_amd.engine import Batcher
         windows = _window_sweep(Batcher, eng, w, [int(x) for x in args.windows.split(",")])
 
+    subscribe = None
+    if rank == 0 and world == 1 and not args.no_subscribe:
+        subscribe = _subscribe_latency(eng, w)
+
+    line = None
     if rank == 0:
         line = {
             "metric": ("published topics matched/sec at 10M filters" if args.cfg == 3
@@ -390,10 +400,48 @@ def main():
             "end_to_end": e2e,
             "nif_windows": windows,
             "nif_concurrent": nif,
+            "subscribe": subscribe,
         }
+    if world > 1 and args.shard == "topics" and not args.no_filter_shard:
+        # the north-star layout beside the replicas (filters split by hash, rank 0's
+        # batch broadcast over RCCL, results gathered and merged on rank 0), measured after the
+        # replicas' figure is final and under a watchdog: a hang or an error of its collectives
+        # is recorded in config.filter_sharded instead of losing the line
+        fsh = _guarded(lambda: _filter_sharded_run(Engine, D, args, w, dbat, rank, world, dev, local),
+                       args.filter_shard_timeout, rank, line)
+        if rank == 0:
+            line["config"]["filter_sharded"] = fsh
+    if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _guarded(run, timeout_s, rank, line):
+    """run() under a watchdog thread: past timeout_s the rank ends itself (rank 0 first prints
+    the line with the timeout recorded), so a collective that never completes cannot take the
+    measurement with it; an exception is recorded as the result."""
+    import threading
+    done = threading.Event()
+
+    def watchdog():
+        if done.wait(timeout_s):
+            return
+        if rank == 0:
+            line["config"]["filter_sharded"] = {"error": f"timeout after {timeout_s:.0f} s"}
+            print(json.dumps(line), flush=True)
+        log(f"[rank {rank}] filter-sharded run timed out after {timeout_s:.0f} s: exiting")
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
+    threading.Thread(target=watchdog, daemon=True).start()
+    try:
+        r = run()
+    except Exception as e:  # a collective's error: recorded, the replicas' line stands
+        log(f"[rank {rank}] filter-sharded run failed: {e!r}")
+        r = {"error": repr(e)[:500]}
+    done.set()
+    return r
 
 
 def _build_engine(Engine, w, idx, args, local):
@@ -528,6 +576,65 @@ def _nif_concurrent(eng, w, spec):
                        "latency = call -> its report (the NIF's term building and enif_send "
                        "excluded)")
     return out
+
+
+def _subscribe_latency(eng, w, n_idle=400, max_build_s=30.0):
+    """The writing node's subscribe path (emqxgm_route_set_batch with EMQXGM_SET_COMMIT: the hook
+    after emqx_router:do_add_route/2, emqx_router.erl:124-138): the time from the call to the
+    new filter being visible to every later match, on the bench's index -- idle, and while a full
+    rebuild of the whole index runs in the background (emqxgm_tune "rebuild").  Each subscribe is
+    followed by a one-topic match that must contain it (the check is not timed); everything is
+    unsubscribed again afterwards."""
+    def pcts(v):
+        v = np.asarray(v) * 1e6
+        return {"n": int(v.size), "p50_us": round(float(np.percentile(v, 50)), 1),
+                "p99_us": round(float(np.percentile(v, 99)), 1),
+                "max_us": round(float(v.max()), 1)} if v.size else {"n": 0}
+
+    base = w.topic(0).split(b"/")
+
+    def filt(k):  # a new wildcard filter under an existing prefix: site/S/device/D/bench{k}/+
+        return b"/".join(base[:4] + [b"bench%d" % k, b"+"])
+
+    def topic(k):
+        return b"/".join(base[:4] + [b"bench%d" % k, b"7"])
+
+    def sub(k, present, lat):
+        t0 = time.perf_counter()
+        eng.route_set_batch([(filt(k), present)])
+        lat.append(time.perf_counter() - t0)
+        row = eng.match([topic(k)]).row(0)
+        got = {eng.filter_bytes(int(f)) for f in row}
+        assert (filt(k) in got) == present, ("subscribe not visible", k, present)
+
+    idle = []
+    for k in range(n_idle):
+        sub(k, True, idle)
+    for k in range(n_idle):
+        sub(k, False, [])
+    s0 = eng.stats()
+    during, build = [], None
+    try:
+        eng.tune("rebuild", 1)
+    except Exception as e:  # (bg builds off for this index size)
+        return {"idle": pcts(idle), "during_rebuild": None, "note": str(e)}
+    t0 = time.perf_counter()
+    k = n_idle
+    while eng.stats()["full_commits"] == s0["full_commits"] and time.perf_counter() - t0 < max_build_s:
+        if len(during) < 4000:
+            sub(k, True, during)
+            k += 1
+        time.sleep(0.001)  # a subscribe every ~1 ms while the build runs
+    build = time.perf_counter() - t0
+    s1 = eng.stats()
+    for j in range(n_idle, k):
+        sub(j, False, [])
+    return {"api": "emqxgm_route_set_batch(.., EMQXGM_SET_COMMIT) then a one-topic match sees it",
+            "idle": pcts(idle),
+            "during_rebuild": dict(pcts(during), rebuild_s=round(build, 2),
+                                   build_ms=round(s1["last_build_ms"], 1),
+                                   waited_for_build=int(s1["bg_waits"] - s0["bg_waits"]),
+                                   catchup_changes=int(s1["catchup_changes"]))}
 
 
 def _census_mean(eng, dbat, nt):
@@ -791,7 +898,9 @@ def _roofline(nt, nbytes, census, pmc, tok_ms, exact_ms, walk_ms, pipe_ms, exact
                                "frac_mixed_ceiling": round(model / sec, 4),
                                "source": p.get("source")}
         if p.get("duration_us") is not None:
-            out["rocprof_avg_us"] = p.get("duration_us")
+            # the PMC run's kernel average over the default (pipelined) command: walks beside the
+            # other pass's kernels at three workgroups per CU, not the one-pass time used above
+            out["rocprof_pipelined_avg_us"] = p.get("duration_us")
     out["kernels_ms"] = {"k_tok": round(tok_ms, 4), "k_exact": round(exact_ms, 4),
                          "k_walk": round(walk_ms, 4), "verify+scan+scatter": round(post, 4),
                          "pass": round(pipe_ms, 4)}

@@ -943,7 +943,9 @@ void commit_stats(emqxgm* h, double ms, bool delta) {
   h->st.n_nodes = m.n_edges + 1;
   h->st.n_edges = m.n_edges;
   h->st.edge_slots = m.ecap;
-  h->st.keyed_nodes = (uint64_t)std::count(m.keyed.begin(), m.keyed.end(), (uint8_t)1);
+  // keyed flags are chosen by full builds only (a delta's new nodes are never keyed); counting
+  // them is O(nodes), 2 ms at cfg3, so a delta commit keeps the count
+  if (!delta) h->st.keyed_nodes = (uint64_t)std::count(m.keyed.begin(), m.keyed.end(), (uint8_t)1);
   h->st.exact_slots = (m.xcap_p + m.xcap_w) * XBUCKET;
   h->st.max_depth = m.max_depth;
   h->st.device_bytes = m.ecap * SLOT_U4 * 16 + (m.xcap_p + m.xcap_w) * XBUCKET * XENT_U4 * 16 + m.tn_cap * 4 +
@@ -959,7 +961,7 @@ void commit_stats(emqxgm* h, double ms, bool delta) {
 // waiting for either gets in first -- a subscribe waits for at most one slice, never for the
 // build.  (A filter's bytes, offset and length never change once registered; its membership
 // flags only change under the registry lock held exclusively.)
-constexpr uint64_t REG_SLICE = 8192;
+constexpr uint64_t REG_SLICE = 1024;
 template <class F>
 void for_slices(emqxgm* h, bool bg, uint64_t n, F f) {
   for (uint64_t i0 = 0; i0 < n; i0 += REG_SLICE) {
@@ -1826,7 +1828,7 @@ bool nearly_full(const emqxgm* h) {
   return m.fv_words0 && fvw * 2 > m.fv_cap + m.fv_words0;
 }
 
-int install_build(emqxgm* h);
+int install_build(emqxgm* h, std::unique_ptr<BuildJob>& spent);
 
 // The background build's thread: build the model and upload its tables without the writer lock
 // (for_slices lets writers in between slices), then install it under the lock.
@@ -1838,10 +1840,25 @@ void build_thread(emqxgm* h, BuildJob* J) {
   J->rc = rc;
   J->build_ms = ms_since(J->t0);
   if (const uint32_t d = h->bg_delay_ms.load()) std::this_thread::sleep_for(std::chrono::milliseconds(d));
-  std::lock_guard<std::mutex> g(h->wmu);
-  h->build_rc = install_build(h);
-  h->builds_done += 1;
-  h->bcv.notify_all();
+  std::unique_ptr<BuildJob> spent;
+  {
+    std::lock_guard<std::mutex> g(h->wmu);
+    h->build_rc = install_build(h, spent);
+    h->builds_done += 1;
+    h->bcv.notify_all();
+  }
+  // The replaced host model (tens of millions of entries at cfg3) is freed here, without the
+  // writer lock, and so are the replaced device tables once the passes that read them are done
+  // -- not by the next subscribe's commit (sweep_graveyard takes only the epoch lock).
+  spent.reset();
+  for (int i = 0; i < 2000; ++i) {
+    sweep_graveyard(h);
+    {
+      std::lock_guard<std::mutex> g(h->emu);
+      if (h->graveyard.empty()) break;
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  }
 }
 
 // Starts a background full build of the registry as it is now (wmu held): the changes pending now
@@ -1886,8 +1903,9 @@ int wait_build(emqxgm* h, std::unique_lock<std::mutex>& lk) {
 // meanwhile and whatever is pending) are replayed onto its model as one delta against the
 // membership it read, and the result is published.  A failed build, or a catch-up too large for
 // a delta, ends in a blocking full build.
-int install_build(emqxgm* h) {
-  std::unique_ptr<BuildJob> J = std::move(h->job);
+int install_build(emqxgm* h, std::unique_ptr<BuildJob>& spent) {
+  spent = std::move(h->job);
+  BuildJob* J = spent.get();
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<uint32_t> ch = std::move(h->build_log);
   h->build_log.clear();
@@ -1900,7 +1918,7 @@ int install_build(emqxgm* h) {
   }
   if (rc == 0) {
     J->m.valid = true;
-    h->tm = std::move(J->m);
+    std::swap(h->tm, J->m);  // J->m: the replaced model, freed by the caller after the lock
     h->o_tab = std::move(J->o);
     h->o_fv.reset();
     set_tables(h->ix, J->nx);
@@ -3048,12 +3066,33 @@ int emqxgm_commit(emqxgm_t* h, uint64_t* epoch) {
   return rc;
 }
 
+// The commit of a synchronous set (EMQXGM_SET_COMMIT): a delta of this call's own changes (those
+// appended to h->changed since c0); changes other callers left pending stay pending -- they are
+// not this caller's to publish, and a bulk of them (a resync's chunks) must not make a single
+// subscribe wait for its full build.  When this delta does not fit, everything pending takes the
+// usual path (commit_locked).
+static int commit_mine(emqxgm* h, std::unique_lock<std::mutex>& lk, size_t c0) {
+  if (c0 == 0) return commit_locked(h, &lk, false);
+  std::vector<uint32_t> rest(h->changed.begin(), h->changed.begin() + c0);
+  h->changed.erase(h->changed.begin(), h->changed.begin() + c0);
+  int rc = try_delta(h, std::chrono::steady_clock::now());
+  if (rc == 0) {
+    h->changed.swap(rest);
+    h->dirty = true;
+    return 0;
+  }
+  h->changed.insert(h->changed.end(), rest.begin(), rest.end());
+  h->dirty = true;
+  return rc < 0 ? rc : commit_locked(h, &lk, false);
+}
+
 int emqxgm_route_set_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets,
                            const uint8_t* present, uint64_t n, uint32_t flags, uint64_t* epoch) {
   if (!h || !offsets || (!bytes && n && offsets[n]) || (flags & ~EMQXGM_SET_COMMIT)) return -EINVAL;
   for (uint64_t i = 0; i < n; ++i)
     if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > 65535) return -EINVAL;
   std::unique_lock<std::mutex> lk(h->wmu);
+  const size_t c0 = h->changed.size();  // changes pending from other callers
   {
     std::unique_lock<std::shared_mutex> g(h->pmu);
     for (uint64_t i = 0; i < n; ++i) {
@@ -3066,7 +3105,7 @@ int emqxgm_route_set_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* of
     }
   }
   int rc = 0;
-  if (flags & EMQXGM_SET_COMMIT) rc = commit_locked(h, &lk, false);
+  if (flags & EMQXGM_SET_COMMIT) rc = commit_mine(h, lk, c0);
   if (epoch) *epoch = h->epoch;
   return rc;
 }
@@ -3083,6 +3122,7 @@ int emqxgm_route_dests_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* 
         return -EINVAL;
   }
   std::unique_lock<std::mutex> lk(h->wmu);
+  const size_t c0 = h->changed.size();  // changes pending from other callers
   {
     std::unique_lock<std::shared_mutex> g(h->pmu);
     std::vector<std::pair<uint32_t, uint32_t>> ds;
@@ -3112,7 +3152,7 @@ int emqxgm_route_dests_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* 
     }
   }
   int rc = 0;
-  if (flags & EMQXGM_SET_COMMIT) rc = commit_locked(h, &lk, false);
+  if (flags & EMQXGM_SET_COMMIT) rc = commit_mine(h, lk, c0);
   if (epoch) *epoch = h->epoch;
   return rc;
 }
@@ -3126,6 +3166,7 @@ int emqxgm_subscribers_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* 
         (sptr[i + 1] > sptr[i] && !subs))
       return -EINVAL;
   std::unique_lock<std::mutex> lk(h->wmu);
+  const size_t c0 = h->changed.size();  // changes pending from other callers
   {
     std::unique_lock<std::shared_mutex> g(h->pmu);
     std::vector<uint32_t> ss;
@@ -3152,7 +3193,7 @@ int emqxgm_subscribers_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* 
     }
   }
   int rc = 0;
-  if (flags & EMQXGM_SET_COMMIT) rc = commit_locked(h, &lk, false);
+  if (flags & EMQXGM_SET_COMMIT) rc = commit_mine(h, lk, c0);
   if (epoch) *epoch = h->epoch;
   return rc;
 }

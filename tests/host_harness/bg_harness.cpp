@@ -268,6 +268,35 @@ int main(int argc, char** argv) {
   }
   for (int i = 0; i < 100; ++i) V.check(word() + "/" + word(), "C random");
 
+  // ---- D: another caller's bulk left pending (a resync's chunks, not committed yet): a single
+  // subscribe commits its own change alone -- no build, no wait -- and the bulk stays pending
+  // until its own commit ----
+  {
+    emqxgm_get_stats(h, &st);
+    const uint64_t builds0 = st.bg_builds, waits0 = st.bg_waits, full0 = st.full_commits;
+    std::vector<std::string> pend;
+    bb.clear();
+    bo.assign(1, 0);
+    for (uint32_t i = 0; i < nmore; ++i) {
+      pend.push_back(filter());
+      bb += pend.back();
+      bo.push_back(bb.size());
+    }
+    CHECK(emqxgm_route_set_many(h, (const uint8_t*)bb.data(), bo.data(), nmore, 1) == 0, "set_many");
+    for (int i = 0; i < 40; ++i) {
+      const std::string f = filter();
+      set1(f, true);
+      V.check(topic_for(f), "D subscribe beside a pending bulk");
+      V.check(topic_for(pend[rnd(pend.size())]), "D pending bulk not visible");
+    }
+    emqxgm_get_stats(h, &st);
+    CHECK(st.bg_builds == builds0 && st.bg_waits == waits0 && st.full_commits == full0,
+          "D: a single subscribe built or waited");
+    CHECK(emqxgm_commit(h, nullptr) == 0, "commit");
+    for (const auto& f : pend) V.vis.insert(f);
+    for (int i = 0; i < 100; ++i) V.check(topic_for(pend[rnd(pend.size())]), "D bulk after its commit");
+  }
+
   std::vector<double> s = lat_a;
   std::sort(s.begin(), s.end());
   const double p50 = s[s.size() / 2], p99 = s[std::min(s.size() - 1, s.size() * 99 / 100)];

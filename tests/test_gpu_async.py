@@ -300,6 +300,13 @@ def test_async_copy_through_long_and_odd_topics(emqx):
         assert am.wait([(i, owner) for i in range(len(topics))], timeout=60)
         return {i: sorted(am.results[(i, owner)].filters) for i in range(len(topics))}
 
+    # the oracle (emqx_trie:match, oracle.emqx_ref) over the same filters: the copy-through
+    # path's answers are pinned to the reference restatement, not only to the host API's
+    trie = R.Trie()
+    for i in range(w.nf):
+        f = w.filter(i)
+        if R.wildcard(f):
+            trie.insert(f)
     for zc in (65536, 0):
         eng.tune("zc_topics", zc)
         am = emqx.AsyncMatcher([eng], window_topics=256, window_bytes=1 << 20, window_us=200,
@@ -310,4 +317,103 @@ def test_async_copy_through_long_and_odd_topics(emqx):
             ids = want.row(i)
             exp = sorted(flt.setdefault(int(f), eng.filter_bytes(int(f))) for f in ids)
             assert got[i] == exp, (zc, i, topics[i][:80])
+            assert got[i] == sorted(trie.match(topics[i])), (zc, i, topics[i][:80])
     eng.tune("zc_topics", 65536)
+
+
+def test_async_single_long_topic_on_an_idle_layer(emqx):
+    """a topic longer than a staging chunk (4 KB) goes into the open window
+    on its own; on an idle layer the flusher must arm its window_us timer for it, so the call is
+    answered within about window_us plus one pass -- not after the caller's 5 s timeout."""
+    w, (eng,) = _cfg1(emqx, nt=10)
+    trie = R.Trie()
+    for i in range(w.nf):
+        f = w.filter(i)
+        if R.wildcard(f):
+            trie.insert(f)
+    am = emqx.AsyncMatcher([eng], window_topics=256, window_bytes=1 << 20, window_us=200)
+    time.sleep(0.05)  # idle: the flusher sleeps with nothing pending
+    for k, t in enumerate([w.topic(0) + b"/" + b"q" * 9000, b"l0w1/" + b"z" * 5000]):
+        t0 = time.perf_counter()
+        assert am.match(t, k, owner=1) == 0
+        assert am.wait([(k, 1)], timeout=2.0), "a lone long topic was never submitted"
+        dt = time.perf_counter() - t0
+        assert dt < 0.05, dt
+        assert sorted(am.results[(k, 1)].filters) == sorted(trie.match(t))
+        time.sleep(0.05)
+    am.close()
+
+
+def test_async_publish_layer_every_call(emqx):
+    """The publish layer (EMQXGM_ASYNC_PUBLISH: the NIF's publish_async/3, emqx_trie_gpu:route/2)
+    from 16 threads, one topic a call: every call's aggre/1 entries and local dispatches equal
+    oracle.emqx_ref.publish (emqx_broker.erl:218-300, 326-355) for its topic.  The broker state
+    reaches the engine through the level-triggered mirror (route dests and subscriber lists)."""
+    import threading
+    import workloads
+    from emqx_amd.mirror import RouteTableMirror
+    w = workloads.generate(1, 4000, 12_000)
+    rng = random.Random(3)
+    rt, subs = R.Router(), {}
+    dests = ["n1", "n2", "n3", ("g1", "n1"), ("g2", "n2"), ("g1", "n3")]
+    names = [w.filter(i) for i in range(w.nf)]
+    for f in names:
+        for d in rng.sample(dests, rng.randint(1, 3)):
+            rt.add_route(f, d)
+        if rng.random() < 0.6:
+            subs[f] = sorted({f"s{rng.randint(0, 40)}" for _ in range(rng.randint(1, 3))})
+    for i in range(0, 12_000, 5):  # exact route keys: some topics are routed by their own name
+        t = w.topic(i)
+        rt.add_route(t, rng.choice(dests))
+        subs.setdefault(t, ["x%d" % (i % 7)])
+    eng = emqx.Engine()
+    m = RouteTableMirror([eng], rt, subscribers=subs, local_node="n1")
+    m.init()
+    am = emqx.AsyncMatcher([eng], window_topics=4096, window_us=100, publish=True)
+    topics = [w.topic(i) for i in range(w.nt)] + names[:200] + [b"", b"l0w1/+"]
+    errors = []
+
+    def publisher(k):
+        try:
+            for i in range(k, len(topics), 16):
+                while True:
+                    rc = am.match(topics[i], i, owner=k + 1)
+                    if rc != -16:
+                        break
+                    time.sleep(0.0002)
+                assert rc == 0, rc
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+    ths = [threading.Thread(target=publisher, args=(k,)) for k in range(16)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors
+    keys = [(i, i % 16 + 1) for i in range(len(topics))]
+    assert am.wait(keys, timeout=120)
+    H = m.handles.names
+
+    def check(r, t):
+        assert r.status == 0
+        got_e = sorted(((to, H["group"][d & ~emqx.engine.DEST_GROUP] if d & emqx.engine.DEST_GROUP
+                         else H["node"][d]) for to, d in r.routes), key=repr)
+        got_d = sorted(((to, H["sub"][s]) for to, s in r.deliveries), key=repr)
+        want_e, want_d = R.publish(rt, t, "n1", subs)
+        assert got_e == sorted(want_e, key=repr), t
+        assert got_d == sorted(want_d, key=repr), t
+        return got_e, got_d
+    for i, t in enumerate(topics):
+        check(am.results[keys[i]], t)
+    am.close()
+    # the writing node's hooks: a new route + subscriber, visible on the very next publish
+    am = emqx.AsyncMatcher([eng], window_topics=256, window_us=50, publish=True)
+    rt.add_route(b"hook/+/x", "n1")
+    subs[b"hook/+/x"] = ["sub-new"]
+    m.route_changed(b"hook/+/x")
+    m.subscribers_changed(b"hook/+/x")
+    assert am.match(b"hook/7/x", 1, owner=99) == 0
+    assert am.wait([(1, 99)], timeout=10)
+    got_e, got_d = check(am.results[(1, 99)], b"hook/7/x")
+    assert (b"hook/+/x", "n1") in got_e and (b"hook/+/x", "sub-new") in got_d
+    am.close()

@@ -149,21 +149,24 @@ def _free_port():
     return p
 
 
-def _rank(rank, world, port, q):
+def _rank(rank, world, port, q, backend="gloo"):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    # nccl (= RCCL): one GPU per rank; gloo: both ranks on GPU 0 (RCCL refuses that)
+    gpu = rank if backend == "nccl" else 0
+    torch.cuda.set_device(gpu)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     try:
         import workloads
         from emqx_amd import Engine
         from emqx_amd import dist as D
         from oracle.cref import RefIndex
-        torch.cuda.set_device(0)
-        dev = torch.device("cuda", 0)
+        dev = torch.device("cuda", gpu)
         w = workloads.generate(2, 30000, 5000)
         mine = np.nonzero(D.filter_shards(w.fbytes, w.foff, world) == rank)[0]
         fb, fo = _subset(w, mine)
-        eng = Engine()
+        eng = Engine(device=gpu)
         rid = eng.route_ref_many(fb, fo)
         wsel = np.nonzero(w.fwild[mine])[0]
         wb, wo = _subset(type("W", (), {"fbytes": fb, "foff": fo})(), wsel)
@@ -203,12 +206,17 @@ def _rank(rank, world, port, q):
 
 
 @pytest.mark.timeout(400)
-def test_sharded_matcher_two_ranks_one_gpu(emqx):
+@pytest.mark.parametrize("backend", ["gloo", "nccl"])
+def test_sharded_matcher_two_ranks(emqx, backend):
+    """gloo: two ranks sharing this box's GPU; nccl: the RCCL branch, one rank per GPU -- run
+    where two GPUs are visible (the driver's multi-GPU node), skipped on a one-GPU box."""
+    if backend == "nccl" and torch.cuda.device_count() < 2:
+        pytest.skip("the RCCL branch needs two GPUs (this box has one)")
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, q, backend)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
