@@ -557,6 +557,7 @@ struct emqxgm {
   // completer thread -- burns its core while a window is in flight, up to this long)
   std::atomic<uint32_t> spin_us{200};
   uint64_t xrange_bytes = 0;  // emqxgm_tune("exact_range_kb")
+  uint32_t walk_pair_on = 1;  // emqxgm_tune("walk_pair")
 
   // ---- delta commits (writer side) ----
   TrieModel tm;
@@ -590,7 +591,10 @@ struct emqxgm {
   // "bg_build"; 0: never): a commit the current tables cannot take waits for the build, every
   // other commit meanwhile is a delta on the index the readers have
   uint64_t bg_min = 16384;
-  std::atomic<uint32_t> bg_delay_ms{0};  // tune "bg_delay_ms": a build holds its install back (tests)
+  std::atomic<uint32_t> bg_delay_ms{0};
+  // synchronous sets (EMQXGM_SET_COMMIT) waiting for the writer lock: a bulk set lets them in
+  // between two of its slices (sync_lock / let_prio_in)
+  std::atomic<uint32_t> prio_waiting{0};  // tune "bg_delay_ms": a build holds its install back (tests)
 };
 
 namespace {
@@ -2025,6 +2029,7 @@ void set_pipe_geometry(emqxgm* h) {
   const uint32_t wg = std::max<uint32_t>(1, std::min(h->pipe_wg_per_cu, h->geom.blocks / std::max<uint32_t>(1, h->geom.cus)));
   h->geom_pipe = walk_geometry(h->cfg.device, wg);
   h->geom_pipe.xrange_bytes = h->geom.xrange_bytes;
+  h->geom_pipe.pair = h->geom.pair;
 }
 
 int ctx_init(emqxgm* h, PassCtx& c, hipStream_t shared = nullptr) {
@@ -2128,6 +2133,10 @@ int pass_prepare(emqxgm* h, PassCtx& c, uint32_t n, uint64_t bytes_len) {
     return -E2BIG;
   }
   uint32_t want_pairs = std::max<uint32_t>(c.sc.p_cap, std::max<uint32_t>(1u << 20, n * 4u));
+  // room for every walk wave's static first chunk (walk_static_chunks; without it each wave's
+  // first flush takes an atomic on one counter, serialised at ~88/us), up to 16M slots
+  const uint64_t stat_need = (uint64_t)walk_blocks(h->geom, n, WALK_SHALLOW) * (256 / 64) * STAGE_CHUNK;
+  want_pairs = std::max<uint32_t>(want_pairs, (uint32_t)std::min<uint64_t>(stat_need, 1u << 24));
   int rc = ensure_scratch(h, c, std::max<uint32_t>(n, 1), words, want_pairs);
   if (rc) return rc;
   if (n == 0) {
@@ -2707,6 +2716,24 @@ struct WriterLock {
   explicit WriterLock(emqxgm* h) : w(h->wmu), p(h->pmu) {}
 };
 
+// The writer lock of a batch set.  A synchronous one (prio: EMQXGM_SET_COMMIT, the writing
+// node's hook) announces itself, so that a bulk set (a resync's 64k-topic chunk) lets it in
+// between two of its slices: a subscribe waits for one slice, not for the chunk.
+std::unique_lock<std::mutex> set_lock(emqxgm* h, bool prio) {
+  if (!prio) return std::unique_lock<std::mutex>(h->wmu);
+  h->prio_waiting.fetch_add(1);
+  std::unique_lock<std::mutex> lk(h->wmu);
+  h->prio_waiting.fetch_sub(1);
+  return lk;
+}
+constexpr uint64_t SET_SLICE = 4096;  // topics of a bulk set per writer-lock hold
+void let_prio_in(emqxgm* h, std::unique_lock<std::mutex>& lk) {
+  if (h->prio_waiting.load() == 0) return;
+  lk.unlock();
+  while (h->prio_waiting.load() != 0) std::this_thread::yield();
+  lk.lock();
+}
+
 }  // namespace
 
 extern "C" {
@@ -2742,6 +2769,7 @@ int emqxgm_create(const emqxgm_cfg* cfg, emqxgm_t** out) {
   h->wstream = h->sync.stream;
   h->geom = walk_geometry(h->cfg.device, h->cfg.walk_wg_per_cu);
   h->geom.xrange_bytes = h->xrange_bytes;
+  h->geom.pair = h->walk_pair_on;
   set_pipe_geometry(h);
   h->dirty = true;
   int rc = commit_locked(h, nullptr, true);  // empty index: epoch 1
@@ -2891,14 +2919,18 @@ int emqxgm_route_set_many(emqxgm_t* h, const uint8_t* bytes, const uint64_t* off
   if (!h || !offsets || (!bytes && n)) return -EINVAL;
   for (uint64_t i = 0; i < n; ++i)
     if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > 65535) return -EINVAL;
-  WriterLock g(h);
-  for (uint64_t i = 0; i < n; ++i) {
-    const uint8_t* p = bytes + offsets[i];
-    const uint32_t len = (uint32_t)(offsets[i + 1] - offsets[i]);
-    const uint32_t id = find_id(h, p, len, present != 0);
-    if (id == NONE) continue;
-    if (h->filters.size() >= 0x7FFFFFFFu) return -E2BIG;
-    route_set_locked(h, id, present != 0);
+  std::unique_lock<std::mutex> lk = set_lock(h, false);
+  for (uint64_t i0 = 0; i0 < n; i0 += SET_SLICE) {
+    if (i0) let_prio_in(h, lk);
+    std::unique_lock<std::shared_mutex> g(h->pmu);
+    for (uint64_t i = i0; i < std::min(n, i0 + SET_SLICE); ++i) {
+      const uint8_t* p = bytes + offsets[i];
+      const uint32_t len = (uint32_t)(offsets[i + 1] - offsets[i]);
+      const uint32_t id = find_id(h, p, len, present != 0);
+      if (id == NONE) continue;
+      if (h->filters.size() >= 0x7FFFFFFFu) return -E2BIG;
+      route_set_locked(h, id, present != 0);
+    }
   }
   return 0;
 }
@@ -3091,11 +3123,13 @@ int emqxgm_route_set_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* of
   if (!h || !offsets || (!bytes && n && offsets[n]) || (flags & ~EMQXGM_SET_COMMIT)) return -EINVAL;
   for (uint64_t i = 0; i < n; ++i)
     if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > 65535) return -EINVAL;
-  std::unique_lock<std::mutex> lk(h->wmu);
+  const bool sync = (flags & EMQXGM_SET_COMMIT) != 0;
+  std::unique_lock<std::mutex> lk = set_lock(h, sync);
   const size_t c0 = h->changed.size();  // changes pending from other callers
-  {
+  for (uint64_t i0 = 0; i0 < n; i0 += sync ? n : SET_SLICE) {
+    if (i0) let_prio_in(h, lk);
     std::unique_lock<std::shared_mutex> g(h->pmu);
-    for (uint64_t i = 0; i < n; ++i) {
+    for (uint64_t i = i0; i < (sync ? n : std::min(n, i0 + SET_SLICE)); ++i) {
       const bool pr = !present || present[i];
       const uint8_t* p = bytes + offsets[i];
       const uint32_t len = (uint32_t)(offsets[i + 1] - offsets[i]);
@@ -3121,12 +3155,14 @@ int emqxgm_route_dests_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* 
       if (!node || !group || node[j] == NONE || (group[j] != NONE && (group[j] & EMQXGM_DEST_GROUP)))
         return -EINVAL;
   }
-  std::unique_lock<std::mutex> lk(h->wmu);
+  const bool sync = (flags & EMQXGM_SET_COMMIT) != 0;
+  std::unique_lock<std::mutex> lk = set_lock(h, sync);
   const size_t c0 = h->changed.size();  // changes pending from other callers
-  {
+  std::vector<std::pair<uint32_t, uint32_t>> ds;
+  for (uint64_t i0 = 0; i0 < n; i0 += sync ? n : SET_SLICE) {
+    if (i0) let_prio_in(h, lk);
     std::unique_lock<std::shared_mutex> g(h->pmu);
-    std::vector<std::pair<uint32_t, uint32_t>> ds;
-    for (uint64_t i = 0; i < n; ++i) {
+    for (uint64_t i = i0; i < (sync ? n : std::min(n, i0 + SET_SLICE)); ++i) {
       ds.clear();
       for (uint32_t j = dptr[i]; j < dptr[i + 1]; ++j) ds.emplace_back(node[j], group[j]);
       std::sort(ds.begin(), ds.end());
@@ -3165,12 +3201,14 @@ int emqxgm_subscribers_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* 
     if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > 65535 || sptr[i + 1] < sptr[i] ||
         (sptr[i + 1] > sptr[i] && !subs))
       return -EINVAL;
-  std::unique_lock<std::mutex> lk(h->wmu);
+  const bool sync = (flags & EMQXGM_SET_COMMIT) != 0;
+  std::unique_lock<std::mutex> lk = set_lock(h, sync);
   const size_t c0 = h->changed.size();  // changes pending from other callers
-  {
+  std::vector<uint32_t> ss;
+  for (uint64_t i0 = 0; i0 < n; i0 += sync ? n : SET_SLICE) {
+    if (i0) let_prio_in(h, lk);
     std::unique_lock<std::shared_mutex> g(h->pmu);
-    std::vector<uint32_t> ss;
-    for (uint64_t i = 0; i < n; ++i) {
+    for (uint64_t i = i0; i < (sync ? n : std::min(n, i0 + SET_SLICE)); ++i) {
       ss.assign(subs + sptr[i], subs + sptr[i + 1]);
       std::sort(ss.begin(), ss.end());
       ss.erase(std::unique(ss.begin(), ss.end()), ss.end());
@@ -4297,6 +4335,7 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
     h->cfg.walk_wg_per_cu = (uint32_t)value;
     h->geom = walk_geometry(h->cfg.device, h->cfg.walk_wg_per_cu);
     h->geom.xrange_bytes = h->xrange_bytes;
+    h->geom.pair = h->walk_pair_on;
     set_pipe_geometry(h);
     return 0;  // spill scratch is re-sized by the next match (ensure_scratch)
   }
@@ -4331,6 +4370,14 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
     for (auto& p : h->hpipes)
       if (p.state == 1) return -EBUSY;
     h->host_out_mode = (uint32_t)value;
+    return 0;
+  }
+  if (strcmp(key, "walk_pair") == 0) {  // 1 (default): two lanes per topic for small batches
+    if (value < 0 || value > 1) return -EINVAL;
+    std::lock_guard<std::mutex> g(h->mmu);
+    if (int rc = drain_pipes(h)) return rc;  // in-flight passes read the geometry
+    h->walk_pair_on = (uint32_t)value;
+    h->geom.pair = h->geom_pipe.pair = h->walk_pair_on;
     return 0;
   }
   if (strcmp(key, "exact_range_kb") == 0) {  // 0 (default): auto; > 0: probe in ranges of v KiB

@@ -137,6 +137,9 @@ struct WalkGeom {
   // exact route-key probe in passes over bucket ranges of this many bytes (0: one pass; see
   // launch_exact); set by the engine, emqxgm_tune("exact_range_kb")
   uint64_t xrange_bytes = 0;
+  // two lanes per topic (k_walk PAIR) for batches of at most half the grid's lanes;
+  // emqxgm_tune("walk_pair", 0) turns it off (A/B)
+  uint32_t pair = 1;
 };
 
 WalkGeom walk_geometry(int device, uint32_t wg_per_cu);
@@ -207,6 +210,8 @@ hipError_t launch_fanout(const DevIndex& ix, const Scratch& sc, FanScratch& fs, 
 // the walk's workgroup count and its static staged-pair chunks (one per wave, or 0); k_tok
 // starts CTL_PAIR_TOP at static_chunks * STAGE_CHUNK
 uint32_t walk_blocks(const WalkGeom& g, uint32_t n, uint32_t level);
+// whether the walk of n topics runs two lanes per topic (k_walk PAIR)
+bool walk_pair(const WalkGeom& g, uint32_t n, uint32_t level);
 uint32_t walk_static_chunks(const WalkGeom& g, uint32_t n, uint32_t level, uint32_t pcap);
 // the claim counters' start values past the walk's static first claims (k_tok sets them)
 void walk_claim_init(const WalkGeom& g, uint32_t n, uint32_t level, uint32_t claim0[WALK_SHARDS]);

@@ -646,15 +646,25 @@ hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, c
 // launches only the blocks it fills: the waves a full grid adds only queue
 // failed claims on the exhausted shard counters (r03: a cfg3 walk took 79 us at 64k topics and
 // 80 us at 262k).
-uint32_t walk_blocks(const WalkGeom& g, uint32_t n, uint32_t level) {
+static uint32_t walk_cap_blocks(const WalkGeom& g, uint32_t level) {
   constexpr uint32_t LDS_CU = 160u * 1024u;
   const uint32_t lds = level >= WALK_SPILL ? walk_lds_bytes(WALK_STK_SPILL)
                        : level == WALK_DEEP ? walk_lds_bytes(WALK_STK_DEEP, WALK_CPT)
                                             : walk_lds_bytes(WALK_STK_SHALLOW, WALK_CPT);
-  uint32_t blocks = std::min<uint32_t>(g.blocks, g.cus * (LDS_CU / lds));
-  // one topic per lane (static_one): only the blocks that hold topics (r04: a 16-topic window
-  // launched one block per CU, all but one of them empty)
-  return std::min<uint32_t>(blocks, std::max<uint32_t>((n + WG - 1) / WG, 1u));
+  return std::min<uint32_t>(g.blocks, g.cus * (LDS_CU / lds));
+}
+
+bool walk_pair(const WalkGeom& g, uint32_t n, uint32_t level) {
+  return g.pair && WALK_CPT && level < WALK_SPILL && n > 0 &&
+         2ull * n <= (uint64_t)walk_cap_blocks(g, level) * WG;
+}
+
+uint32_t walk_blocks(const WalkGeom& g, uint32_t n, uint32_t level) {
+  const uint32_t blocks = walk_cap_blocks(g, level);
+  // one topic per lane (static_one), or per pair of lanes: only the blocks that hold topics
+  // (r04: a 16-topic window launched one block per CU, all but one of them empty)
+  const uint64_t lanes = walk_pair(g, n, level) ? 2ull * n : (uint64_t)n;
+  return std::min<uint32_t>(blocks, std::max<uint32_t>((uint32_t)((lanes + WG - 1) / WG), 1u));
 }
 
 // Topics per claim: a batch too small to give every wave TBLK topics is spread over all of them
@@ -722,6 +732,7 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   // at most one topic per lane of the launched grid: lane gl walks topic gl, no claims (r03:
   // the failed claims of every wave on the exhausted counters dominated small batches)
   a.static_one = (uint64_t)n <= (uint64_t)blocks * WG ? 1u : 0u;
+  const bool pair = !census && walk_pair(g, n, level);
   a.stat_chunks = stat_chunks;
   a.static_claim = 1;
   a.census = census;
@@ -740,8 +751,12 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   } else {
     if (level >= WALK_SPILL)
       hipLaunchKernelGGL((k_walk<false, true, SP>), grid, dim3(WG), 0, s, a);
+    else if (level == WALK_DEEP && pair)
+      hipLaunchKernelGGL((k_walk<false, false, DP, C, true>), grid, dim3(WG), 0, s, a);
     else if (level == WALK_DEEP)
       hipLaunchKernelGGL((k_walk<false, false, DP, C>), grid, dim3(WG), 0, s, a);
+    else if (pair)
+      hipLaunchKernelGGL((k_walk<false, false, SH, C, true>), grid, dim3(WG), 0, s, a);
     else
       hipLaunchKernelGGL((k_walk<false, false, SH, C>), grid, dim3(WG), 0, s, a);
   }

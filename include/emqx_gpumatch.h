@@ -586,7 +586,8 @@ int emqxgm_set_profiling(emqxgm_t* h, int on);
 /* Runtime tuning knobs: "walk_wg_per_cu" (persistent walk workgroups per CU); "leaf_prune"
  * (1 default: depth-code pruning in the walk, 0 off); "host_out" (host pipes copy results to the
  * host with hipMemcpyAsync, 0 default, or with a kernel writing host memory, 1);
- * "exact_range_kb" (0 default: one route-key probe pass over the whole table; > 0: the probe
+ * "walk_pair" (1 default: a batch of at most half the walk grid's lanes is walked by two lanes
+ * per topic; 0: one lane per topic); "exact_range_kb" (0 default: one route-key probe pass over the whole table; > 0: the probe
  * runs in passes over bucket ranges of that many KiB, so that the lines in flight share page
  * translations -- measured slower on a 100M-key table, kept as an option); "delta_commit": 0 = every commit rebuilds the index, 1 = small deltas are patched in place
  * (default), 2 = every delta that fits the tables' load bounds is patched in place; "delta_max":

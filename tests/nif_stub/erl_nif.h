@@ -52,3 +52,6 @@ ErlNifRWLock* enif_rwlock_create(char*); void enif_rwlock_destroy(ErlNifRWLock*)
 void enif_rwlock_rlock(ErlNifRWLock*); void enif_rwlock_runlock(ErlNifRWLock*);
 void enif_rwlock_rwlock(ErlNifRWLock*); void enif_rwlock_rwunlock(ErlNifRWLock*);
 void* enif_realloc(void*, size_t);
+typedef unsigned long ErlNifTid; typedef struct ErlNifThreadOpts ErlNifThreadOpts;
+int enif_thread_create(char*, ErlNifTid*, void* (*)(void*), void*, ErlNifThreadOpts*);
+int enif_thread_join(ErlNifTid, void**);

@@ -33,19 +33,30 @@ def chunks(w, size):
         yield w.fbytes[int(w.foff[a]):int(w.foff[b])], off
 
 
-def resync(engs, w, size):
+def resync(engs, w, size, pool=None):
     gens = [e.sync_begin() for e in engs]
     t0 = time.perf_counter()
     n = 0
+    last = t0
     for buf, off in chunks(w, size):
-        for e in engs:  # the NIF calls every engine in turn, per chunk
-            e.route_set_many(buf, off, True)
+        if pool is None:
+            for e in engs:  # every engine in turn, per chunk
+                e.route_set_many(buf, off, True)
+        else:  # one thread per engine, as the NIF's on_engines (ctypes drops the GIL)
+            list(pool.map(lambda e: e.route_set_many(buf, off, True), engs))
         n += 1
+        if time.perf_counter() - last > 30:
+            last = time.perf_counter()
+            print(f"  ... {n} chunks", flush=True)
     t_chunks = time.perf_counter() - t0
     removed = [e.sync_end(g) for e, g in zip(engs, gens)]
     t1 = time.perf_counter()
-    for e in engs:
-        e.commit()
+    if pool is None:
+        for e in engs:
+            e.commit()
+    else:
+        list(pool.map(lambda e: e.commit(), engs))
+    print("  ... committed", flush=True)
     return {"chunks": n, "set_s": round(t_chunks, 3), "sync_end_s": round(t1 - t0 - t_chunks, 3),
             "commit_s": round(time.perf_counter() - t1, 3), "removed": int(removed[0]),
             "total_s": round(time.perf_counter() - t0, 3)}
@@ -54,7 +65,8 @@ def resync(engs, w, size):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--filters", type=int, default=10_000_000)
-    ap.add_argument("--engines", default="1,8")
+    ap.add_argument("--engines", default="1,8,8p",
+                    help="engine counts; a 'p' suffix: one thread per engine per chunk")
     ap.add_argument("--chunk", type=int, default=65536)
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
@@ -63,12 +75,15 @@ def main():
     w = workloads.generate(3, args.filters, 1)
     out = {"workload": f"cfg3 route table: {w.nf} routes (every filter a wildcard: trie + route key)",
            "chunk_topics": args.chunk, "runs": {}}
-    for k in [int(x) for x in args.engines.split(",")]:
+    from concurrent.futures import ThreadPoolExecutor
+    for spec in args.engines.split(","):
+        k = int(spec.rstrip("p"))
+        pool = ThreadPoolExecutor(k) if spec.endswith("p") and k > 1 else None
         engs = [Engine() for _ in range(k)]
-        r = {"first_sync": resync(engs, w, args.chunk)}
-        print(f"[{k} engines] first sync {r['first_sync']}", flush=True)
-        r["resync"] = resync(engs, w, args.chunk)
-        print(f"[{k} engines] resync {r['resync']}", flush=True)
+        r = {"first_sync": resync(engs, w, args.chunk, pool)}
+        print(f"[{spec} engines] first sync {r['first_sync']}", flush=True)
+        r["resync"] = resync(engs, w, args.chunk, pool)
+        print(f"[{spec} engines] resync {r['resync']}", flush=True)
         # a hook on the writing node while the resync runs
         lat, stop = [], threading.Event()
 
@@ -84,7 +99,7 @@ def main():
                 time.sleep(0.002)
         th = threading.Thread(target=hook)
         th.start()
-        r["resync_with_hooks"] = resync(engs, w, args.chunk)
+        r["resync_with_hooks"] = resync(engs, w, args.chunk, pool)
         stop.set()
         th.join()
         v = np.asarray(lat) * 1e3
@@ -92,8 +107,10 @@ def main():
                                       "p99": round(float(np.percentile(v, 99)), 3),
                                       "max": round(float(v.max()), 3)}
         r["queued_event_lag_s"] = r["resync_with_hooks"]["total_s"]
-        print(f"[{k} engines] hooks during resync {r['hook_during_resync_ms']}", flush=True)
-        out["runs"][str(k)] = r
+        print(f"[{spec} engines] hooks during resync {r['hook_during_resync_ms']}", flush=True)
+        out["runs"][spec] = r
+        if pool is not None:
+            pool.shutdown()
         for e in engs:
             e.close()
     line = json.dumps(out)
