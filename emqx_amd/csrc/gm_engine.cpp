@@ -2173,7 +2173,8 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
   c.census = census;
   c.walk_level = (census ? E.census_level : E.walk_level).load(std::memory_order_relaxed);
   // (census passes and the synchronous ones keep the full geometry)
-  const WalkGeom& WG_ = (c.pipelined && !census) ? h->geom_pipe : h->geom;
+  WalkGeom WG_ = (c.pipelined && !census) ? h->geom_pipe : h->geom;
+  if (census) WG_.pair = 0;  // census walks are one lane per topic (their buffers count lanes)
   const uint32_t stat = ix.trie_empty ? 0u : walk_static_chunks(WG_, n, c.walk_level, s.p_cap);
   roctx_mark(h->roctx, "k_tok");
   // (per-topic reject counts: only the verification passes write -- and then read -- them;

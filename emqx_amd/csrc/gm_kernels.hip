@@ -646,21 +646,25 @@ hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, c
 // launches only the blocks it fills: the waves a full grid adds only queue
 // failed claims on the exhausted shard counters (r03: a cfg3 walk took 79 us at 64k topics and
 // 80 us at 262k).
-static uint32_t walk_cap_blocks(const WalkGeom& g, uint32_t level) {
+// Resident walk blocks: LDS-bound (all) or also bound by the geometry (wg_per_cu).
+static uint32_t walk_cap_blocks(const WalkGeom& g, uint32_t level, bool lds_only = false) {
   constexpr uint32_t LDS_CU = 160u * 1024u;
   const uint32_t lds = level >= WALK_SPILL ? walk_lds_bytes(WALK_STK_SPILL)
                        : level == WALK_DEEP ? walk_lds_bytes(WALK_STK_DEEP, WALK_CPT)
                                             : walk_lds_bytes(WALK_STK_SHALLOW, WALK_CPT);
-  return std::min<uint32_t>(g.blocks, g.cus * (LDS_CU / lds));
+  return lds_only ? g.cus * (LDS_CU / lds) : std::min<uint32_t>(g.blocks, g.cus * (LDS_CU / lds));
 }
 
+// A pair walk may use every block LDS allows, also in the pipelined passes' geometry (three
+// workgroups per CU, which leaves room for the other pass's kernels): a batch this small has
+// little of them to run beside it, and 100k topics need 782 blocks, just past 768.
 bool walk_pair(const WalkGeom& g, uint32_t n, uint32_t level) {
   return g.pair && WALK_CPT && level < WALK_SPILL && n > 0 &&
-         2ull * n <= (uint64_t)walk_cap_blocks(g, level) * WG;
+         2ull * n <= (uint64_t)walk_cap_blocks(g, level, true) * WG;
 }
 
 uint32_t walk_blocks(const WalkGeom& g, uint32_t n, uint32_t level) {
-  const uint32_t blocks = walk_cap_blocks(g, level);
+  const uint32_t blocks = walk_cap_blocks(g, level, walk_pair(g, n, level));
   // one topic per lane (static_one), or per pair of lanes: only the blocks that hold topics
   // (r04: a 16-topic window launched one block per CU, all but one of them empty)
   const uint64_t lanes = walk_pair(g, n, level) ? 2ull * n : (uint64_t)n;

@@ -40,7 +40,7 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 KRE="k_walk|k_tok|k_exact|k_scatter|k_verify|k_scan"
 NOCPU="--no-cpu-baseline --no-e2e --nif="
-PROF="$NOCPU --settle-s 0"  # profiled runs: every launch is profiled, so no settle phase
+PROF="$NOCPU --settle-s 0 --no-subscribe"  # profiled runs: every launch is profiled, so no settle phase
 
 step_tests() {
   local args=${1:-tests,-m,gpu}
