@@ -27,6 +27,7 @@ ap.add_argument("--topics", type=int, default=4000000)
 ap.add_argument("--batches", type=int, default=3)
 ap.add_argument("--stats", default=None)
 ap.add_argument("--out", default=None)
+ap.add_argument("--sq", default=None, help="tools/job.sh sq=N output dir: issue counters of k_walk")
 a = ap.parse_args()
 s = json.load(open(os.path.join(a.root, "summary.json")))
 dur = {}
@@ -64,6 +65,19 @@ for name, k in s.items():
         kern[short] = ent
 out = {"topics": a.topics, "batches": a.batches, "cfg": a.cfg, "source": a.root,
        "stats": a.stats, "kernels": kern}
+if a.sq and os.path.exists(os.path.join(a.sq, "summary.json")):
+    # per launch of the production walk (not the census one): instructions per wave, issue share
+    for name, k in json.load(open(os.path.join(a.sq, "summary.json"))).items():
+        if not name.startswith("k_walk<false") or "SQ_WAVES" not in k:
+            continue
+        waves = k["SQ_WAVES"]
+        sq = {c: v for c, v in k.items() if c.startswith(("SQ_", "GRBM_"))}
+        sq["insts_per_wave"] = (k.get("SQ_INSTS_VALU", 0) + k.get("SQ_INSTS_SALU", 0) +
+                                k.get("SQ_INSTS_LDS", 0) + k.get("SQ_INSTS_VMEM_RD", 0) +
+                                k.get("SQ_INSTS_VMEM_WR", 0)) / waves
+        sq["source"] = a.sq
+        if "k_walk" in kern and kern["k_walk"]["kernel"] == name:
+            kern["k_walk"]["sq"] = sq
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 p = a.out or os.path.join(root, "profiles", f"pmc_cfg{a.cfg}.json")
 json.dump(out, open(p, "w"), indent=1)
