@@ -4374,7 +4374,7 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
     return 0;
   }
   if (strcmp(key, "walk_pair") == 0) {  // 1 (default): two lanes per topic for small batches
-    if (value < 0 || value > 1) return -EINVAL;
+    if (value < 0 || value > 2) return -EINVAL;  // (2: every batch, an A/B)
     std::lock_guard<std::mutex> g(h->mmu);
     if (int rc = drain_pipes(h)) return rc;  // in-flight passes read the geometry
     h->walk_pair_on = (uint32_t)value;

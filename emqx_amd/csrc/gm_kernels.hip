@@ -659,15 +659,21 @@ static uint32_t walk_cap_blocks(const WalkGeom& g, uint32_t level, bool lds_only
 // workgroups per CU, which leaves room for the other pass's kernels): a batch this small has
 // little of them to run beside it, and 100k topics need 782 blocks, just past 768.
 bool walk_pair(const WalkGeom& g, uint32_t n, uint32_t level) {
-  return g.pair && WALK_CPT && level < WALK_SPILL && n > 0 &&
-         2ull * n <= (uint64_t)walk_cap_blocks(g, level, true) * WG;
+  if (!g.pair || !WALK_CPT || level >= WALK_SPILL || n == 0) return false;
+  // pair = 2 (A/B): every batch, with claims past the grid's lanes
+  return g.pair == 2 || 2ull * n <= (uint64_t)walk_cap_blocks(g, level, true) * WG;
+}
+
+// topics' lanes: two per topic for a pair walk
+static uint64_t walk_lanes(const WalkGeom& g, uint32_t n, uint32_t level) {
+  return walk_pair(g, n, level) ? 2ull * n : (uint64_t)n;
 }
 
 uint32_t walk_blocks(const WalkGeom& g, uint32_t n, uint32_t level) {
-  const uint32_t blocks = walk_cap_blocks(g, level, walk_pair(g, n, level));
+  const uint32_t blocks = walk_cap_blocks(g, level, walk_pair(g, n, level) && g.pair != 2);
   // one topic per lane (static_one), or per pair of lanes: only the blocks that hold topics
   // (r04: a 16-topic window launched one block per CU, all but one of them empty)
-  const uint64_t lanes = walk_pair(g, n, level) ? 2ull * n : (uint64_t)n;
+  const uint64_t lanes = walk_lanes(g, n, level);
   return std::min<uint32_t>(blocks, std::max<uint32_t>((uint32_t)((lanes + WG - 1) / WG), 1u));
 }
 
@@ -687,7 +693,7 @@ void walk_claim_init(const WalkGeom& g, uint32_t n, uint32_t level, uint32_t cla
   const uint32_t blocks = walk_blocks(g, n, level);
   const uint32_t tblk = walk_tblk(blocks, n);
   // exactly the walk's condition: claims at all (not static_one), static first ones
-  const bool on = (uint64_t)n > (uint64_t)blocks * WG;
+  const bool on = walk_lanes(g, n, level) > (uint64_t)blocks * WG;
   for (uint32_t cs = 0; cs < WALK_SHARDS; ++cs) {
     const uint32_t lo = (uint32_t)((uint64_t)n * cs / WALK_SHARDS);
     const uint32_t hi = (uint32_t)((uint64_t)n * (cs + 1) / WALK_SHARDS);
@@ -735,8 +741,8 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   a.tblk = walk_tblk(blocks, n);
   // at most one topic per lane of the launched grid: lane gl walks topic gl, no claims (r03:
   // the failed claims of every wave on the exhausted counters dominated small batches)
-  a.static_one = (uint64_t)n <= (uint64_t)blocks * WG ? 1u : 0u;
   const bool pair = !census && walk_pair(g, n, level);
+  a.static_one = (pair ? 2ull * n : (uint64_t)n) <= (uint64_t)blocks * WG ? 1u : 0u;
   a.stat_chunks = stat_chunks;
   a.static_claim = 1;
   a.census = census;

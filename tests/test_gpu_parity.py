@@ -455,6 +455,19 @@ def test_cfg2_full(emqx):
     assert int(res.row_ptr[-1]) > 0 and (res.exact_id != emqx.NONE).any()
 
 
+@pytest.mark.parametrize("cfg", [1, 2])
+def test_pair_walk_with_claims(emqx, cfg):
+    """walk_pair = 2: every batch walked by two lanes per topic, claims past the grid's lanes
+    (cfg1's 100k topics and cfg2's 1M) -- bit-exact against the oracle like the default walk."""
+    import workloads
+    w = workloads.generate(cfg)
+    eng, ref = _load_both(emqx, w)
+    eng.tune("walk_pair", 2)
+    _assert_engine_equals_ref(eng, ref, None, w.tbytes, w.toff)
+    eng.tune("walk_pair", 0)  # and one lane per topic for the same batch
+    _assert_engine_equals_ref(eng, ref, None, w.tbytes, w.toff)
+
+
 def test_cfg3_sample_at_1m_filters(emqx):
     import workloads
     w = workloads.generate(3, 1_000_000, 200_000)
