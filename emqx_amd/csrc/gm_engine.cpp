@@ -191,6 +191,9 @@ struct Epoch {
   std::atomic<uint32_t> census_level{WALK_SHALLOW};  // the same for diagnostic census passes
                                                       // (their unpruned walks stack deeper)
   mutable std::atomic<bool> ready_seen{false};  // `ready` has completed (passes skip the query)
+  // retired by a background build's install: the last epoch on the replaced tables frees
+  // gigabytes (hipFree synchronises), so the builder thread frees it, not a subscribe's commit
+  bool heavy = false;
   ~Epoch() {
     if (ready) (void)hipEventDestroy(ready);
   }
@@ -1738,13 +1741,16 @@ int publish_epoch(emqxgm* h, bool delta) {
 }
 
 // Frees retired epochs no reader holds any more (writers only: readers never free).
-void sweep_graveyard(emqxgm* h) {
+// all = false (writers): heavy epochs are left to the builder thread.  Returns the heavy epochs
+// still retired (held by a pass).
+size_t sweep_graveyard(emqxgm* h, bool all = false) {
   std::vector<EpochP> dead;
+  size_t left = 0;
   {
     std::lock_guard<std::mutex> g(h->emu);
     auto& gy = h->graveyard;
     for (size_t i = 0; i < gy.size();) {
-      if (gy[i].use_count() == 1) {
+      if (gy[i].use_count() == 1 && (all || !gy[i]->heavy)) {
         dead.push_back(std::move(gy[i]));
         gy[i] = std::move(gy.back());
         gy.pop_back();
@@ -1752,8 +1758,11 @@ void sweep_graveyard(emqxgm* h) {
         ++i;
       }
     }
+    for (const auto& e : gy) left += e->heavy ? 1u : 0u;
   }
   // dead epochs (and the device buffers only they owned) are freed here, outside emu
+  dead.clear();
+  return left;
 }
 
 double ms_since(std::chrono::steady_clock::time_point t0) {
@@ -1855,14 +1864,10 @@ void build_thread(emqxgm* h, BuildJob* J) {
   // writer lock, and so are the replaced device tables once the passes that read them are done
   // -- not by the next subscribe's commit (sweep_graveyard takes only the epoch lock).
   spent.reset();
-  for (int i = 0; i < 2000; ++i) {
-    sweep_graveyard(h);
-    {
-      std::lock_guard<std::mutex> g(h->emu);
-      if (h->graveyard.empty()) break;
-    }
+  for (int i = 0; i < 10000 && sweep_graveyard(h, true) != 0; ++i)
     std::this_thread::sleep_for(std::chrono::milliseconds(1));
-  }
+  std::lock_guard<std::mutex> g(h->emu);  // (a pass held on for 10 s: writers free them later)
+  for (auto& e : h->graveyard) e->heavy = false;
 }
 
 // Starts a background full build of the registry as it is now (wmu held): the changes pending now
@@ -1935,7 +1940,14 @@ int install_build(emqxgm* h, std::unique_ptr<BuildJob>& spent) {
       J->covered.clear();
       if (rc == 0) J->covered.push_back(NONE);  // flip every flag below
     }
-    if (rc == 0) rc = publish_epoch(h, false);
+    if (rc == 0) {
+      {
+        std::lock_guard<std::mutex> g(h->emu);  // every epoch on the replaced tables
+        if (h->cur) h->cur->heavy = true;
+        for (auto& e : h->graveyard) e->heavy = true;
+      }
+      rc = publish_epoch(h, false);
+    }
   } else {
     h->changed = ch;
     set_err(h, "background build failed: a blocking full build follows");
