@@ -69,7 +69,7 @@ def main():
                          "the replicas, after their figure is final, under a watchdog")
     ap.add_argument("--no-filter-shard", action="store_true",
                     help="N>1: leave the filter-sharded layout out")
-    ap.add_argument("--filter-shard-timeout", type=float, default=240.0,
+    ap.add_argument("--filter-shard-timeout", type=float, default=120.0,
                     help="N>1: seconds the filter-sharded run may take before the watchdog prints "
                          "the line with config.filter_sharded = {error: timeout} and ends the rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")

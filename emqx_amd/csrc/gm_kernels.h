@@ -124,7 +124,10 @@ constexpr bool WALK_CPT = true;
 constexpr uint32_t WALK_STK_SHALLOW = 12;
 constexpr uint32_t WALK_STK_DEEP = 24;
 constexpr uint32_t WALK_STK_SPILL = 12;
-enum WalkLevel : uint32_t { WALK_SHALLOW = 0, WALK_DEEP = 1, WALK_SPILL = 2 };
+// The walk variant a committed index needs, raised when a pass's lanes outgrow their stack:
+// shallow LDS stack (pairs for small batches only), shallow stack with pairs for every batch (two
+// lanes share a topic's items), deep stack with pairs, deep + global spill (one lane per topic).
+enum WalkLevel : uint32_t { WALK_SHALLOW = 0, WALK_PAIRED = 1, WALK_DEEP = 2, WALK_SPILL = 3 };
 constexpr uint32_t WALK_SPILL_MIN = 32;  // initial spill items per lane (grown on overflow)
 // spill items per lane that no walk can exceed: a resolved probe pushes <= 4 items spanning
 // 3 levels, and the LIFO holds <= 3 unexplored siblings per level of the current path

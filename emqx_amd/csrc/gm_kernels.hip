@@ -658,10 +658,15 @@ static uint32_t walk_cap_blocks(const WalkGeom& g, uint32_t level, bool lds_only
 // A pair walk may use every block LDS allows, also in the pipelined passes' geometry (three
 // workgroups per CU, which leaves room for the other pass's kernels): a batch this small has
 // little of them to run beside it, and 100k topics need 782 blocks, just past 768.
+// Pairs also for large batches (claims past the grid's lanes) once an index's walks outgrew the
+// shallow stack with one lane per topic (WALK_PAIRED and up): its searches are bushy, and two
+// lanes share them, each with a shallower stack (r05, cfg2 1M topics: walk 1.207 -> 1.017 ms in
+// the shallow stack instead of the deep one, verify+scan+scatter 0.224 -> 0.170 ms).  A narrow
+// search (cfg3) only loses lanes to it: walk 0.33 -> 0.58 ms.  pair = 2 (A/B): every batch.
 bool walk_pair(const WalkGeom& g, uint32_t n, uint32_t level) {
   if (!g.pair || !WALK_CPT || level >= WALK_SPILL || n == 0) return false;
-  // pair = 2 (A/B): every batch, with claims past the grid's lanes
-  return g.pair == 2 || 2ull * n <= (uint64_t)walk_cap_blocks(g, level, true) * WG;
+  return g.pair == 2 || level >= WALK_PAIRED ||
+         2ull * n <= (uint64_t)walk_cap_blocks(g, level, true) * WG;
 }
 
 // topics' lanes: two per topic for a pair walk
@@ -670,7 +675,9 @@ static uint64_t walk_lanes(const WalkGeom& g, uint32_t n, uint32_t level) {
 }
 
 uint32_t walk_blocks(const WalkGeom& g, uint32_t n, uint32_t level) {
-  const uint32_t blocks = walk_cap_blocks(g, level, walk_pair(g, n, level) && g.pair != 2);
+  // (a static pair walk may use every block LDS allows; a claiming one keeps the geometry)
+  const bool pair = walk_pair(g, n, level);
+  const uint32_t blocks = walk_cap_blocks(g, level, pair && 2ull * n <= (uint64_t)walk_cap_blocks(g, level, true) * WG);
   // one topic per lane (static_one), or per pair of lanes: only the blocks that hold topics
   // (r04: a 16-topic window launched one block per CU, all but one of them empty)
   const uint64_t lanes = walk_lanes(g, n, level);
