@@ -79,11 +79,12 @@ def main():
     ap.add_argument("--windows", default="16384,65536,262144,1048576",
                     help="NIF batcher window sizes (topics) for the operating-point sweep "
                          "('' = skip); rank 0, N=1, with the host-in/host-out timing")
-    ap.add_argument("--nif", default="16:16384,16:65536,64:16384,64:65536,16:16384:1024,16:65536:4096",
-                    help="concurrent publish entry load (threads:window[:processes per thread], "
-                         "'' = skip): publisher threads each calling emqxgm_async_match one topic "
-                         "at a time; processes default to (host pipes + 1) windows outstanding; "
-                         "rank 0, N=1")
+    ap.add_argument("--nif", default="16:16384,16:65536,64:16384,64:65536,16:16384:1024,16:65536:4096,"
+                                     "16:65536:0:500:1,16:65536:0:500:8",
+                    help="concurrent publish entry load (threads:window[:processes per thread"
+                         "[:ns of work per reported call:report threads]], '' = skip): publisher "
+                         "threads each calling emqxgm_async_match one topic at a time; processes "
+                         "default (0) to (host pipes + 1) windows outstanding; rank 0, N=1")
     ap.add_argument("--only-nif", action="store_true",
                     help="build the index and run only the concurrent-entry load (no timed steps)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -551,12 +552,17 @@ def _nif_concurrent(eng, w, spec):
         # closed loop: calls outstanding = T x procs, so by Little's law the latency is that over
         # the rate -- (pipes + 1) windows' worth saturates the pipes, one window's worth shows
         # the latency at a lighter load
-        procs = run[2] if len(run) > 2 else max(1, -(-W * (eng.HOST_PIPES + 1) // T))
-        key = f"T{T}_W{W}" + (f"_P{procs}" if len(run) > 2 else "")
+        procs = run[2] if len(run) > 2 and run[2] else max(1, -(-W * (eng.HOST_PIPES + 1) // T))
+        # T:W[:P[:R:D]]: R ns of work per reported call standing for the NIF's terms + enif_send,
+        # reported by D threads (emqxgm_async_cfg.deliver_threads)
+        rns, dth = (run[3], run[4]) if len(run) > 4 else (0, 0)
+        key = f"T{T}_W{W}" + (f"_P{procs}" if len(run) > 2 and run[2] else "") + \
+            (f"_R{rns}_D{dth}" if len(run) > 4 else "")
         calls = max(2 * procs, min(8_000_000, 100 * W) // T)
-        publishers.run([eng], tb, to, T, procs, min(calls, 4 * procs), W)  # warm-up
+        publishers.run([eng], tb, to, T, procs, min(calls, 4 * procs), W, deliver_threads=dth,
+                       report_ns=rns)  # warm-up
         th0, s0 = _cgroup_throttled(), eng.stats()
-        r = publishers.run([eng], tb, to, T, procs, calls, W)
+        r = publishers.run([eng], tb, to, T, procs, calls, W, deliver_threads=dth, report_ns=rns)
         th1, s1 = _cgroup_throttled(), eng.stats()
         out[key] = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}
         out[key]["processes_per_thread"] = procs

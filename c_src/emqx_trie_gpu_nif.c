@@ -68,7 +68,7 @@ typedef struct {
 
 static ErlNifResourceType *RT, *CALL_RT;
 static ERL_NIF_TERM A_OK, A_ERROR, A_TRUE, A_FALSE, A_MOD, A_ROUTES, A_NONE, A_NODE, A_GROUP, A_SUB,
-    A_SPIN_US, A_BG_BUILD, A_PUBLISH, A_UNDEFINED;
+    A_SPIN_US, A_BG_BUILD, A_PUBLISH, A_UNDEFINED, A_REPORT_THREADS;
 
 static int tab_init(term_tab* t, char* name) {
   t->lk = enif_rwlock_create(name);
@@ -224,16 +224,19 @@ static int opt_uint(ErlNifEnv* env, ERL_NIF_TERM map, ERL_NIF_TERM key, ErlNifSI
  * broker.perf.gpu_match.{devices, batch_max, batch_window_us, max_levels} (src/
  * emqx_trie_gpu_schema.erl): one engine per device, windows of WindowTopics topics.  Opts:
  * #{spin_us => N (0: a completer blocks at once instead of polling; the default),
- *   bg_build => N (emqxgm_tune "bg_build"), publish => boolean() (a publish_async layer too)} */
+ *   bg_build => N (emqxgm_tune "bg_build"), publish => boolean() (a publish_async layer too),
+ *   report_threads => N (emqxgm_async_cfg.deliver_threads, default 8: a window's calls are
+ *   answered -- terms built, enif_send -- by up to N threads, not by the completer alone)} */
 static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   unsigned ndev, wt, wb, wus, ml;
   ERL_NIF_TERM list = argv[0], head, pub;
-  ErlNifSInt64 spin, bg;
+  ErlNifSInt64 spin, bg, rth;
   (void)argc;
   if (!enif_get_list_length(env, list, &ndev) || ndev == 0 || ndev > GM_MAX_DEVICES ||
       !enif_get_uint(env, argv[1], &wt) || !enif_get_uint(env, argv[2], &wb) ||
       !enif_get_uint(env, argv[3], &wus) || !enif_get_uint(env, argv[4], &ml) ||
-      !opt_uint(env, argv[5], A_SPIN_US, 0, &spin) || !opt_uint(env, argv[5], A_BG_BUILD, 16384, &bg))
+      !opt_uint(env, argv[5], A_SPIN_US, 0, &spin) || !opt_uint(env, argv[5], A_BG_BUILD, 16384, &bg) ||
+      !opt_uint(env, argv[5], A_REPORT_THREADS, 8, &rth) || rth < 0 || rth > 64)
     return enif_make_badarg(env);
   const int publish = enif_get_map_value(env, argv[5], A_PUBLISH, &pub) && pub == A_TRUE;
   gm_res* r = enif_alloc_resource(RT, sizeof(gm_res));
@@ -269,6 +272,7 @@ static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
   ac.window_bytes = wb;
   ac.window_us = wus;
   ac.max_levels = ml;
+  ac.deliver_threads = (uint32_t)rth;
   if (!rc) rc = emqxgm_async_create(r->h, r->nh, &ac, on_window, r, &r->a);
   if (!rc && publish) {
     ac.flags = EMQXGM_ASYNC_PUBLISH;
@@ -859,6 +863,7 @@ static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   A_SUB = enif_make_atom(env, "sub");
   A_SPIN_US = enif_make_atom(env, "spin_us");
   A_BG_BUILD = enif_make_atom(env, "bg_build");
+  A_REPORT_THREADS = enif_make_atom(env, "report_threads");
   A_PUBLISH = enif_make_atom(env, "publish");
   A_UNDEFINED = enif_make_atom(env, "undefined");
   return 0;

@@ -21,6 +21,9 @@ bg_build           16384              ``emqxgm_tune("bg_build")``: full builds o
                                       least this many filters run in the background (r05)
 publish            true               a publish layer (``EMQXGM_ASYNC_PUBLISH``) beside the match one
 spin_us            0                  ``emqxgm_tune("spin_us")``: completer threads block at once
+report_threads     8                  ``emqxgm_async_cfg.deliver_threads``: a window's calls are
+                                      answered by up to this many threads (the NIF's per-call
+                                      terms and enif_send), not by one completer per GPU
 timeout_ms         5000               a publisher's wait before it cancels and takes the
                                       reference's match (src/emqx_trie_gpu.erl)
 resync_interval_ms (role)             period of the mirror's full resync (``emqxgm_route_sync_begin``
@@ -46,6 +49,7 @@ class GpuMatchConfig:
     bg_build: int = 16384
     publish: bool = True
     spin_us: int = 0
+    report_threads: int = 8
     timeout_ms: int = 5000
     resync_interval_ms: Optional[int] = None  # None: by the node's mria role
 
@@ -78,6 +82,7 @@ class GpuMatchConfig:
         if self.resync_interval_ms is not None:
             rng("resync_interval_ms", self.resync_interval_ms, 0, 86_400_000)
         rng("bg_build", self.bg_build, 0, 1 << 62)
+        rng("report_threads", self.report_threads, 0, 64)
         rng("spin_us", self.spin_us, 0, 1_000_000)
         if not isinstance(self.publish, bool):
             raise ValueError("broker.perf.gpu_match.publish: expected a boolean")
@@ -91,7 +96,8 @@ class GpuMatchConfig:
     def async_kwargs(self) -> Dict[str, int]:
         """``emqxgm_async_cfg`` fields (emqx_amd.AsyncMatcher keywords)."""
         return {"window_topics": self.batch_max, "window_bytes": 64 * self.batch_max,
-                "window_us": self.batch_window_us, "max_levels": self.max_levels}
+                "window_us": self.batch_window_us, "max_levels": self.max_levels,
+                "deliver_threads": self.report_threads}
 
     def batcher_kwargs(self) -> Dict[str, int]:
         """``emqxgm_batcher_cfg`` fields (emqx_amd.Batcher keywords: the single-driver batcher

@@ -55,6 +55,10 @@ enum SlotState { FREE, OPEN, READY, SUBMITTING, INFLIGHT, DELIVERING };
 constexpr uint32_t SEAL = 1u << 31;        // calls a seal adds: every later reservation fails
 constexpr uint32_t CHUNK_CALLS = 64;       // a thread's staging chunk (at most: a window's size)
 constexpr uint32_t CHUNK_BYTES = 4096;
+#ifndef GM_DELIVER_MIN
+#define GM_DELIVER_MIN 1024  // (the host harness builds with a small value to split small windows)
+#endif
+constexpr uint32_t DELIVER_MIN = GM_DELIVER_MIN;  // calls per part of a window the pool reports
 
 static_assert(sizeof(std::atomic<uint64_t>) == sizeof(uint64_t), "tags are read as uint64_t");
 
@@ -150,6 +154,65 @@ struct emqxgm_async {
   std::vector<std::vector<uint64_t>> rf_off;
   bool publish_mode() const { return (cfg.flags & EMQXGM_ASYNC_PUBLISH) != 0; }
   uint64_t st_windows = 0, st_cancelled = 0, st_errors = 0, st_delivered = 0;
+
+  // ---- delivery: cfg.deliver_threads > 1 splits a large window's reports over a pool (the
+  // caller's per-call work -- the NIF builds each call's terms and enif_sends them -- would
+  // otherwise run on the one completer thread of the handle and bound the layer's rate) ----
+  struct Part {
+    emqxgm_async_window w;          // a view of calls [i0, i1) of the window
+    std::atomic<uint32_t>* left;    // parts of the window not yet reported
+  };
+  std::vector<std::thread> dpool;
+  std::mutex dmu;
+  std::condition_variable dcv, ddone;
+  std::deque<Part> dq;
+  bool dstop = false;
+
+  static emqxgm_async_window part_view(const emqxgm_async_window& w, uint32_t i0, uint32_t i1) {
+    emqxgm_async_window v = w;
+    v.n = i1 - i0;
+    v.tag = w.tag + i0;
+    v.owner = w.owner + i0;
+    if (w.row) v.row = w.row + i0;  // (pair indices stay absolute)
+    if (w.exact_id) v.exact_id = w.exact_id + i0;
+    if (w.route_ptr) v.route_ptr = w.route_ptr + i0;
+    if (w.deliver_ptr) v.deliver_ptr = w.deliver_ptr + i0;
+    return v;
+  }
+
+  void deliver_loop() {
+    std::unique_lock<std::mutex> g(dmu);
+    for (;;) {
+      while (dq.empty() && !dstop) dcv.wait(g);
+      if (dq.empty()) return;
+      Part pt = dq.front();
+      dq.pop_front();
+      g.unlock();
+      cb(user, &pt.w);
+      g.lock();
+      if (pt.left->fetch_sub(1) == 1) ddone.notify_all();
+    }
+  }
+
+  // Reports window w: in parts over the pool when it is large, the completer taking one part.
+  void deliver(const emqxgm_async_window& w) {
+    const uint32_t k = std::min<uint32_t>((uint32_t)dpool.size() + 1, w.n / DELIVER_MIN);
+    if (k <= 1 || w.status) {
+      cb(user, &w);
+      return;
+    }
+    std::atomic<uint32_t> left{k - 1};
+    {
+      std::lock_guard<std::mutex> g(dmu);
+      for (uint32_t p = 1; p < k; ++p)
+        dq.push_back(Part{part_view(w, (uint32_t)((uint64_t)w.n * p / k), (uint32_t)((uint64_t)w.n * (p + 1) / k)), &left});
+    }
+    dcv.notify_all();
+    const emqxgm_async_window v0 = part_view(w, 0, (uint32_t)((uint64_t)w.n / k));
+    cb(user, &v0);
+    std::unique_lock<std::mutex> g(dmu);
+    ddone.wait(g, [&] { return left.load() == 0; });
+  }
 
   // Seals slot si (with mu held): no reservation after this one succeeds; the window goes to the
   // ready queue (the flusher submits it once its reservations settled).
@@ -481,7 +544,7 @@ struct emqxgm_async {
       w.first_ns = s.first_ns.load(std::memory_order_relaxed);
       w.flush_ns = s.flush_ns;
       w.done_ns = done;
-      cb(user, &w);
+      deliver(w);
       g.lock();
       st_delivered += s.n;
       if (rc) st_errors += 1;
@@ -512,7 +575,7 @@ int emqxgm_async_create(emqxgm_t* const* hs, uint32_t n_handles, const emqxgm_as
   if (!a->cfg.window_us) a->cfg.window_us = 50;
   if (!a->cfg.queued_windows) a->cfg.queued_windows = 2;
   if (a->cfg.window_topics >= SEAL || a->cfg.window_bytes >= SEAL ||
-      (a->cfg.flags & ~EMQXGM_ASYNC_PUBLISH)) {
+      (a->cfg.flags & ~EMQXGM_ASYNC_PUBLISH) || a->cfg.deliver_threads > 64) {
     delete a;
     return -EINVAL;
   }
@@ -562,6 +625,7 @@ int emqxgm_async_create(emqxgm_t* const* hs, uint32_t n_handles, const emqxgm_as
     std::lock_guard<std::mutex> g(a->mu);
     a->open_slot();
   }
+  for (uint32_t k = 1; k < a->cfg.deliver_threads; ++k) a->dpool.emplace_back([a] { a->deliver_loop(); });
   a->flusher = std::thread([a] { a->flusher_loop(); });
   for (uint32_t k = 0; k < n_handles; ++k) a->completers.emplace_back([a, k] { a->completer_loop(k); });
   *out = a;
@@ -577,6 +641,12 @@ void emqxgm_async_destroy(emqxgm_async_t* a) {
   }
   a->flusher.join();  // drains the chunks, seals and submits what is left, wakes the completers
   for (auto& t : a->completers) t.join();  // deliver every accepted call
+  {
+    std::lock_guard<std::mutex> g(a->dmu);
+    a->dstop = true;
+  }
+  a->dcv.notify_all();
+  for (auto& t : a->dpool) t.join();
   const uint32_t H = (uint32_t)a->hs.size();
   for (size_t i = 0; i < a->slots.size(); ++i) {
     emqxgm_host_free(a->hs[i % H], a->slots[i]->bytes);

@@ -74,7 +74,7 @@ class _AsyncCfg(C.Structure):
     _fields_ = [("window_topics", C.c_uint32), ("window_bytes", C.c_uint32),
                 ("window_us", C.c_uint32), ("max_levels", C.c_uint32),
                 ("queued_windows", C.c_uint32), ("flags", C.c_uint32),
-                ("reserved", C.c_uint32 * 2)]
+                ("deliver_threads", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 ASYNC_PUBLISH = 1  # EMQXGM_ASYNC_PUBLISH
@@ -829,7 +829,7 @@ class AsyncMatcher:
 
     def __init__(self, engines: Sequence[Engine], callback=None, window_topics: int = 0,
                  window_bytes: int = 0, window_us: int = 0, max_levels: int = 0,
-                 queued_windows: int = 0, publish: bool = False):
+                 queued_windows: int = 0, publish: bool = False, deliver_threads: int = 0):
         import threading
         self._engines = list(engines)  # kept alive: the layer uses their handles
         self._lib = self._engines[0]._lib
@@ -874,7 +874,7 @@ class AsyncMatcher:
                     self._cv.notify_all()
         self._cb = ASYNC_CB(on_window)  # kept alive as long as the layer
         cfg = _AsyncCfg(window_topics, window_bytes, window_us, max_levels, queued_windows,
-                        ASYNC_PUBLISH if publish else 0)
+                        ASYNC_PUBLISH if publish else 0, deliver_threads)
         arr = (C.c_void_p * len(self._engines))(*[e._h for e in self._engines])
         a = C.c_void_p()
         self._engines[0]._check(self._lib.emqxgm_async_create(arr, len(self._engines), C.byref(cfg),

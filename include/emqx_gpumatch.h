@@ -488,7 +488,14 @@ typedef struct emqxgm_async_cfg {
   uint32_t queued_windows; /* full windows that may wait for a pipe (0 = 2) */
   uint32_t flags;          /* EMQXGM_ASYNC_PUBLISH: windows are answered with the publish
                               fan-out (emqxgm_publish_batch) instead of trie rows */
-  uint32_t reserved[2];
+  uint32_t deliver_threads;/* 0 or 1: each completer calls cb once per window; k > 1: a window
+                              of at least 2,048 calls is reported in up to k parts of >= 1,024
+                              calls, `cb` running concurrently on the completer and k - 1 pool
+                              threads (a view per part: n, tag, owner, row / exact_id /
+                              route_ptr / deliver_ptr offset to the part; pair and entry indices
+                              stay absolute).  For a caller whose per-call report is costly (the
+                              NIF: terms + enif_send), so one thread does not bound the rate */
+  uint32_t reserved;
 } emqxgm_async_cfg;
 #define EMQXGM_ASYNC_PUBLISH 1u
 typedef struct emqxgm_async_window {

@@ -20,6 +20,8 @@
 %%   spin_us             -> emqxgm_tune(h, "spin_us"): a completer thread polls a window's pass
 %%                          this long before it blocks (0: block at once -- no core taken from the
 %%                          schedulers; ADVICE r04)
+%%   report_threads      -> emqxgm_async_cfg.deliver_threads: a window's calls are answered (terms,
+%%                          enif_send) by up to this many threads, not by one completer per GPU
 %%   timeout_ms          -> how long a publisher waits for the device before it cancels and takes
 %%                          the reference's path
 %%   resync_interval_ms  -> period of emqx_trie_gpu_sync's full resync (emqxgm_route_sync_*);
@@ -46,6 +48,7 @@ fields("gpu_match") ->
         {"bg_build", hoconsc:mk(non_neg_integer(), #{default => 16384})},
         {"publish", hoconsc:mk(boolean(), #{default => true})},
         {"spin_us", hoconsc:mk(range(0, 1000000), #{default => 0})},
+        {"report_threads", hoconsc:mk(range(0, 64), #{default => 8})},
         {"timeout_ms", hoconsc:mk(range(1, 600000), #{default => 5000})},
         {"resync_interval_ms", hoconsc:mk(range(0, 86400000), #{required => false})}
     ].

@@ -90,6 +90,7 @@ open(Index) ->
             Opts = #{
                 spin_us => ?CONF(spin_us, 0),
                 bg_build => ?CONF(bg_build, 16384),
+                report_threads => ?CONF(report_threads, 8),
                 publish => Index =:= route andalso ?CONF(publish, true)
             },
             case

@@ -70,12 +70,12 @@ struct Load {
   uint32_t* out_count = nullptr;
   uint64_t* out_hash = nullptr;
   uint8_t* out_exact = nullptr;
+  uint32_t report_ns = 0;                 // per call: work standing for the NIF's terms + enif_send
   std::atomic<uint64_t> reported{0}, failed{0};
 };
 
 void on_window(void* user, const emqxgm_async_window* w) {
   Load* L = (Load*)user;
-  const uint64_t now = mono_ns();
   // reports per publisher thread, released once per window (one wake-up, not one per call)
   thread_local std::vector<uint32_t> done;
   done.assign(L->threads, 0);
@@ -92,7 +92,12 @@ void on_window(void* user, const emqxgm_async_window* w) {
       L->out_hash[c] = h;
       L->out_exact[c] = w->exact_id[i] != EMQXGM_NONE;
     }
-    L->lat_us[c] = (uint32_t)std::min<uint64_t>((now - L->t0[c]) / 1000, 0xFFFFFFFFu);
+    if (L->report_ns) {  // a model of the NIF's per-call report (built terms, a message send)
+      const uint64_t until = mono_ns() + L->report_ns;
+      while (mono_ns() < until) {
+      }
+    }
+    L->lat_us[c] = (uint32_t)std::min<uint64_t>((mono_ns() - L->t0[c]) / 1000, 0xFFFFFFFFu);
     done[w->owner[i]] += 1;
   }
   uint64_t total = 0;
@@ -117,7 +122,7 @@ int async_load_run(emqxgm_t* const* hs, uint32_t nh, const emqxgm_async_cfg* cfg
                    const uint8_t* tb, const uint64_t* toff, uint64_t n_topics, uint32_t threads,
                    uint32_t procs, uint64_t calls_per_thread, uint32_t* out_topic,
                    uint32_t* out_count, uint64_t* out_hash, uint8_t* out_exact,
-                   double* out_stats) {
+                   double* out_stats, uint32_t report_ns) {
   if (!hs || !nh || !tb || !toff || !n_topics || !threads || !procs || !out_stats) return -EINVAL;
   Load L;
   const uint64_t total = (uint64_t)threads * calls_per_thread;
@@ -130,6 +135,7 @@ int async_load_run(emqxgm_t* const* hs, uint32_t nh, const emqxgm_async_cfg* cfg
   L.out_count = out_count;
   L.out_hash = out_hash;
   L.out_exact = out_exact;
+  L.report_ns = report_ns;
   emqxgm_async_t* a = nullptr;
   int rc = emqxgm_async_create(hs, nh, cfg, on_window, &L, &a);
   if (rc) return rc;

@@ -28,7 +28,8 @@ def _build(name, cxx, flags):
     if os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in DEPS):
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    r = subprocess.run([cxx, "-std=c++17", "-O1", "-g", "-pthread"] + flags + SRCS + ["-o", out],
+    r = subprocess.run([cxx, "-std=c++17", "-O1", "-g", "-pthread", "-DGM_DELIVER_MIN=4"] + flags + SRCS +
+                       ["-o", out],
                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     assert r.returncode == 0, r.stdout[-4000:]
     return out

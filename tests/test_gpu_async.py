@@ -230,14 +230,17 @@ def _check_load(r, want):
     assert bad.size == 0, (bad[:10], t[bad[:10]])
 
 
-@pytest.mark.parametrize("threads,window", [(16, 4096), (64, 16384)])
-def test_async_load_cfg1_every_call(emqx, threads, window):
+@pytest.mark.parametrize("threads,window,deliver", [(16, 4096, 0), (64, 16384, 0), (16, 16384, 8)])
+def test_async_load_cfg1_every_call(emqx, threads, window, deliver):
+    """deliver: the layer's report pool (emqxgm_async_cfg.deliver_threads): a window's calls
+    reported in parts by several threads, each part's view offset into the window's result."""
     from workloads import publishers
     w, (eng,) = _cfg1(emqx, nt=100_000)
     want = _oracle_rows(w)
     procs = max(1, window * 4 // threads)
     r = publishers.run([eng], w.tbytes, w.toff.astype(np.uint64), threads, procs,
-                       max(2 * procs, 300_000 // threads), window, record=True)
+                       max(2 * procs, 300_000 // threads), window, record=True,
+                       deliver_threads=deliver, report_ns=200 if deliver else 0)
     _check_load(r, want)
     assert r["windows"] > 0 and r["calls_per_window"] > 1
 

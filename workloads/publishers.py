@@ -31,7 +31,8 @@ def _load():
         lib.async_load_run.restype = C.c_int
         lib.async_load_run.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, C.c_void_p,
-                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_uint32]
         _lib = lib
     return _lib
 
@@ -41,9 +42,12 @@ def _p(a):
 
 
 def run(engines, tbytes, toff, threads: int, procs: int, calls_per_thread: int,
-        window_topics: int, window_us: int = 50, max_levels: int = 0, record: bool = False):
+        window_topics: int, window_us: int = 50, max_levels: int = 0, record: bool = False,
+        deliver_threads: int = 0, report_ns: int = 0):
     """One load run over the engines (one AsyncMatcher-equivalent layer inside the harness).
-    Returns a dict of stats, plus 'topic', 'count', 'hash', 'exact' arrays when record."""
+    Returns a dict of stats, plus 'topic', 'count', 'hash', 'exact' arrays when record.
+    deliver_threads: the layer's report pool (emqxgm_async_cfg); report_ns: a busy wait per
+    reported call standing for the NIF's per-call work (terms, enif_send)."""
     from emqx_amd.engine import _AsyncCfg
     lib = _load()
     tbytes = np.ascontiguousarray(tbytes, np.uint8)
@@ -51,7 +55,7 @@ def run(engines, tbytes, toff, threads: int, procs: int, calls_per_thread: int,
     n_topics = len(toff) - 1
     total = threads * calls_per_thread
     arr = (C.c_void_p * len(engines))(*[e._h for e in engines])
-    cfg = _AsyncCfg(window_topics, 64 * window_topics, window_us, max_levels, 0)
+    cfg = _AsyncCfg(window_topics, 64 * window_topics, window_us, max_levels, 0, 0, deliver_threads)
     topic = count = hsh = exact = None
     if record:
         topic = np.zeros(total, np.uint32)
@@ -61,7 +65,7 @@ def run(engines, tbytes, toff, threads: int, procs: int, calls_per_thread: int,
     st = np.zeros(10, np.float64)
     rc = lib.async_load_run(arr, len(engines), C.byref(cfg), _p(tbytes), _p(toff), n_topics,
                             threads, procs, calls_per_thread, _p(topic), _p(count), _p(hsh),
-                            _p(exact), _p(st))
+                            _p(exact), _p(st), report_ns)
     if rc:
         raise RuntimeError(f"async_load_run failed: {rc}")
     out = {"seconds": float(st[0]), "calls": int(st[1]), "topics_per_s": float(st[1] / st[0]),
