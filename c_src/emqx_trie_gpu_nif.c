@@ -713,6 +713,40 @@ static ERL_NIF_TERM nif_commit(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
   return enif_make_tuple2(env, A_OK, enif_make_uint64(env, epoch));
 }
 
+/* snapshot_save(Res, Path :: binary()) -> ok | {error, R}: the committed index of engine 0 (every
+ * engine holds the same one) -- emqxgm_snapshot_save.  snapshot_load(Res, Path) -> ok | {error, R}:
+ * into every engine of a fresh resource, before its first resync (emqxgm_snapshot_load: no full
+ * build; the resync then commits only what changed since, as a delta).  The reference rebuilds its
+ * ram_copies route tables from its peers at start (emqx_router.erl:78-92). */
+static int get_path(ErlNifEnv* env, ERL_NIF_TERM t, char* buf, size_t cap) {
+  ErlNifBinary b;
+  if (!enif_inspect_binary(env, t, &b) || b.size == 0 || b.size >= cap || memchr(b.data, 0, b.size)) return 0;
+  memcpy(buf, b.data, b.size);
+  buf[b.size] = 0;
+  return 1;
+}
+
+static ERL_NIF_TERM nif_snapshot_save(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_res* r;
+  char path[4096];
+  (void)argc;
+  if (!get_res(env, argv[0], &r) || !get_path(env, argv[1], path, sizeof path)) return enif_make_badarg(env);
+  const int rc = emqxgm_snapshot_save(r->h[0], path);
+  return rc ? err_term(env, rc) : A_OK;
+}
+
+static ERL_NIF_TERM nif_snapshot_load(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_res* r;
+  char path[4096];
+  (void)argc;
+  if (!get_res(env, argv[0], &r) || !get_path(env, argv[1], path, sizeof path)) return enif_make_badarg(env);
+  for (unsigned k = 0; k < r->nh; ++k) {
+    const int rc = emqxgm_snapshot_load(r->h[k], path);
+    if (rc) return err_term(env, rc);
+  }
+  return A_OK;
+}
+
 /* empty(Res) -> boolean(): emqx_trie:empty/0 (emqx_trie.erl:172-178) of the committed index
  * (an atomic read: never waits for a commit) */
 static ERL_NIF_TERM nif_empty(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
@@ -882,6 +916,8 @@ static ErlNifFunc funcs[] = {
     {"sync_begin", 1, nif_sync_begin, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"sync_end", 2, nif_sync_end, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"commit", 1, nif_commit, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"snapshot_save", 2, nif_snapshot_save, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"snapshot_load", 2, nif_snapshot_load, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"empty", 1, nif_empty, 0},
     {"trie_member", 2, nif_trie_member, 0},
     {"route_member", 2, nif_route_member, 0},

@@ -24,6 +24,8 @@ spin_us            0                  ``emqxgm_tune("spin_us")``: completer thre
 report_threads     8                  ``emqxgm_async_cfg.deliver_threads``: a window's calls are
                                       answered by up to this many threads (the NIF's per-call
                                       terms and enif_send), not by one completer per GPU
+snapshot_dir       (none)             ``emqxgm_snapshot_save`` at the mirror's shutdown,
+                                      ``emqxgm_snapshot_load`` at its next start (no full build)
 timeout_ms         5000               a publisher's wait before it cancels and takes the
                                       reference's match (src/emqx_trie_gpu.erl)
 resync_interval_ms (role)             period of the mirror's full resync (``emqxgm_route_sync_begin``
@@ -50,6 +52,7 @@ class GpuMatchConfig:
     publish: bool = True
     spin_us: int = 0
     report_threads: int = 8
+    snapshot_dir: Optional[str] = None
     timeout_ms: int = 5000
     resync_interval_ms: Optional[int] = None  # None: by the node's mria role
 

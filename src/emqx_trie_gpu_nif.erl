@@ -16,6 +16,8 @@
     sync_begin/1,
     sync_end/2,
     commit/1,
+    snapshot_save/2,
+    snapshot_load/2,
     empty/1,
     trie_member/2,
     route_member/2,
@@ -58,6 +60,10 @@ register(_Res, _Kind, _Items) -> ?NOT_LOADED.
 set_local_node(_Res, _NodeH) -> ?NOT_LOADED.
 %% sync_begin(Res) -> {ok, Gen}
 sync_begin(_Res) -> ?NOT_LOADED.
+%% snapshot_save(Res, Path :: binary()) -> ok | {error, Reason}: the committed index to a file
+snapshot_save(_Res, _Path) -> ?NOT_LOADED.
+%% snapshot_load(Res, Path :: binary()) -> ok | {error, Reason}: into a fresh resource, no build
+snapshot_load(_Res, _Path) -> ?NOT_LOADED.
 %% sync_end(Res, Gen) -> {ok, Removed}
 sync_end(_Res, _Gen) -> ?NOT_LOADED.
 %% commit(Res) -> {ok, Epoch}

@@ -22,6 +22,8 @@
 %%                          schedulers; ADVICE r04)
 %%   report_threads      -> emqxgm_async_cfg.deliver_threads: a window's calls are answered (terms,
 %%                          enif_send) by up to this many threads, not by one completer per GPU
+%%   snapshot_dir        -> emqxgm_snapshot_save at the mirror's shutdown, emqxgm_snapshot_load at
+%%                          its next start (no full build; the resync commits the difference)
 %%   timeout_ms          -> how long a publisher waits for the device before it cancels and takes
 %%                          the reference's path
 %%   resync_interval_ms  -> period of emqx_trie_gpu_sync's full resync (emqxgm_route_sync_*);
@@ -49,6 +51,7 @@ fields("gpu_match") ->
         {"publish", hoconsc:mk(boolean(), #{default => true})},
         {"spin_us", hoconsc:mk(range(0, 1000000), #{default => 0})},
         {"report_threads", hoconsc:mk(range(0, 64), #{default => 8})},
+        {"snapshot_dir", hoconsc:mk(string(), #{required => false})},
         {"timeout_ms", hoconsc:mk(range(1, 600000), #{default => 5000})},
         {"resync_interval_ms", hoconsc:mk(range(0, 86400000), #{required => false})}
     ].

@@ -35,7 +35,7 @@
 -include_lib("emqx/include/emqx.hrl").
 
 -export([start_link/1, table/1, repair/1]).
--export([init/1, handle_continue/2, handle_call/3, handle_cast/2, handle_info/2]).
+-export([init/1, handle_continue/2, handle_call/3, handle_cast/2, handle_info/2, terminate/2]).
 
 -define(CHUNK, 65536).       %% distinct topics per resync call
 -define(BATCH, 65536).       %% table events per device call
@@ -63,12 +63,16 @@ repair(Index) ->
 init(Index) ->
     %% a restarted mirror: publishers take the reference's path until its resync is committed
     %% (the handles table died with the old process)
+    process_flag(trap_exit, true),
     ok = emqx_trie_gpu:publish(Index, undefined),
     {ok, #{index => Index, h => undefined, tab => table(Index)}, {continue, open}}.
 
 handle_continue(open, S = #{index := Index, tab := Tab}) ->
     case open(Index) of
-        {ok, H} ->
+        {ok, H, Fresh} ->
+            %% fresh engines start from the last snapshot, when there is one: no full build,
+            %% the resync below commits what changed since as a delta
+            _ = Fresh andalso load_snapshot(Index, H),
             {ok, _} = mnesia:subscribe({table, Tab, simple}),
             S1 = S#{h := H},
             ok = prepare(Index, H),
@@ -105,13 +109,42 @@ open(Index) ->
             of
                 {ok, H} ->
                     persistent_term:put({emqx_trie_gpu, {engines, Index}}, H),
-                    {ok, H};
+                    {ok, H, true};
                 Error ->
                     Error
             end;
         H ->
-            {ok, H}
+            {ok, H, false}
     end.
+
+%% broker.perf.gpu_match.snapshot_dir: the index of each table saved there at shutdown and loaded
+%% at the next start (emqxgm_snapshot_save / _load)
+snapshot_path(Index) ->
+    case ?CONF(snapshot_dir, undefined) of
+        undefined -> undefined;
+        Dir -> iolist_to_binary(filename:join(Dir, ["emqx_trie_gpu.", atom_to_list(Index), ".snap"]))
+    end.
+
+load_snapshot(Index, H) ->
+    case snapshot_path(Index) of
+        undefined ->
+            ok;
+        Path ->
+            case filelib:is_regular(Path) andalso emqx_trie_gpu_nif:snapshot_load(H, Path) of
+                ok -> ok;
+                false -> ok;
+                %% a snapshot of another configuration: the resync's full build instead
+                {error, _} -> ok
+            end
+    end.
+
+terminate(_Reason, #{index := Index, h := H}) when H =/= undefined ->
+    case snapshot_path(Index) of
+        undefined -> ok;
+        Path -> _ = emqx_trie_gpu_nif:snapshot_save(H, Path), ok
+    end;
+terminate(_Reason, _S) ->
+    ok.
 
 %% the engines' knobs; for the route index the handle registry (node(), the dest and subscriber
 %% handles made so far) -- from here on every new handle is registered as it is made
