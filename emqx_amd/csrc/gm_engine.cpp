@@ -3530,6 +3530,9 @@ int emqxgm_snapshot_load(emqxgm_t* h, const char* path) {
     set_err(h, "snapshot corrupt: " + why);
     return -EINVAL;
   }
+  // a resync generation belongs to the handle that ran it: a loaded handle's first resync must
+  // not take the saved marks for its own (it would keep every key the table lost meanwhile)
+  for (Filter& f : filters) f.sync_gen = 0;
   {
     std::unique_lock<std::shared_mutex> pg(h->pmu);
     h->pool.swap(pool);

@@ -61,8 +61,7 @@ class RouteTableMirror:
         self.handles = Handles()
         self.chunk = chunk
         self.queue: Deque[Tuple[str, bytes]] = deque()  # the process's mailbox of table events
-        for e in self.engines:
-            e.set_local_node(self.handles("node", local_node))
+        self.local = self.handles("node", local_node)  # set on the engines by init()
 
     # -- mnesia table events: {write, Route, _} / {delete_object, Route, _} / {delete, {Tab, T}, _}
     def event(self, kind: str, topic: bytes) -> None:
@@ -115,8 +114,26 @@ class RouteTableMirror:
         for e in self.engines:
             e.commit()
 
-    def init(self) -> None:
-        """handle_continue(open): (subscribed first,) one full resync, then the first commit;
-        the index is published only after it."""
+    def init(self, snapshot: Optional[str] = None) -> None:
+        """handle_continue(open): fresh engines start from `snapshot` (broker.perf.gpu_match.
+        snapshot_dir) when there is one -- no full build --, then (subscribed first,) one full
+        resync and the first commit, which is then a delta of what changed since the save; the
+        index is published only after it."""
+        if snapshot is not None:
+            import os
+            if os.path.isfile(snapshot):
+                for e in self.engines:
+                    try:
+                        e.snapshot_load(snapshot)
+                    except Exception:  # another configuration's snapshot: the resync builds
+                        pass
+        # prepare/2: the local node after the load (it makes the engines dirty, and a snapshot
+        # loads into fresh engines only)
+        for e in self.engines:
+            e.set_local_node(self.local)
         self.resync()
         self.commit()
+
+    def save(self, snapshot: str) -> None:
+        """terminate/2: the committed index to `snapshot` (engine 0: they all hold the same)."""
+        self.engines[0].snapshot_save(snapshot)

@@ -234,3 +234,43 @@ def test_random_churn_interleavings(fakelib, seed, engines):
     m.commit()
     for e in engs:
         _check(e, rt, topics)
+
+
+def test_restart_from_snapshot_commits_a_delta(fakelib, tmp_path):
+    """broker.perf.gpu_match.snapshot_dir: the mirror saves its index at shutdown (terminate/2),
+    and fresh engines start from it (emqxgm_snapshot_load, no full build); the first resync then
+    commits only what changed while the node was down -- as a delta -- and the committed state
+    is the table's."""
+    rng = random.Random(11)
+    rt = R.Router()
+    topics = [b"s/%d/+" % i for i in range(300)] + [b"k/%d" % i for i in range(300)]
+    for t in topics:
+        rt.add_route(t, rng.choice(["n1", "n2"]))
+    eng = _engine(fakelib)
+    m = RouteTableMirror([eng], rt)
+    m.init()
+    _check(eng, rt, topics)
+    snap = str(tmp_path / "emqx_trie_gpu.route.snap")
+    m.save(snap)
+    eng.close()
+    # while "down"
+    for t in rng.sample(topics, 40):
+        for d in ("n1", "n2"):
+            rt.delete_route(t, d)
+    new = [b"z/%d/#" % i for i in range(25)]
+    for t in new:
+        rt.add_route(t, "n3")
+    eng2 = _engine(fakelib)
+    f0 = eng2.stats()["full_commits"]
+    m2 = RouteTableMirror([eng2], rt)
+    m2.init(snapshot=snap)
+    st = eng2.stats()
+    # the load publishes the saved index (one epoch from the model, no build); the resync's
+    # commit is a delta (the 40 keys gone, the 25 new ones)
+    assert st["full_commits"] == f0 + 1 and st["delta_commits"] >= 1, st
+    _check(eng2, rt, topics + new)
+    # a missing snapshot: the resync's full build
+    eng3 = _engine(fakelib)
+    m3 = RouteTableMirror([eng3], rt)
+    m3.init(snapshot=str(tmp_path / "none.snap"))
+    _check(eng3, rt, topics + new)
