@@ -76,6 +76,7 @@ struct Load {
 
 void on_window(void* user, const emqxgm_async_window* w) {
   Load* L = (Load*)user;
+  const uint64_t now0 = mono_ns();  // (one clock read per window unless each report costs time)
   // reports per publisher thread, released once per window (one wake-up, not one per call)
   thread_local std::vector<uint32_t> done;
   done.assign(L->threads, 0);
@@ -97,7 +98,8 @@ void on_window(void* user, const emqxgm_async_window* w) {
       while (mono_ns() < until) {
       }
     }
-    L->lat_us[c] = (uint32_t)std::min<uint64_t>((mono_ns() - L->t0[c]) / 1000, 0xFFFFFFFFu);
+    const uint64_t now = L->report_ns ? mono_ns() : now0;
+    L->lat_us[c] = (uint32_t)std::min<uint64_t>((now - L->t0[c]) / 1000, 0xFFFFFFFFu);
     done[w->owner[i]] += 1;
   }
   uint64_t total = 0;
