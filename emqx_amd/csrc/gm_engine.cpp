@@ -696,7 +696,14 @@ int dev_upload(emqxgm* h, std::vector<DevBuf>& keep, const std::vector<T>& v, co
   b.bytes = std::max<size_t>(sizeof(T), v.size() * sizeof(T));
   HIPCHK(h, hipMalloc(&b.p, b.bytes));
   keep.push_back(b);
-  if (!v.empty()) HIPCHK(h, hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  // in 64-MiB pieces: a background build uploads gigabytes, and the small copies of the commits
+  // and passes running meanwhile queue on the same copy engines -- between pieces, not behind
+  // a whole table
+  constexpr size_t PIECE = 64ull << 20;
+  const size_t total = v.size() * sizeof(T);
+  for (size_t o = 0; o < total; o += PIECE)
+    HIPCHK(h, hipMemcpy((uint8_t*)b.p + o, (const uint8_t*)v.data() + o, std::min(PIECE, total - o),
+                        hipMemcpyHostToDevice));
   *out = (const T*)b.p;
   return 0;
 }
