@@ -185,10 +185,6 @@ constexpr uint32_t VINL = 60;
 // (tokens past the last level are 0); level tokens from REC_TOKS on are read from the token
 // array at wbase.  Topics have at most 32,768 levels (65,535 bytes).
 constexpr uint32_t REC_U4 = 4;
-#ifndef GM_NT_REC
-#define GM_NT_REC 0  // A/B: topic records written and read non-temporally
-#endif
-typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 constexpr uint32_t REC_TOKS = 7;
 constexpr uint32_t T_WILD = 1u;    // some level is exactly '+' or '#'  -> trie result []
 constexpr uint32_t T_DOLLAR = 2u;  // first byte is '$' -> no root '+'/'#' (emqx_trie.erl:282)
