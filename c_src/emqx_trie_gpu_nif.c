@@ -66,9 +66,9 @@ typedef struct {
   int publish;
 } gm_call;
 
-static ErlNifResourceType *RT, *CALL_RT;
+static ErlNifResourceType *RT, *CALL_RT, *RETAIN_RT;
 static ERL_NIF_TERM A_OK, A_ERROR, A_TRUE, A_FALSE, A_MOD, A_ROUTES, A_NONE, A_NODE, A_GROUP, A_SUB,
-    A_SPIN_US, A_BG_BUILD, A_PUBLISH, A_UNDEFINED, A_REPORT_THREADS;
+    A_SPIN_US, A_BG_BUILD, A_PUBLISH, A_UNDEFINED, A_REPORT_THREADS, A_EQ, A_WORDS, A_BINARY;
 
 static int tab_init(term_tab* t, char* name) {
   t->lk = enif_rwlock_create(name);
@@ -879,12 +879,216 @@ static ERL_NIF_TERM nif_stats(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
   return m;
 }
 
+/* ---- the retainer's reverse match and the ordered topic rules ------------
+ * emqx_retainer_mnesia keeps its messages; its topics (with their expiry) are mirrored into an
+ * emqxgm_retain_t store, and match_messages/3 (emqx_retainer_mnesia.erl:185-195) asks the device
+ * for the stored topics a batch of filters selects (search_table/3's set, :300-330); the caller
+ * reads the messages of those topics from its own table.  emqx_authz_rule:match_topics/3 and
+ * emqx_rewrite:match_and_rewrite/3 keep their rule lists; match_rules/3 returns per name the
+ * index of the first matching rule (emqxgm_match_rules). */
+typedef struct {
+  emqxgm_retain_t* r;
+  ErlNifMutex* mu; /* the store is single-writer; matches read its committed state */
+} gm_retain;
+
+static void gm_retain_dtor(ErlNifEnv* env, void* obj) {
+  gm_retain* g = (gm_retain*)obj;
+  (void)env;
+  if (g->r) emqxgm_retain_destroy(g->r);
+  if (g->mu) enif_mutex_destroy(g->mu);
+}
+
+static int get_retain(ErlNifEnv* env, ERL_NIF_TERM t, gm_retain** g) {
+  return enif_get_resource(env, t, RETAIN_RT, (void**)g) && (*g)->r;
+}
+
+/* retain_open(Device, IndexSpecs :: [[Pos]]) -> {ok, R} | {error, Reason}
+ * (retainer.backend.index_specs, emqx_retainer_schema.erl:24-29; [] = the full scan only) */
+static ERL_NIF_TERM nif_retain_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  int dev;
+  unsigned ns;
+  (void)argc;
+  if (!enif_get_int(env, argv[0], &dev) || !enif_get_list_length(env, argv[1], &ns) || ns > 64)
+    return enif_make_badarg(env);
+  uint32_t pos[64 * 16], off[65];
+  ERL_NIF_TERM l = argv[1], spec;
+  unsigned np = 0;
+  off[0] = 0;
+  for (unsigned i = 0; i < ns; ++i) {
+    ERL_NIF_TERM sl, ph;
+    if (!enif_get_list_cell(env, l, &spec, &l)) return enif_make_badarg(env);
+    for (sl = spec; enif_get_list_cell(env, sl, &ph, &sl);) {
+      unsigned v;
+      if (np >= 64 * 16 || !enif_get_uint(env, ph, &v)) return enif_make_badarg(env);
+      pos[np++] = v;
+    }
+    off[i + 1] = np;
+  }
+  gm_retain* g = enif_alloc_resource(RETAIN_RT, sizeof(gm_retain));
+  memset(g, 0, sizeof *g);
+  g->mu = enif_mutex_create("emqx_trie_gpu.retain");
+  int rc = g->mu ? emqxgm_retain_create(dev, &g->r) : -ENOMEM;
+  if (!rc) rc = emqxgm_retain_set_indices(g->r, pos, off, ns);
+  if (rc) {
+    enif_release_resource(g);
+    return rc == -EINVAL ? enif_make_badarg(env) : err_term(env, rc);
+  }
+  ERL_NIF_TERM t = enif_make_resource(env, g);
+  enif_release_resource(g);
+  return enif_make_tuple2(env, A_OK, t);
+}
+
+/* retain_store(R, Topic, ExpiryMs) -> ok (store_retained/2, :138-152; 0 = never expires),
+ * retain_delete(R, Topic) -> ok (delete_message/2, :166-170), retain_clean(R) -> ok (clean/1),
+ * retain_commit(R) -> ok: the mutations visible to retain_match/3 */
+static ERL_NIF_TERM nif_retain_store(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_retain* g;
+  ErlNifBinary b;
+  ErlNifUInt64 exp;
+  uint32_t id;
+  (void)argc;
+  if (!get_retain(env, argv[0], &g) || !enif_inspect_binary(env, argv[1], &b) ||
+      !enif_get_uint64(env, argv[2], &exp))
+    return enif_make_badarg(env);
+  if (b.size > GM_MAX_TOPIC) return err_term(env, -E2BIG);
+  enif_mutex_lock(g->mu);
+  const int rc = emqxgm_retain_store(g->r, b.data, (uint32_t)b.size, exp, &id);
+  enif_mutex_unlock(g->mu);
+  return rc ? err_term(env, rc) : A_OK;
+}
+
+static ERL_NIF_TERM nif_retain_delete(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_retain* g;
+  ErlNifBinary b;
+  (void)argc;
+  if (!get_retain(env, argv[0], &g) || !enif_inspect_binary(env, argv[1], &b)) return enif_make_badarg(env);
+  if (b.size > GM_MAX_TOPIC) return A_OK; /* never stored */
+  enif_mutex_lock(g->mu);
+  const int rc = emqxgm_retain_delete(g->r, b.data, (uint32_t)b.size);
+  enif_mutex_unlock(g->mu);
+  return rc ? err_term(env, rc) : A_OK;
+}
+
+static ERL_NIF_TERM nif_retain_clean(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_retain* g;
+  (void)argc;
+  if (!get_retain(env, argv[0], &g)) return enif_make_badarg(env);
+  enif_mutex_lock(g->mu);
+  const int rc = emqxgm_retain_clean(g->r);
+  enif_mutex_unlock(g->mu);
+  return rc ? err_term(env, rc) : A_OK;
+}
+
+static ERL_NIF_TERM nif_retain_commit(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_retain* g;
+  (void)argc;
+  if (!get_retain(env, argv[0], &g)) return enif_make_badarg(env);
+  enif_mutex_lock(g->mu);
+  const int rc = emqxgm_retain_commit(g->r);
+  enif_mutex_unlock(g->mu);
+  return rc ? err_term(env, rc) : A_OK;
+}
+
+/* the packed list with 32-bit offsets (the retainer and rules entry points take those) */
+static uint32_t* off32(const packed* p) {
+  uint32_t* o = enif_alloc(sizeof(uint32_t) * ((size_t)p->n + 1));
+  if (o)
+    for (unsigned i = 0; i <= p->n; ++i) o[i] = (uint32_t)p->off[i];
+  return o;
+}
+
+/* retain_match(R, [Filter], NowMs) -> [[Topic]] | {error, Reason}: match_messages/3 for a batch
+ * of filters -- per filter the stored, live topics it selects (its messages are the caller's) */
+static ERL_NIF_TERM nif_retain_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_retain* g;
+  packed p;
+  ErlNifUInt64 now;
+  (void)argc;
+  if (!get_retain(env, argv[0], &g) || !enif_get_uint64(env, argv[2], &now)) return enif_make_badarg(env);
+  int rc = pack_list(env, argv[1], 0, &p);
+  uint32_t* o = rc ? NULL : off32(&p);
+  if (!rc && !o) rc = -ENOMEM;
+  if (!rc && p.off[p.n] > 0xFFFFFFFFull) rc = -E2BIG;
+  emqxgm_retain_out out;
+  memset(&out, 0, sizeof out);
+  ERL_NIF_TERM res = 0;
+  if (!rc) {
+    enif_mutex_lock(g->mu); /* the result lives in the store's buffers until its next call */
+    rc = emqxgm_retain_match(g->r, p.bytes, o, p.n, now, &out);
+    if (!rc) {
+      res = enif_make_list(env, 0);
+      for (uint32_t i = out.n; i-- > 0;) {
+        ERL_NIF_TERM tl = enif_make_list(env, 0);
+        for (uint64_t j = out.ptr[i + 1]; j-- > out.ptr[i];) {
+          const uint8_t* tp;
+          uint32_t tlen;
+          if (emqxgm_retain_topic(g->r, out.id[j], &tp, &tlen) == 0)
+            tl = enif_make_list_cell(env, bytes_term(env, tp, tlen), tl);
+        }
+        res = enif_make_list_cell(env, tl, res);
+      }
+    }
+    enif_mutex_unlock(g->mu);
+  }
+  enif_free(o);
+  packed_free(&p);
+  if (rc == -EINVAL) return enif_make_badarg(env);
+  return rc ? err_term(env, rc) : res;
+}
+
+/* match_rules(Res, [Name], [{Filter, eq | words | binary}]) -> [Index | none]: the first rule
+ * each name matches (emqx_authz_rule:match_topics/3 with eq / words, emqx_rewrite's binary
+ * match/2; placeholders substituted by the caller), on engine 0's device */
+static ERL_NIF_TERM nif_match_rules(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_res* r;
+  packed nm, ru;
+  (void)argc;
+  if (!get_res(env, argv[0], &r)) return enif_make_badarg(env);
+  int rc = pack_list(env, argv[1], 0, &nm);
+  if (!rc) rc = pack_list(env, argv[2], 1, &ru);
+  else memset(&ru, 0, sizeof ru);
+  uint32_t *no = NULL, *ro = NULL, *fl = NULL, *out = NULL;
+  if (!rc) {
+    no = off32(&nm);
+    ro = off32(&ru);
+    fl = enif_alloc(sizeof(uint32_t) * (ru.n ? ru.n : 1));
+    out = enif_alloc(sizeof(uint32_t) * (nm.n ? nm.n : 1));
+    if (!no || !ro || !fl || !out) rc = -ENOMEM;
+  }
+  if (!rc && (nm.off[nm.n] > 0xFFFFFFFFull || ru.off[ru.n] > 0xFFFFFFFFull)) rc = -E2BIG;
+  ERL_NIF_TERM head, l = argv[2];
+  for (unsigned i = 0; !rc && i < ru.n; ++i) {
+    int ar;
+    const ERL_NIF_TERM* el;
+    enif_get_list_cell(env, l, &head, &l);
+    enif_get_tuple(env, head, &ar, &el);
+    if (ar != 2) rc = -EINVAL;
+    else if (el[1] == A_EQ) fl[i] = EMQXGM_RULE_EQ;
+    else if (el[1] == A_WORDS) fl[i] = EMQXGM_RULE_WORDS;
+    else if (el[1] == A_BINARY) fl[i] = 0;
+    else rc = -EINVAL;
+  }
+  if (!rc) rc = emqxgm_match_rules(r->h[0], nm.bytes, no, nm.n, ru.bytes, ro, fl, ru.n, out);
+  ERL_NIF_TERM res = enif_make_list(env, 0);
+  for (uint32_t i = nm.n; !rc && i-- > 0;)
+    res = enif_make_list_cell(env, out[i] == EMQXGM_NONE ? A_NONE : enif_make_uint(env, out[i]), res);
+  enif_free(no);
+  enif_free(ro);
+  enif_free(fl);
+  enif_free(out);
+  packed_free(&nm);
+  packed_free(&ru);
+  if (rc == -EINVAL) return enif_make_badarg(env);
+  return rc ? err_term(env, rc) : res;
+}
+
 static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   (void)priv;
   (void)info;
   RT = enif_open_resource_type(env, NULL, "emqx_trie_gpu", gm_res_dtor, ERL_NIF_RT_CREATE, NULL);
   CALL_RT = enif_open_resource_type(env, NULL, "emqx_trie_gpu_call", gm_call_dtor, ERL_NIF_RT_CREATE, NULL);
-  if (!RT || !CALL_RT || emqxgm_abi_version() != EMQXGM_ABI_VERSION) return -1;
+  RETAIN_RT = enif_open_resource_type(env, NULL, "emqx_trie_gpu_retain", gm_retain_dtor, ERL_NIF_RT_CREATE, NULL);
+  if (!RT || !CALL_RT || !RETAIN_RT || emqxgm_abi_version() != EMQXGM_ABI_VERSION) return -1;
   A_OK = enif_make_atom(env, "ok");
   A_ERROR = enif_make_atom(env, "error");
   A_TRUE = enif_make_atom(env, "true");
@@ -898,6 +1102,9 @@ static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   A_SPIN_US = enif_make_atom(env, "spin_us");
   A_BG_BUILD = enif_make_atom(env, "bg_build");
   A_REPORT_THREADS = enif_make_atom(env, "report_threads");
+  A_EQ = enif_make_atom(env, "eq");
+  A_WORDS = enif_make_atom(env, "words");
+  A_BINARY = enif_make_atom(env, "binary");
   A_PUBLISH = enif_make_atom(env, "publish");
   A_UNDEFINED = enif_make_atom(env, "undefined");
   return 0;
@@ -926,6 +1133,13 @@ static ErlNifFunc funcs[] = {
     {"cancel", 2, nif_cancel, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"tune", 3, nif_tune, ERL_NIF_DIRTY_JOB_IO_BOUND}, /* some keys drain the passes in flight */
     {"stats", 1, nif_stats, 0},
+    {"retain_open", 2, nif_retain_open, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"retain_store", 3, nif_retain_store, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"retain_delete", 2, nif_retain_delete, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"retain_clean", 1, nif_retain_clean, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"retain_commit", 1, nif_retain_commit, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"retain_match", 3, nif_retain_match, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"match_rules", 3, nif_match_rules, ERL_NIF_DIRTY_JOB_IO_BOUND},
 };
 
 ERL_NIF_INIT(emqx_trie_gpu_nif, funcs, load, NULL, NULL, NULL)

@@ -25,7 +25,14 @@
     publish_async/3,
     cancel/2,
     tune/3,
-    stats/1
+    stats/1,
+    retain_open/2,
+    retain_store/3,
+    retain_delete/2,
+    retain_clean/1,
+    retain_commit/1,
+    retain_match/3,
+    match_rules/3
 ]).
 
 -on_load(init/0).
@@ -60,6 +67,22 @@ register(_Res, _Kind, _Items) -> ?NOT_LOADED.
 set_local_node(_Res, _NodeH) -> ?NOT_LOADED.
 %% sync_begin(Res) -> {ok, Gen}
 sync_begin(_Res) -> ?NOT_LOADED.
+%% ---- the retainer's reverse match (emqx_retainer_mnesia.erl:138-195, 241-247) ----
+%% retain_open(Device, IndexSpecs :: [[pos_integer()]]) -> {ok, R} | {error, Reason}
+retain_open(_Device, _IndexSpecs) -> ?NOT_LOADED.
+%% retain_store(R, Topic, ExpiryMs) -> ok (store_retained/2; 0: never expires)
+retain_store(_R, _Topic, _ExpiryMs) -> ?NOT_LOADED.
+%% retain_delete(R, Topic) -> ok (delete_message/2 of one topic)
+retain_delete(_R, _Topic) -> ?NOT_LOADED.
+%% retain_clean(R) -> ok (clean/1)
+retain_clean(_R) -> ?NOT_LOADED.
+%% retain_commit(R) -> ok: the mutations visible to retain_match/3
+retain_commit(_R) -> ?NOT_LOADED.
+%% retain_match(R, [Filter], NowMs) -> [[Topic]]: match_messages/3 for a batch of filters
+retain_match(_R, _Filters, _NowMs) -> ?NOT_LOADED.
+%% match_rules(Res, [Name], [{Filter, eq | words | binary}]) -> [Index | none]: the first rule
+%% each name matches (emqx_authz_rule:match_topics/3, emqx_rewrite:match_and_rewrite/3)
+match_rules(_Res, _Names, _Rules) -> ?NOT_LOADED.
 %% snapshot_save(Res, Path :: binary()) -> ok | {error, Reason}: the committed index to a file
 snapshot_save(_Res, _Path) -> ?NOT_LOADED.
 %% snapshot_load(Res, Path :: binary()) -> ok | {error, Reason}: into a fresh resource, no build

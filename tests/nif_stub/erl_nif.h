@@ -55,3 +55,6 @@ void* enif_realloc(void*, size_t);
 typedef unsigned long ErlNifTid; typedef struct ErlNifThreadOpts ErlNifThreadOpts;
 int enif_thread_create(char*, ErlNifTid*, void* (*)(void*), void*, ErlNifThreadOpts*);
 int enif_thread_join(ErlNifTid, void**);
+typedef struct ErlNifMutex ErlNifMutex;
+ErlNifMutex* enif_mutex_create(char*); void enif_mutex_destroy(ErlNifMutex*);
+void enif_mutex_lock(ErlNifMutex*); void enif_mutex_unlock(ErlNifMutex*);
