@@ -347,7 +347,8 @@ def test_async_single_long_topic_on_an_idle_layer(emqx):
     am.close()
 
 
-def test_async_publish_layer_every_call(emqx):
+@pytest.mark.parametrize("deliver", [0, 4])
+def test_async_publish_layer_every_call(emqx, deliver):
     """The publish layer (EMQXGM_ASYNC_PUBLISH: the NIF's publish_async/3, emqx_trie_gpu:route/2)
     from 16 threads, one topic a call: every call's aggre/1 entries and local dispatches equal
     oracle.emqx_ref.publish (emqx_broker.erl:218-300, 326-355) for its topic.  The broker state
@@ -372,7 +373,10 @@ def test_async_publish_layer_every_call(emqx):
     eng = emqx.Engine()
     m = RouteTableMirror([eng], rt, subscribers=subs, local_node="n1")
     m.init()
-    am = emqx.AsyncMatcher([eng], window_topics=4096, window_us=100, publish=True)
+    # deliver: the report pool (emqxgm_async_cfg.deliver_threads) -- full windows reported in
+    # parts of >= 1,024 calls, each part's view offset into the window's publish result
+    am = emqx.AsyncMatcher([eng], window_topics=4096, window_us=100, publish=True,
+                           deliver_threads=deliver)
     topics = [w.topic(i) for i in range(w.nt)] + names[:200] + [b"", b"l0w1/+"]
     errors = []
 
@@ -420,3 +424,32 @@ def test_async_publish_layer_every_call(emqx):
     got_e, got_d = check(am.results[(1, 99)], b"hook/7/x")
     assert (b"hook/+/x", "n1") in got_e and (b"hook/+/x", "sub-new") in got_d
     am.close()
+
+
+def test_mirror_restart_from_snapshot(emqx, tmp_path):
+    """broker.perf.gpu_match.snapshot_dir on the GPU: the mirror saves its index, fresh engines
+    start from it, the first resync commits what changed meanwhile as a delta, and match_routes
+    equals the oracle's router afterwards."""
+    rng = random.Random(5)
+    rt = R.Router()
+    topics = [b"site/%d/+/t" % i for i in range(2000)] + [b"k/%d" % i for i in range(2000)]
+    for t in topics:
+        rt.add_route(t, rng.choice(["n1", "n2", ("g", "n1")]))
+    eng = emqx.Engine()
+    m = RouteTableMirror([eng], rt)
+    m.init()
+    snap = str(tmp_path / "emqx_trie_gpu.route.snap")
+    m.save(snap)
+    eng.close()
+    for t in rng.sample(topics, 300):
+        rt.delete_route(t, rt.lookup_routes(t)[0][1])
+    for i in range(100):
+        rt.add_route(b"site/%d/#" % i, "n3")
+    eng2 = emqx.Engine()
+    f0 = eng2.stats()["full_commits"]
+    m2 = RouteTableMirror([eng2], rt)
+    m2.init(snapshot=snap)
+    st = eng2.stats()
+    assert st["full_commits"] == f0 + 1 and st["delta_commits"] >= 1, st
+    probe = [b"site/%d/x/t" % i for i in range(0, 2000, 7)] + [b"k/%d" % i for i in range(0, 2000, 7)]
+    _check_routes(eng2, rt, probe)
