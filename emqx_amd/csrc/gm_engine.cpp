@@ -1776,6 +1776,20 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// EMQXGM_DEBUG_SLOW=<ms>: writer-side steps slower than that are reported on stderr (diagnosis
+// of the subscribe path's tail; off by default)
+double debug_slow_ms() {
+  static const double v = [] {
+    const char* e = getenv("EMQXGM_DEBUG_SLOW");
+    return e ? atof(e) : 0.0;
+  }();
+  return v;
+}
+void debug_slow(const char* what, double ms) {
+  const double lim = debug_slow_ms();
+  if (lim > 0 && ms >= lim) fprintf(stderr, "[emqxgm slow] %s %.1f ms\n", what, ms);
+}
+
 // The registry's committed flags (trie_member, route_member, the next delta's base) follow the
 // published epoch: for the listed filters, or for all.
 void flip_committed(emqxgm* h, const std::vector<uint32_t>* ids) {
@@ -1862,17 +1876,25 @@ void build_thread(emqxgm* h, BuildJob* J) {
   if (const uint32_t d = h->bg_delay_ms.load()) std::this_thread::sleep_for(std::chrono::milliseconds(d));
   std::unique_ptr<BuildJob> spent;
   {
+    const auto tw = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> g(h->wmu);
+    debug_slow("install: waited for the writer lock", ms_since(tw));
+    const auto ti = std::chrono::steady_clock::now();
     h->build_rc = install_build(h, spent);
+    debug_slow("install", ms_since(ti));
     h->builds_done += 1;
     h->bcv.notify_all();
   }
+  const auto tf = std::chrono::steady_clock::now();
   // The replaced host model (tens of millions of entries at cfg3) is freed here, without the
   // writer lock, and so are the replaced device tables once the passes that read them are done
   // -- not by the next subscribe's commit (sweep_graveyard takes only the epoch lock).
   spent.reset();
+  debug_slow("free the replaced model", ms_since(tf));
+  const auto ts = std::chrono::steady_clock::now();
   for (int i = 0; i < 10000 && sweep_graveyard(h, true) != 0; ++i)
     std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  debug_slow("free the replaced tables", ms_since(ts));
   std::lock_guard<std::mutex> g(h->emu);  // (a pass held on for 10 s: writers free them later)
   for (auto& e : h->graveyard) e->heavy = false;
 }
@@ -3124,6 +3146,11 @@ int emqxgm_commit(emqxgm_t* h, uint64_t* epoch) {
 // subscribe wait for its full build.  When this delta does not fit, everything pending takes the
 // usual path (commit_locked).
 static int commit_mine(emqxgm* h, std::unique_lock<std::mutex>& lk, size_t c0) {
+  const auto t0 = std::chrono::steady_clock::now();
+  struct Slow {
+    std::chrono::steady_clock::time_point t0;
+    ~Slow() { debug_slow("synchronous commit", ms_since(t0)); }
+  } slow{t0};
   if (c0 == 0) return commit_locked(h, &lk, false);
   std::vector<uint32_t> rest(h->changed.begin(), h->changed.begin() + c0);
   h->changed.erase(h->changed.begin(), h->changed.begin() + c0);
@@ -3144,11 +3171,15 @@ int emqxgm_route_set_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* of
   for (uint64_t i = 0; i < n; ++i)
     if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > 65535) return -EINVAL;
   const bool sync = (flags & EMQXGM_SET_COMMIT) != 0;
+  const auto tl = std::chrono::steady_clock::now();
   std::unique_lock<std::mutex> lk = set_lock(h, sync);
+  if (sync) debug_slow("synchronous set: waited for the writer lock", ms_since(tl));
   const size_t c0 = h->changed.size();  // changes pending from other callers
   for (uint64_t i0 = 0; i0 < n; i0 += sync ? n : SET_SLICE) {
     if (i0) let_prio_in(h, lk);
+    const auto tp = std::chrono::steady_clock::now();
     std::unique_lock<std::shared_mutex> g(h->pmu);
+    if (sync) debug_slow("synchronous set: waited for the registry lock", ms_since(tp));
     for (uint64_t i = i0; i < (sync ? n : std::min(n, i0 + SET_SLICE)); ++i) {
       const bool pr = !present || present[i];
       const uint8_t* p = bytes + offsets[i];
