@@ -975,17 +975,48 @@ void commit_stats(emqxgm* h, double ms, bool delta) {
 // waiting for either gets in first -- a subscribe waits for at most one slice, never for the
 // build.  (A filter's bytes, offset and length never change once registered; its membership
 // flags only change under the registry lock held exclusively.)
+//
+// The slice is copied out under the locks -- its records and their bytes, offsets rebased -- and
+// f works on the copy after they are released: f's own work (tokenising, growing the model's
+// node arrays and hash map: a reallocation of a 10M-entry array takes ~100 ms) never holds a
+// writer (r05: synchronous sets waited up to 91 ms for the registry lock).  f(i0, i1, F, pool):
+// filter id is F[id - i0], its bytes pool + F[id - i0].off.
 constexpr uint64_t REG_SLICE = 1024;
 template <class F>
 void for_slices(emqxgm* h, bool bg, uint64_t n, F f) {
+  std::vector<Filter> lf;
+  std::vector<uint8_t> lp;
   for (uint64_t i0 = 0; i0 < n; i0 += REG_SLICE) {
-    std::shared_lock<std::shared_mutex> g(h->pmu, std::defer_lock);
-    if (bg) {
-      { std::lock_guard<std::mutex> w(h->wmu); }
-      g.lock();
+    const uint64_t i1 = std::min<uint64_t>(n, i0 + REG_SLICE);
+    if (!bg) {
+      f(i0, i1, h->filters.data() + i0, h->pool.data());
+      continue;
     }
-    f(i0, std::min<uint64_t>(n, i0 + REG_SLICE), h->filters.data(), h->pool.data());
+    {
+      { std::lock_guard<std::mutex> w(h->wmu); }
+      std::shared_lock<std::shared_mutex> g(h->pmu);
+      lf.assign(h->filters.begin() + i0, h->filters.begin() + i1);
+      lp.clear();
+      for (Filter& x : lf) {
+        const uint64_t o = lp.size();
+        lp.insert(lp.end(), h->pool.data() + x.off, h->pool.data() + x.off + x.len);
+        x.off = o;
+      }
+    }
+    f(i0, i1, lf.data(), lp.data());
   }
+}
+
+// f(F, pool) with the registry readable (a background build takes and drops the writer lock
+// first, then holds the registry lock shared): for short reads of arbitrary ids.
+template <class F>
+void with_registry(emqxgm* h, bool bg, F f) {
+  std::shared_lock<std::shared_mutex> g(h->pmu, std::defer_lock);
+  if (bg) {
+    { std::lock_guard<std::mutex> w(h->wmu); }
+    g.lock();
+  }
+  f(h->filters.data(), h->pool.data());
 }
 
 // The device tables of a host model (its node slots, side array, verify bits, exact entries,
@@ -1008,9 +1039,9 @@ int upload_tables(emqxgm* h, const BuildIn& in, TrieModel& m, DevIndex& nx, Owne
   for_slices(h, in.bg, m.xpos.size(), [&](uint64_t i0, uint64_t i1, const Filter* F, const uint8_t* pool) {
     for (uint64_t id = i0; id < i1; ++id) {
       if (m.xpos[id] == NONE) continue;
-      const uint8_t* p = pool + F[id].off;
-      xent(key_hash(p, F[id].len, fmask), (uint32_t)id, p, F[id].len,
-           &xslots[XENT_U4 * (uint64_t)m.xpos[id]]);
+      const Filter& f = F[id - i0];
+      const uint8_t* p = pool + f.off;
+      xent(key_hash(p, f.len, fmask), (uint32_t)id, p, f.len, &xslots[XENT_U4 * (uint64_t)m.xpos[id]]);
     }
   });
   std::vector<DevBuf> nbufs;
@@ -1155,7 +1186,7 @@ int build_model(emqxgm* h, const BuildIn& in, TrieModel& m) {
   for_slices(h, in.bg, nf, [&](uint64_t i0, uint64_t i1, const Filter* F, const uint8_t* pool) {
     for (uint64_t i = i0; i < i1 && !rc; ++i) {
       const uint32_t id = (uint32_t)i;
-      const Filter& f = F[id];
+      const Filter& f = F[i - i0];
       if (in.seen) (*in.seen)[id] = f.in_trie ? 1 : 0;
       if (!f.in_trie) continue;
       ++m.n_trie;
@@ -1308,10 +1339,10 @@ int build_model(emqxgm* h, const BuildIn& in, TrieModel& m) {
                                // registry may change between two reads)
   for_slices(h, in.bg, nf, [&](uint64_t i0, uint64_t i1, const Filter* F, const uint8_t*) {
     for (uint64_t id = i0; id < i1; ++id) {
-      if (!F[id].route_refs) continue;
+      if (!F[id - i0].route_refs) continue;
       if (in.seen) (*in.seen)[id] |= 2;
       rids.push_back((uint32_t)id);
-      m.nroute(F[id].wild) += 1;
+      m.nroute(F[id - i0].wild) += 1;
     }
   });
   m.n_route = m.n_route_p + m.n_route_w;
@@ -1325,7 +1356,7 @@ int build_model(emqxgm* h, const BuildIn& in, TrieModel& m) {
   for (uint64_t k0 = 0; k0 < rids.size(); k0 += REG_SLICE) {
     const uint64_t k1 = std::min<uint64_t>(rids.size(), k0 + REG_SLICE);
     // (bytes of registered filters never change: only the storage may move, under the lock)
-    for_slices(h, in.bg, 1, [&](uint64_t, uint64_t, const Filter* F, const uint8_t* pool) {
+    with_registry(h, in.bg, [&](const Filter* F, const uint8_t* pool) {
       for (uint64_t k = k0; k < k1; ++k) {
         const uint32_t id = rids[k];
         const Filter& f = F[id];
