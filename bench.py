@@ -22,6 +22,12 @@ against the measured random-gather ceiling, with SURVEY 8d algorithmic bytes and
 bytes beside it as fractions of the 8 TB/s HBM peak (DESIGN.md "Roofline").
 ``cpu_baseline`` is the C++ restatement of the reference's emqx_trie match (oracle/ref_trie.cpp)
 timed on this host's cores on a bounded sample of the same topics (rank 0, N=1 only).
+``subscribe`` (N=1): the writing node's subscribe path -- emqxgm_route_set_batch with
+EMQXGM_SET_COMMIT, then a one-topic match that must see it -- idle and during a background
+rebuild of the whole index (p50 / p99 / max).  ``nif_concurrent`` (N=1): the concurrent publish
+entry under T publisher threads; points ``..._R<ns>_D<k>`` model the NIF's per-call report as
+<ns> of work, reported by k threads.  N>1: ``config.filter_sharded`` holds the filter-sharded
+layout's step, or the error / timeout its watchdog recorded.
 """
 from __future__ import annotations
 
