@@ -602,6 +602,7 @@ hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, con
   a.ctl = sc.ctl;
   a.test_mask = ix.test_mask;
   a.wild_empty = ix.wild_empty;
+  a.nt_rec = n >= TOK_NT_MIN;
   const dim3 grid(grid_for(n, 8192));
   const ExactArgs X = exact_args(ix, sc.xseq);
   if (a.cp_bytes) {
