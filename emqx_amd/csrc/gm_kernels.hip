@@ -27,20 +27,24 @@ static_assert(FB_SMALL_PAIRS == SCAN_TILE, "k_fb_small scans one tile");
 static_assert(SCATTER_SCAN_MAX == SCAN_TILE, "k_scatter<true> scans one tile");
 constexpr uint32_t TILE_BYTES = 16384;  // tokenizer LDS tile (256 topics)
 constexpr uint32_t TILE_CHUNKS = TILE_BYTES / 16 + 2;
-// The route-key probe over a table beyond the TLB's reach: random lines over a 2-3 GiB table
-// come at ~52 G/s, over 4 GiB at 23 G/s and 8 GiB at 17 G/s (profiles/r02/gather_tlb.txt;
-// contiguous or 1-GiB-granule allocations change nothing, profiles/r02/gather_alloc.txt).  Two
-// ways to give the lines in flight a few ranges' translations were measured on cfg4 (100M keys,
-// 8.6 GB, 1M names) and are slower than one pass over the whole table (0.103 ms):
-//   * passes over 2-GiB bucket ranges (k_xhash + one k_exact_range per range, gm_tok.inc):
-//     0.015 + 5 x 0.031 ms -- each pass re-reads every name's hash and runs its names' chain
-//     of dependent loads (offsets, bytes, bucket) at a quarter of the lanes' occupancy;
-//   * names binned by range and probed in that order: 0.170 ms (random per-name gathers).
-// The ranged passes stay as an option (emqxgm_tune("exact_range_kb"), tested) and are never
-// chosen by default (XRANGE_MIN_TABLE).
+// The route-key probe over a table beyond the TLB's reach: random lines over an 8 GiB table come
+// at a third of the 2 GiB rate (profiles/r02/gather_tlb.txt), and at the 2 GiB rate again when
+// each workgroup draws from one range of at most ~2 GiB (profiles/r05/gather_part.txt).  Three
+// ways to give cfg4's probe (100M keys, 8.6 GB, 1M names) that shape were measured, and all are
+// slower than one plain pass (k_exact: 0.088 ms at r05):
+//   * one pass per 2-GiB range (r02): 0.015 + 5 x 0.031 ms (each pass re-read every name and
+//     probed at a fifth of the lanes);
+//   * names binned by range, then probed in that order (r02): 0.170 ms (random per-name gathers);
+//   * one partitioned launch (r05, k_exact_part): k_xhash + k_exact_part 0.110 ms.  Each wave
+//     queues its range's names and probes them.  The added round trips per name (its hash,
+//     then its bytes, then the bucket) cost more than the faster bucket lines save
+//     (profiles/r05/ab_xpart/).
+// k_exact_part stays as an option (emqxgm_tune("exact_range_kb"), tested); the default never
+// chooses it (XRANGE_MIN_TABLE).
 constexpr uint64_t XRANGE_MIN_TABLE = ~0ull;
 constexpr uint32_t XRANGE_MIN_NAMES = 65536;
 constexpr uint64_t XRANGE_DEFAULT = 2ull << 30;
+constexpr uint32_t XPART_BLOCKS = 2048;  // k_exact_part workgroups (8 per CU)
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
@@ -633,11 +637,12 @@ hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, c
   const ExactArgs X = exact_args(ix, sc.xseq);
   hipLaunchKernelGGL(k_xhash, dim3(grid_for(n, 1u << 20)), dim3(WG), 0, s, bytes, off, n,
                      sc.exact_id, X, ix.wild_empty, sc.xh);
-  for (uint64_t lo = 0; lo < buckets; lo += rb) {
-    const uint64_t hi = std::min<uint64_t>(buckets, lo + rb);
-    hipLaunchKernelGGL(k_exact_range, dim3(grid_for(n, 1u << 20)), dim3(WG), 0, s, bytes, off, n,
-                       sc.exact_id, X, (const uint2*)sc.xh, (uint32_t)lo, (uint32_t)hi, sc.ctl);
-  }
+  // R equal ranges of at most rb buckets; G name slices per range
+  const uint64_t R = (buckets + std::max<uint64_t>(rb, buckets >> 16) - 1) / std::max<uint64_t>(rb, buckets >> 16);
+  const uint64_t rbe = (buckets + R - 1) / R;
+  const uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>(XPART_BLOCKS / R, (n + 511) / 512));
+  hipLaunchKernelGGL(k_exact_part, dim3((uint32_t)(R * G)), dim3(WG), 0, s, bytes, off, n,
+                     sc.exact_id, X, (const uint2*)sc.xh, (uint32_t)R, (uint32_t)rbe, sc.ctl);
   return hipGetLastError();
 }
 

@@ -260,8 +260,9 @@ def test_route_key_regions(emqx, kinds, full_bits, range_kb):
     publish name only probes the region of its own kind.  Only-wildcard keys (the IoT-tree
     case: no probe for plain names at all), only-plain keys, both; 2-bit key hashes force every
     key of a region onto one probe chain; a 40 kB wildcard name takes the global-memory path.
-    range_kb=1: the probe runs in passes over 16-bucket ranges (k_xhash + k_exact_range, the
-    path of tables beyond 3 GiB), chains running across range ends and the region boundary."""
+    range_kb=1: the probe is partitioned over 16-bucket ranges (k_xhash + k_exact_part, the
+    option for tables beyond the TLB's reach), chains running across range ends and the region
+    boundary."""
     rng = random.Random(17)
     wild = [f"s/{i}/+/#".encode() for i in range(300)] + [b"+", b"#", b"a/+/b", b"+/+"]
     plain = [f"s/{i}/x/y".encode() for i in range(300)] + [b"", b"a", b"a//b", b"$SYS/x"]
@@ -535,7 +536,7 @@ def test_cfg4_exact_heavy_10m(emqx):
     eng, ref = _load_both(emqx, w)
     res = _assert_engine_equals_ref(eng, ref, None, w.tbytes, w.toff)
     assert (res.exact_id != emqx.NONE).mean() > 0.85
-    # the same batch probed in passes over 64-MiB bucket ranges (the > 3 GiB table path)
+    # the same batch probed partitioned over 64-MiB bucket ranges (k_exact_part, the option)
     eng.tune("exact_range_kb", 64 << 10)
     res2 = eng.match_packed(w.tbytes, w.toff)
     assert np.array_equal(res2.exact_id, res.exact_id)

@@ -1,7 +1,8 @@
 // gather_bench.hip -- what random small-line gathers cost on this MI355X (calibration for the
 // k_walk roofline).  Every lane issues `depth` independent random loads per round of `width`
 // bytes (16/32/64) from a table of `table_mb` MiB, for `rounds` dependent rounds (the next
-// address depends on the loaded data, like a trie walk).  Prints lines/s and GB/s.
+// address depends on the loaded data, like a trie walk).  Prints lines/s and GB/s.  With `part`
+// each workgroup draws from one range of the table (r05: profiles/r05/gather_part.txt).
 // Build: hipcc --offload-arch=gfx950 -O3 tools/gather_bench.hip -o tools/gather_bench
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -18,8 +19,14 @@ __device__ __forceinline__ uint64_t mix(uint64_t k) {
 
 template <int W>  // W = 16-B loads per access
 __global__ __launch_bounds__(256) void k_gather(const uint4* __restrict__ tab, uint64_t nslots,
-                                                int rounds, int depth, uint64_t* out) {
+                                                int rounds, int depth, uint64_t* out, int part) {
   const uint64_t gid = blockIdx.x * 256ull + threadIdx.x;
+  // part > 0: block b draws from range b % part of the table (blocks are dealt to the 8 XCDs
+  // round-robin, so part = 8 gives each XCD one eighth); part < 0: range b * |part| / grid (each
+  // range spread over every XCD)
+  const uint64_t np = part ? (uint64_t)(part > 0 ? part : -part) : 1ull;
+  const uint64_t rs = nslots / np;
+  const uint64_t base = rs * (part > 0 ? blockIdx.x % np : part < 0 ? (uint64_t)blockIdx.x * np / gridDim.x : 0ull);
   uint64_t st[4];
   for (int d = 0; d < 4; ++d) st[d] = mix(gid * 4 + d + 1);
   uint32_t acc = 0;
@@ -28,7 +35,7 @@ __global__ __launch_bounds__(256) void k_gather(const uint4* __restrict__ tab, u
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       if (d < depth) {
-        const uint64_t s = st[d] % nslots;
+        const uint64_t s = base + st[d] % rs;
 #pragma unroll
         for (int w = 0; w < W; ++w) v[d][w] = tab[s * W + w];
       }
@@ -50,7 +57,7 @@ __global__ __launch_bounds__(256) void k_gather(const uint4* __restrict__ tab, u
 int main(int argc, char** argv) {
   // usage: gather_bench [table_MiB=2048] [wg_per_cu=8] [width_16B_units=0 (all)] [depth=0 (all)]
   //                     [alloc=0: hipMalloc, 1: hipExtMallocWithFlags(hipDeviceMallocContiguous),
-  //                      2: hipMemCreate/hipMemMap at 1 GiB granularity]
+  //                      2: hipMemCreate/hipMemMap at 1 GiB granularity] [part=0, see k_gather]
   const uint64_t mb = argc > 1 ? atoll(argv[1]) : 2048;
   const int wgpc = argc > 2 ? atoi(argv[2]) : 8;
   const int only_w = argc > 3 ? atoi(argv[3]) : 0;
@@ -61,6 +68,7 @@ int main(int argc, char** argv) {
   uint4* tab;
   uint64_t* out;
   const int alloc = argc > 5 ? atoi(argv[5]) : 0;
+  const int part = argc > 6 ? atoi(argv[6]) : 0;  // see k_gather
   if (alloc == 1) {
     CHK(hipExtMallocWithFlags((void**)&tab, bytes, hipDeviceMallocContiguous));
   } else if (alloc == 2) {
@@ -95,7 +103,7 @@ int main(int argc, char** argv) {
   CHK(hipEventCreate(&b));
   const int blocks = p.multiProcessorCount * wgpc;
   const int rounds = 64;
-  printf("table %llu MiB, %d CUs x %d WG, %d rounds, alloc %d\n", (unsigned long long)mb, p.multiProcessorCount, wgpc, rounds, alloc);
+  printf("table %llu MiB, %d CUs x %d WG, %d rounds, alloc %d, part %d\n", (unsigned long long)mb, p.multiProcessorCount, wgpc, rounds, alloc, part);
   for (int W : {1, 2, 4}) {
     if (only_w && W != only_w) continue;
     for (int depth : {1, 2, 4}) {
@@ -103,9 +111,9 @@ int main(int argc, char** argv) {
       const uint64_t nslots = bytes / (16ull * W);
       for (int rep = 0; rep < 2; ++rep) {
         CHK(hipEventRecord(a));
-        if (W == 1) hipLaunchKernelGGL(k_gather<1>, dim3(blocks), dim3(256), 0, 0, tab, nslots, rounds, depth, out);
-        if (W == 2) hipLaunchKernelGGL(k_gather<2>, dim3(blocks), dim3(256), 0, 0, tab, nslots, rounds, depth, out);
-        if (W == 4) hipLaunchKernelGGL(k_gather<4>, dim3(blocks), dim3(256), 0, 0, tab, nslots, rounds, depth, out);
+        if (W == 1) hipLaunchKernelGGL(k_gather<1>, dim3(blocks), dim3(256), 0, 0, tab, nslots, rounds, depth, out, part);
+        if (W == 2) hipLaunchKernelGGL(k_gather<2>, dim3(blocks), dim3(256), 0, 0, tab, nslots, rounds, depth, out, part);
+        if (W == 4) hipLaunchKernelGGL(k_gather<4>, dim3(blocks), dim3(256), 0, 0, tab, nslots, rounds, depth, out, part);
         CHK(hipEventRecord(b));
         CHK(hipEventSynchronize(b));
         float ms;
