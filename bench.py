@@ -909,6 +909,10 @@ def _roofline(nt, nbytes, census, pmc, tok_ms, exact_ms, walk_ms, pipe_ms, exact
                                # ceilings, over the kernel's time
                                "frac_mixed_ceiling": round(model / sec, 4),
                                "source": p.get("source")}
+        if p.get("stalls"):
+            # the memory-subsystem stall counters of the committed HEAD profile (tools/
+            # pmc_stalls.py): which unit bounds the kernel ("What bounds the walk")
+            out["stall_counters"] = {k: v for k, v in p["stalls"].items() if k != "raw"}
         if p.get("duration_us") is not None:
             # the PMC run's kernel average over the default (pipelined) command: walks beside the
             # other pass's kernels at three workgroups per CU, not the one-pass time used above

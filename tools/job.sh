@@ -108,6 +108,22 @@ step_sq() {
   python3 $R/tools/pmc_summary.py $O/sq_cfg$c > $O/sq_cfg${c}_summary.txt 2>&1
 }
 
+step_stall() {
+  # memory-subsystem stall counters of one kernel: issue/wait split (SQ),
+  # address/data path busy and stalls (TA, TD), L1 pending and translation stalls (TCP)
+  local c=${1%%:*} k=k_walk i=0 grp
+  [ "$1" != "$c" ] && k=${1#*:}
+  for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE" \
+             "SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE" \
+             "TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCP_TA_ADDR_STALL_CYCLES_sum TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_STALL_INFLIGHT_MAX_sum GRBM_GUI_ACTIVE"; do
+    i=$((i+1))
+    timeout -s KILL 400 rocprofv3 --pmc $grp --kernel-include-regex "$k" -d $O/stall_cfg$c/p$i -o run \
+      --output-format csv -- python3 $R/bench.py --cfg $c $PROF --steps 3 --warmup 1 \
+      > $O/stall_cfg${c}_p$i.log 2>&1 || return 1
+  done
+  python3 $R/tools/pmc_summary.py $O/stall_cfg$c > $O/stall_cfg${c}_summary.txt 2>&1
+}
+
 step_ab() {
   local specs=${1%%/*} variants=${1#*/} V spec
   cp $R/emqx_amd/libemqx_gpumatch.so $R/ablib/lib_base.so || return 1
