@@ -154,6 +154,28 @@ struct emqxgm_async {
   std::vector<std::vector<uint64_t>> rf_off;
   bool publish_mode() const { return (cfg.flags & EMQXGM_ASYNC_PUBLISH) != 0; }
   uint64_t st_windows = 0, st_cancelled = 0, st_errors = 0, st_delivered = 0;
+  // health (cfg.fail_threshold > 0): consecutive failures -- pending calls cancelled by callers
+  // that timed out, windows that failed -- until every handle is marked stale
+  std::atomic<uint32_t> fails{0};
+  std::atomic<uint64_t> st_timeouts{0}, st_failed{0}, st_stale{0};
+
+  bool all_stale() const {
+    for (emqxgm_t* h : hs)
+      if (!gm_stale(h)) return false;
+    return true;
+  }
+  // a pending call cancelled: with health counting on, its caller timed out
+  void timed_out() {
+    if (!cfg.fail_threshold) return;
+    st_timeouts.fetch_add(1, std::memory_order_relaxed);
+    note_failure(-ETIMEDOUT);
+  }
+  void note_failure(int err) {
+    if (!cfg.fail_threshold) return;
+    if (fails.fetch_add(1) + 1 < cfg.fail_threshold) return;
+    fails.store(0);
+    for (emqxgm_t* h : hs) (void)emqxgm_mark_stale(h, err);
+  }
 
   // ---- delivery: cfg.deliver_threads > 1 splits a large window's reports over a pool (the
   // caller's per-call work -- the NIF builds each call's terms and enif_sends them -- would
@@ -404,14 +426,19 @@ struct emqxgm_async {
       bool progressed = false;
       while (!ready.empty()) {
         const uint32_t H = (uint32_t)hs.size();
-        uint32_t k = H;
+        // a handle with a pipe free, one whose index is not stale first (a stale one refuses the
+        // window: its calls are reported -ESTALE and answered by their callers)
+        uint32_t k = H, ks = H;
         for (uint32_t j = 0; j < H; ++j) {
           const uint32_t c = (rr + j) % H;
-          if (outstanding[c] < EMQXGM_HOST_PIPES) {
+          if (outstanding[c] >= EMQXGM_HOST_PIPES) continue;
+          if (!gm_stale(hs[c])) {
             k = c;
             break;
           }
+          if (ks == H) ks = c;
         }
+        if (k == H) k = ks;
         if (k == H) break;  // every pipe busy: a completer's release wakes us
         const int si = ready.front();
         Slot& s = *slots[si];
@@ -512,6 +539,12 @@ struct emqxgm_async {
         rc = emqxgm_match_batch_wait_filters(hs[k], s.ticket, &bo, &foff, &fb);
       }
       const uint64_t done = mono_ns();
+      if (rc == 0) {
+        fails.store(0, std::memory_order_relaxed);
+      } else if (rc != -ESTALE) {
+        st_failed.fetch_add(1, std::memory_order_relaxed);
+        note_failure(rc);
+      }
       g.lock();
       inflight[k].pop_front();
       s.state = DELIVERING;  // a cancel() of one of its calls waits for the release below
@@ -659,6 +692,10 @@ int emqxgm_async_match(emqxgm_async_t* a, const uint8_t* topic, uint32_t len, ui
                        uint64_t owner) {
   if (!a || (!topic && len) || tag == EMQXGM_TAG_CANCELLED) return -EINVAL;
   if (len > a->cfg.window_bytes) return -E2BIG;
+  if (a->all_stale()) {  // no index may answer: the caller's own path (include: "Health")
+    a->st_stale.fetch_add(1, std::memory_order_relaxed);
+    return -ESTALE;
+  }
   if (a->cfg.max_levels) {
     // emqx_topic:levels/1 = words: separators + 1 (the zone's max_topic_levels, checked here so
     // a caller does not tokenise on the host first)
@@ -738,8 +775,11 @@ int emqxgm_async_cancel(emqxgm_async_t* a, uint64_t tag, uint64_t owner) {
       if (c->tag[j] == tag && c->owner[j] == owner) {
         c->tag[j] = EMQXGM_TAG_CANCELLED;  // still matched, never reported
         c->unlock();
-        std::lock_guard<std::mutex> g(a->mu);
-        a->st_cancelled += 1;
+        {
+          std::lock_guard<std::mutex> g(a->mu);
+          a->st_cancelled += 1;
+        }
+        a->timed_out();
         return 1;
       }
     c->unlock();
@@ -766,6 +806,8 @@ int emqxgm_async_cancel(emqxgm_async_t* a, uint64_t tag, uint64_t owner) {
       }
       s.tag[j].store(EMQXGM_TAG_CANCELLED, std::memory_order_relaxed);  // matched, never reported
       a->st_cancelled += 1;
+      g.unlock();
+      a->timed_out();
       return 1;
     }
   }
@@ -801,6 +843,17 @@ int emqxgm_async_stats(emqxgm_async_t* a, uint64_t out[8]) {
   for (auto v : a->outstanding) q += v;
   out[7] = q;
   return 0;
+}
+
+int emqxgm_async_health(emqxgm_async_t* a, uint64_t out[4]) {
+  if (!a || !out) return -EINVAL;
+  uint64_t n = 0;
+  for (emqxgm_t* h : a->hs) n += gm_stale(h) ? 1 : 0;
+  out[0] = n;
+  out[1] = a->st_timeouts.load();
+  out[2] = a->st_failed.load();
+  out[3] = a->st_stale.load();
+  return (int)n;
 }
 
 }  // extern "C"

@@ -598,6 +598,26 @@ struct emqxgm {
   // synchronous sets (EMQXGM_SET_COMMIT) waiting for the writer lock: a bulk set lets them in
   // between two of its slices (sync_lock / let_prio_in)
   std::atomic<uint32_t> prio_waiting{0};  // tune "bg_delay_ms": a build holds its install back (tests)
+
+  // ---- health (r06, SURVEY 5 "Failure detection"; hmu): a failed commit, a set that failed
+  // half-way, or the host's report of a timeout marks the index STALE -- it may lack a change the
+  // caller's tables already hold -- and every match entry refuses with -ESTALE (the caller takes
+  // the reference's path) until a repair: a successful emqxgm_commit (after a full resync begun
+  // after the last mark, when a mark asked for one) and a probe of the device's streams ----
+  std::mutex hmu;
+  std::atomic<uint32_t> stale{0};  // EMQXGM_STALE_* bits
+  uint64_t stale_seq = 0;          // marks so far
+  uint64_t resync_from = 0;        // stale_seq at the last emqxgm_route_sync_begin
+  uint64_t resynced = ~0ull;       // stale_seq the last completed resync covers (~0: none)
+  int32_t stale_err = 0;           // the last mark's errno (negative)
+  std::atomic<uint64_t> refused{0};
+  uint64_t repairs = 0;
+  uint32_t probe_ms = 2000;        // the repair's bounded wait on the streams (tune "probe_ms")
+  // fault injection (tune "fail_commits" / "fail_errno" / "hang_ms"): the next n commits fail
+  // before they touch anything; host-pipe waits and publish passes stall this long first
+  std::atomic<int64_t> inject_commits{0};
+  std::atomic<int32_t> inject_errno{EIO};
+  std::atomic<uint32_t> hang_ms{0};
 };
 
 namespace {
@@ -617,6 +637,38 @@ int fail(emqxgm* h, hipError_t e, const char* what) {
     hipError_t _e = (expr);                      \
     if (_e != hipSuccess) return fail(h, _e, #expr); \
   } while (0)
+
+// ---- health (emqxgm::stale) ----
+void mark_stale(emqxgm* h, uint32_t bits, int err) {
+  std::lock_guard<std::mutex> g(h->hmu);
+  h->stale.fetch_or(bits, std::memory_order_seq_cst);
+  h->stale_seq += 1;
+  h->stale_err = err;
+}
+
+// -ESTALE for a match entry while the index is stale (counted), else 0
+int refuse_stale(emqxgm* h) {
+  if (h->stale.load(std::memory_order_acquire) == 0) return 0;
+  h->refused.fetch_add(1, std::memory_order_relaxed);
+  set_err(h, "the device index is stale (a failed commit or a timeout): repair it with a resync "
+             "and emqxgm_commit; callers take the reference path meanwhile");
+  return -ESTALE;
+}
+
+// The injected failure of a commit (tune "fail_commits"), before it touches anything
+int injected(emqxgm* h) {
+  if (h->inject_commits.load(std::memory_order_relaxed) <= 0) return 0;
+  if (h->inject_commits.fetch_sub(1) <= 0) return 0;
+  set_err(h, "injected commit failure (tune fail_commits)");
+  return -h->inject_errno.load(std::memory_order_relaxed);
+}
+
+// tune "hang_ms": a host-pipe wait or a publish pass stalls first (tests: a window that does
+// not complete within the caller's timeout)
+void injected_hang(emqxgm* h) {
+  if (const uint32_t ms = h->hang_ms.load(std::memory_order_relaxed))
+    std::this_thread::sleep_for(std::chrono::milliseconds(ms));
+}
 
 uint64_t str_hash(const uint8_t* p, uint32_t len) {
   uint64_t x = FNV_OFF;
@@ -1912,6 +1964,7 @@ void build_thread(emqxgm* h, BuildJob* J) {
     debug_slow("install: waited for the writer lock", ms_since(tw));
     const auto ti = std::chrono::steady_clock::now();
     h->build_rc = install_build(h, spent);
+    if (h->build_rc) mark_stale(h, EMQXGM_STALE_COMMIT, h->build_rc);  // (no caller may be waiting)
     debug_slow("install", ms_since(ti));
     h->builds_done += 1;
     h->bcv.notify_all();
@@ -3014,6 +3067,8 @@ int emqxgm_route_sync_begin(emqxgm_t* h, uint32_t* gen) {
   h->sync_gen = h->sync_next++;
   if (h->sync_next == 0) h->sync_next = 1;  // 0 means "no resync"
   if (gen) *gen = h->sync_gen;
+  std::lock_guard<std::mutex> hg(h->hmu);
+  h->resync_from = h->stale_seq;  // a repair needs a resync begun after the last mark
   return 0;
 }
 
@@ -3031,6 +3086,8 @@ int emqxgm_route_sync_end(emqxgm_t* h, uint32_t gen, uint64_t* removed) {
   }
   h->sync_gen = 0;
   if (removed) *removed = k;
+  std::lock_guard<std::mutex> hg(h->hmu);
+  h->resynced = h->resync_from;
   return 0;
 }
 
@@ -3163,28 +3220,130 @@ int emqxgm_route_ref_many(emqxgm_t* h, const uint8_t* bytes, const uint64_t* off
   return 0;
 }
 
-int emqxgm_commit(emqxgm_t* h, uint64_t* epoch) {
-  if (!h) return -EINVAL;
-  std::unique_lock<std::mutex> lk(h->wmu);
-  const int rc = commit_locked(h, &lk, true);
-  if (epoch) *epoch = h->epoch;
+}  // extern "C"
+namespace {
+
+// Every stream the passes and the writer use answers within probe_ms (a repair's proof that the
+// device runs again): an event recorded on each, polled.  -ETIMEDOUT: some stream did not.
+int probe_streams(emqxgm* h) {
+  std::vector<hipEvent_t> evs;
+  int rc = 0;
+  auto rec = [&](hipStream_t s) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return (rc = -EIO), false;
+    evs.push_back(e);
+    if (hipEventRecord(e, s) != hipSuccess) return (rc = -EIO), false;
+    return true;
+  };
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
+  if (rec(h->wstream))
+    for (hipStream_t s : h->pipe_streams)
+      if (s && !rec(s)) break;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (size_t i = 0; !rc && i < evs.size();) {
+    const hipError_t q = hipEventQuery(evs[i]);
+    if (q == hipSuccess) {
+      ++i;
+    } else if (q != hipErrorNotReady) {
+      rc = -EIO;
+    } else if (ms_since(t0) > h->probe_ms) {
+      (void)hipGetLastError();
+      rc = -ETIMEDOUT;
+    } else {
+      std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+  }
+  for (hipEvent_t e : evs) (void)hipEventDestroy(e);
+  if (rc) set_err(h, rc == -ETIMEDOUT ? "repair: a device stream did not answer within probe_ms"
+                                      : "repair: the stream probe failed");
   return rc;
 }
 
+// After a successful commit of a stale index (wmu held): clear the mark when no mark came since
+// seq0, a mark that asked for a resync has one that began after it, and the streams answer.
+// 0: healthy again; -ESTALE: still stale (a mark since, or no covering resync); -ETIMEDOUT/-EIO:
+// the probe failed.
+int try_repair(emqxgm* h, uint64_t seq0) {
+  {
+    std::lock_guard<std::mutex> g(h->hmu);
+    if (h->stale_seq != seq0 ||
+        ((h->stale.load() & EMQXGM_STALE_RESYNC) && h->resynced != seq0)) {
+      set_err(h, "still stale: a resync begun after the last mark must complete before the commit");
+      return -ESTALE;
+    }
+  }
+  if (int rc = probe_streams(h)) return rc;
+  std::lock_guard<std::mutex> g(h->hmu);
+  if (h->stale_seq != seq0) return -ESTALE;
+  h->stale.store(0, std::memory_order_seq_cst);
+  h->repairs += 1;
+  return 0;
+}
+
+}  // namespace
+extern "C" {
+
+int emqxgm_commit(emqxgm_t* h, uint64_t* epoch) {
+  if (!h) return -EINVAL;
+  std::unique_lock<std::mutex> lk(h->wmu);
+  uint64_t seq0;
+  {
+    std::lock_guard<std::mutex> g(h->hmu);
+    seq0 = h->stale_seq;
+  }
+  int rc = injected(h);
+  if (rc == 0) rc = commit_locked(h, &lk, true);
+  if (epoch) *epoch = h->epoch;
+  if (rc < 0) {
+    mark_stale(h, EMQXGM_STALE_COMMIT, rc);
+    return rc;
+  }
+  return h->stale.load() ? try_repair(h, seq0) : 0;
+}
+
+int emqxgm_get_health(emqxgm_t* h, emqxgm_health_t* out) {
+  if (!h || !out) return -EINVAL;
+  std::lock_guard<std::mutex> g(h->hmu);
+  out->stale = h->stale.load();
+  out->last_error = h->stale_err;
+  out->marks = h->stale_seq;
+  out->repairs = h->repairs;
+  out->refused = h->refused.load();
+  return (int)out->stale;
+}
+
+int emqxgm_mark_stale(emqxgm_t* h, int err) {
+  if (!h) return -EINVAL;
+  mark_stale(h, EMQXGM_STALE_RESYNC, err > 0 ? -err : err);
+  return 0;
+}
+
 // The commit of a synchronous set (EMQXGM_SET_COMMIT): a delta of this call's own changes (those
-// appended to h->changed since c0); changes other callers left pending stay pending -- they are
-// not this caller's to publish, and a bulk of them (a resync's chunks) must not make a single
-// subscribe wait for its full build.  When this delta does not fit, everything pending takes the
-// usual path (commit_locked).
-static int commit_mine(emqxgm* h, std::unique_lock<std::mutex>& lk, size_t c0) {
+// appended to h->changed since c0, and the filters `mine` -- every filter the call resolved --
+// whose state another caller left pending: a resync chunk that already set the state this call
+// asks for leaves this call nothing to append, and its hook must still see the filter committed
+// when it returns); other callers' pending changes stay pending -- they are not this
+// caller's to publish, and a bulk of them (a resync's chunks) must not make a single subscribe
+// wait for its full build.  When this delta does not fit, everything pending takes the usual
+// path (commit_locked).
+static int commit_mine(emqxgm* h, std::unique_lock<std::mutex>& lk, size_t c0,
+                       std::vector<uint32_t>& mine) {
   const auto t0 = std::chrono::steady_clock::now();
   struct Slow {
     std::chrono::steady_clock::time_point t0;
     ~Slow() { debug_slow("synchronous commit", ms_since(t0)); }
   } slow{t0};
+  if (int rc = injected(h)) return rc;
   if (c0 == 0) return commit_locked(h, &lk, false);
-  std::vector<uint32_t> rest(h->changed.begin(), h->changed.begin() + c0);
-  h->changed.erase(h->changed.begin(), h->changed.begin() + c0);
+  std::sort(mine.begin(), mine.end());
+  std::vector<uint32_t> rest, own;
+  rest.reserve(c0);
+  for (size_t i = 0; i < c0; ++i) {
+    const uint32_t id = h->changed[i];
+    (std::binary_search(mine.begin(), mine.end(), id) ? own : rest).push_back(id);
+  }
+  own.insert(own.end(), h->changed.begin() + c0, h->changed.end());
+  h->changed.swap(own);
   int rc = try_delta(h, std::chrono::steady_clock::now());
   if (rc == 0) {
     h->changed.swap(rest);
@@ -3194,6 +3353,19 @@ static int commit_mine(emqxgm* h, std::unique_lock<std::mutex>& lk, size_t c0) {
   h->changed.insert(h->changed.end(), rest.begin(), rest.end());
   h->dirty = true;
   return rc < 0 ? rc : commit_locked(h, &lk, false);
+}
+
+// A synchronous set's end: its commit, and the health mark when the set or its commit failed (the
+// caller's table holds a change the index may now lack: matches refuse until a repair)
+static int set_done(emqxgm* h, std::unique_lock<std::mutex>& lk, int rc, uint32_t flags, size_t c0,
+                    std::vector<uint32_t>& mine, uint64_t* epoch) {
+  if (rc == -E2BIG) mark_stale(h, EMQXGM_STALE_RESYNC, rc);  // half applied
+  if (rc == 0 && (flags & EMQXGM_SET_COMMIT)) {
+    rc = commit_mine(h, lk, c0, mine);
+    if (rc < 0) mark_stale(h, EMQXGM_STALE_COMMIT, rc);
+  }
+  if (epoch) *epoch = h->epoch;
+  return rc;
 }
 
 int emqxgm_route_set_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets,
@@ -3206,7 +3378,9 @@ int emqxgm_route_set_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* of
   std::unique_lock<std::mutex> lk = set_lock(h, sync);
   if (sync) debug_slow("synchronous set: waited for the writer lock", ms_since(tl));
   const size_t c0 = h->changed.size();  // changes pending from other callers
-  for (uint64_t i0 = 0; i0 < n; i0 += sync ? n : SET_SLICE) {
+  std::vector<uint32_t> mine;
+  int rc = 0;
+  for (uint64_t i0 = 0; i0 < n && !rc; i0 += sync ? n : SET_SLICE) {
     if (i0) let_prio_in(h, lk);
     const auto tp = std::chrono::steady_clock::now();
     std::unique_lock<std::shared_mutex> g(h->pmu);
@@ -3215,15 +3389,17 @@ int emqxgm_route_set_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* of
       const bool pr = !present || present[i];
       const uint8_t* p = bytes + offsets[i];
       const uint32_t len = (uint32_t)(offsets[i + 1] - offsets[i]);
-      if (pr && h->filters.size() >= 0x7FFFFFFFu) return -E2BIG;
+      if (pr && h->filters.size() >= 0x7FFFFFFFu) {
+        rc = -E2BIG;
+        break;
+      }
       const uint32_t id = find_id(h, p, len, pr);
-      if (id != NONE) route_set_locked(h, id, pr);
+      if (id == NONE) continue;
+      route_set_locked(h, id, pr);
+      if (sync) mine.push_back(id);
     }
   }
-  int rc = 0;
-  if (flags & EMQXGM_SET_COMMIT) rc = commit_mine(h, lk, c0);
-  if (epoch) *epoch = h->epoch;
-  return rc;
+  return set_done(h, lk, rc, flags, c0, mine, epoch);
 }
 
 int emqxgm_route_dests_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
@@ -3241,7 +3417,9 @@ int emqxgm_route_dests_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* 
   std::unique_lock<std::mutex> lk = set_lock(h, sync);
   const size_t c0 = h->changed.size();  // changes pending from other callers
   std::vector<std::pair<uint32_t, uint32_t>> ds;
-  for (uint64_t i0 = 0; i0 < n; i0 += sync ? n : SET_SLICE) {
+  std::vector<uint32_t> mine;
+  int rc = 0;
+  for (uint64_t i0 = 0; i0 < n && !rc; i0 += sync ? n : SET_SLICE) {
     if (i0) let_prio_in(h, lk);
     std::unique_lock<std::shared_mutex> g(h->pmu);
     for (uint64_t i = i0; i < (sync ? n : std::min(n, i0 + SET_SLICE)); ++i) {
@@ -3251,7 +3429,10 @@ int emqxgm_route_dests_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* 
       ds.erase(std::unique(ds.begin(), ds.end()), ds.end());
       const uint8_t* p = bytes + offsets[i];
       const uint32_t len = (uint32_t)(offsets[i + 1] - offsets[i]);
-      if (!ds.empty() && h->filters.size() >= 0x7FFFFFFFu) return -E2BIG;
+      if (!ds.empty() && h->filters.size() >= 0x7FFFFFFFu) {
+        rc = -E2BIG;
+        break;
+      }
       const uint32_t id = find_id(h, p, len, !ds.empty());
       if (id == NONE) continue;  // absent and unknown: nothing to remove
       auto it = h->rdest.find(id);
@@ -3267,12 +3448,10 @@ int emqxgm_route_dests_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* 
         h->dirty = true;
       }
       route_set_locked(h, id, !ds.empty());
+      if (sync) mine.push_back(id);
     }
   }
-  int rc = 0;
-  if (flags & EMQXGM_SET_COMMIT) rc = commit_mine(h, lk, c0);
-  if (epoch) *epoch = h->epoch;
-  return rc;
+  return set_done(h, lk, rc, flags, c0, mine, epoch);
 }
 
 int emqxgm_subscribers_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
@@ -3286,8 +3465,9 @@ int emqxgm_subscribers_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* 
   const bool sync = (flags & EMQXGM_SET_COMMIT) != 0;
   std::unique_lock<std::mutex> lk = set_lock(h, sync);
   const size_t c0 = h->changed.size();  // changes pending from other callers
-  std::vector<uint32_t> ss;
-  for (uint64_t i0 = 0; i0 < n; i0 += sync ? n : SET_SLICE) {
+  std::vector<uint32_t> ss, mine;  // (fan-out changes commit whole: nothing of `mine` needed)
+  int rc = 0;
+  for (uint64_t i0 = 0; i0 < n && !rc; i0 += sync ? n : SET_SLICE) {
     if (i0) let_prio_in(h, lk);
     std::unique_lock<std::shared_mutex> g(h->pmu);
     for (uint64_t i = i0; i < (sync ? n : std::min(n, i0 + SET_SLICE)); ++i) {
@@ -3296,7 +3476,10 @@ int emqxgm_subscribers_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* 
       ss.erase(std::unique(ss.begin(), ss.end()), ss.end());
       const uint8_t* p = bytes + offsets[i];
       const uint32_t len = (uint32_t)(offsets[i + 1] - offsets[i]);
-      if (!ss.empty() && h->filters.size() >= 0x7FFFFFFFu) return -E2BIG;
+      if (!ss.empty() && h->filters.size() >= 0x7FFFFFFFu) {
+        rc = -E2BIG;
+        break;
+      }
       const uint32_t id = find_id(h, p, len, !ss.empty());
       if (id == NONE) continue;
       auto it = h->lsubs.find(id);
@@ -3312,10 +3495,7 @@ int emqxgm_subscribers_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* 
       h->dirty = true;
     }
   }
-  int rc = 0;
-  if (flags & EMQXGM_SET_COMMIT) rc = commit_mine(h, lk, c0);
-  if (epoch) *epoch = h->epoch;
-  return rc;
+  return set_done(h, lk, rc, flags, c0, mine, epoch);
 }
 
 // ---- index snapshot (SURVEY 5 "checkpoint / resume"): the committed registry and the host
@@ -3711,6 +3891,7 @@ int emqxgm_filters_copy(emqxgm_t* h, const uint32_t* ids, uint64_t n, uint8_t* b
 int emqxgm_match_device(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_offsets, uint32_t n,
                         uint64_t bytes_len, emqxgm_dev_out* out) {
   if (!h || !out || (!d_offsets && n)) return -EINVAL;
+  if (int rc = refuse_stale(h)) return rc;
   std::lock_guard<std::mutex> g(h->mmu);
   if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
   uint32_t pairs = 0;
@@ -3729,6 +3910,7 @@ int emqxgm_match_device(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_o
 int emqxgm_match_device_submit(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_offsets,
                                uint32_t n, uint64_t bytes_len, uint64_t* ticket) {
   if (!h || !ticket || (!d_offsets && n)) return -EINVAL;
+  if (int rc = refuse_stale(h)) return rc;
   std::lock_guard<std::mutex> g(h->mmu);
   if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
   const uint64_t tk = h->next_ticket;
@@ -3804,6 +3986,7 @@ int batch_submit(emqxgm* h, const uint8_t* bytes, const uint32_t* offsets, uint3
                  uint64_t* ticket, bool want_fb, bool trusted = false) {
   if (!h || !ticket || !offsets || offsets[0] != 0 || (!bytes && offsets[n])) return -EINVAL;
   if (n > h->cfg.batch_max) return -E2BIG;
+  if (int rc = refuse_stale(h)) return rc;
   // a decreasing offset would make k_tok / k_exact read a topic of ~4 G bytes past the batch
   // (the concurrent entry's windows build theirs increasing: no O(n) scan on their path)
   for (uint32_t i = 0; !trusted && i < n; ++i)
@@ -3946,6 +4129,8 @@ int gm_submit_window(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets,
   return batch_submit(h, bytes, offsets, n, ticket, true, true);
 }
 
+int gm_stale(emqxgm_t* h) { return h->stale.load(std::memory_order_acquire) != 0; }
+
 // gm_async.cpp at create: every host pipe's buffers sized for windows of n topics / nb bytes
 // (and the filter block for the default density estimate), so that no window of a running
 // layer reallocates -- a hipFree synchronises the whole device (r04: 8 reallocations in a load
@@ -3985,6 +4170,7 @@ extern "C" {
 // wait of host_pipe_complete is then immediate).  Only the waiter of a ticket changes its pipe's
 // state while it is in flight (a resubmit of the pipe needs the ticket waited: -EBUSY).
 static int host_pipe_prewait(emqxgm* h, uint64_t ticket) {
+  injected_hang(h);
   hipEvent_t ev = nullptr;
   {
     std::lock_guard<std::mutex> g(h->mmu);
@@ -4076,6 +4262,7 @@ int emqxgm_match_batch_wait_filters(emqxgm_t* h, uint64_t ticket, emqxgm_batch_o
 int emqxgm_match_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets, uint32_t n,
                        emqxgm_out* out) {
   if (!h || !out || (!offsets && n)) return -EINVAL;
+  if (int rc = refuse_stale(h)) return rc;
   std::lock_guard<std::mutex> g(h->mmu);
   if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
   PassCtx& c = h->sync;
@@ -4153,6 +4340,8 @@ void emqxgm_host_free(emqxgm_t* h, void* p) {
 int emqxgm_publish_batch(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets, uint32_t n,
                          emqxgm_publish_out* out) {
   if (!h || !out || (!offsets && n)) return -EINVAL;
+  if (int rc = refuse_stale(h)) return rc;
+  injected_hang(h);
   std::lock_guard<std::mutex> g(h->mmu);
   if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
   PassCtx& c = h->sync;
@@ -4495,6 +4684,27 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
   if (strcmp(key, "bg_delay_ms") == 0) {  // tests: a background build holds its install back
     if (value < 0 || value > 600000) return -EINVAL;
     h->bg_delay_ms.store((uint32_t)value);
+    return 0;
+  }
+  if (strcmp(key, "fail_commits") == 0) {  // tests: the next v commits fail (health, r06)
+    if (value < 0 || value > 1000000) return -EINVAL;
+    h->inject_commits.store(value);
+    return 0;
+  }
+  if (strcmp(key, "fail_errno") == 0) {  // the errno an injected failure returns (default EIO)
+    if (value <= 0 || value > 4095) return -EINVAL;
+    h->inject_errno.store((int32_t)value);
+    return 0;
+  }
+  if (strcmp(key, "hang_ms") == 0) {  // tests: host-pipe waits and publish passes stall first
+    if (value < 0 || value > 600000) return -EINVAL;
+    h->hang_ms.store((uint32_t)value);
+    return 0;
+  }
+  if (strcmp(key, "probe_ms") == 0) {  // a repair's bounded wait for the device's streams
+    if (value < 1 || value > 600000) return -EINVAL;
+    std::lock_guard<std::mutex> g(h->wmu);
+    h->probe_ms = (uint32_t)value;
     return 0;
   }
   if (strcmp(key, "rebuild") == 0) {  // 1: a full build in the background now (not waited for)

@@ -12,3 +12,5 @@ int gm_submit_window(emqxgm_t* h, const uint8_t* bytes, const uint32_t* offsets,
                      uint64_t* ticket);
 // every host pipe of h sized for windows of n topics / nb bytes (no reallocation later)
 int gm_reserve_windows(emqxgm_t* h, uint32_t n, uint64_t nb);
+// whether h's index is stale (include/emqx_gpumatch.h "Health"): one atomic load, per call
+int gm_stale(emqxgm_t* h);

@@ -79,7 +79,7 @@ extern "C" {
 #define EMQXGM_DEST_GROUP 0x80000000u /* dest handle bit: a shared-subscription group */
 #define EMQXGM_RULE_EQ 1u    /* rule flag: {eq, Filter} -- the name must equal the filter */
 #define EMQXGM_RULE_WORDS 2u /* rule flag: match/2 on word lists (no '$' clauses) */
-#define EMQXGM_ABI_VERSION 4
+#define EMQXGM_ABI_VERSION 5
 #define EMQXGM_SET_COMMIT 1u /* emqxgm_route_set_batch: visible before the call returns */
 
 typedef struct emqxgm emqxgm_t;
@@ -163,6 +163,31 @@ int emqxgm_trie_insert_many(emqxgm_t* h, const uint8_t* bytes, const uint64_t* o
 int emqxgm_route_ref_many(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets,
                           uint64_t n, uint32_t* ids /* nullable */);
 int emqxgm_commit(emqxgm_t* h, uint64_t* epoch /* nullable */);
+/* Health of the index (r06; SURVEY 5 "Failure detection").  The reference's route writes abort in
+ * the caller when they fail (mria transactions, emqx_router_utils.erl:114-118); here the caller's
+ * tables already hold a change when the device refuses it, so the engine fails CLOSED: a commit
+ * that fails (emqxgm_commit, or the commit of an EMQXGM_SET_COMMIT set), a set that fails half-way
+ * (-E2BIG) and emqxgm_mark_stale (the host saw a timeout or a failed window) mark the index
+ * STALE, and every match entry (emqxgm_match_batch*, _match_device*, emqxgm_publish_batch, the
+ * windows of the concurrent entry) returns -ESTALE until a repair -- the caller answers from its
+ * own tables (the reference path) meanwhile, so no answer ever comes from an index that lacks a
+ * change the caller made.  Repair: a successful emqxgm_commit clears the mark when no mark came
+ * during it, every EMQXGM_STALE_RESYNC mark has a full resync (emqxgm_route_sync_begin .. _end)
+ * begun after it, and an event on each of the engine's streams completes within "probe_ms"
+ * (emqxgm_tune, 2000 default).  emqxgm_commit returns -ESTALE (-ETIMEDOUT: the probe) while the
+ * index stays stale after its commit.  emqxgm_get_health returns the stale bits (0 = healthy). */
+#define EMQXGM_STALE_COMMIT 1u /* a commit failed: the pending registry holds the change */
+#define EMQXGM_STALE_RESYNC 2u /* the registry may lack changes: a full resync must follow */
+typedef struct emqxgm_health_s {
+  uint32_t stale;     /* EMQXGM_STALE_* bits; 0 = healthy */
+  int32_t last_error; /* the last mark's errno (negative) */
+  uint64_t marks;     /* times marked */
+  uint64_t repairs;   /* times a repair cleared the marks */
+  uint64_t refused;   /* match calls refused with -ESTALE */
+} emqxgm_health_t;
+int emqxgm_get_health(emqxgm_t* h, emqxgm_health_t* out);
+/* The host's report (a window that timed out or failed): EMQXGM_STALE_RESYNC with errno err. */
+int emqxgm_mark_stale(emqxgm_t* h, int err);
 /* Index snapshot (the reference rebuilds its ram_copies route tables at start,
  * emqx_router.erl:78-92): _save commits pending changes and writes the committed registry (filter
  * strings, trie / route-key membership, routes, subscribers) and the host model of the device
@@ -472,7 +497,9 @@ int emqxgm_batcher_collect(emqxgm_batcher_t* b, uint64_t window, emqxgm_window_o
  * (from that thread; the windows of different handles concurrently).  The window passed to `cb`
  * is valid during the call only.  Every accepted call is reported exactly once, unless cancelled
  * first.  Errors of emqxgm_async_match: -E2BIG (longer than a window, or more than max_levels
- * levels), -EBUSY (every window full or in flight), -EINVAL: the caller answers those itself.
+ * levels), -EBUSY (every window full or in flight), -ESTALE (every handle's index is stale: see
+ * "Health"), -EINVAL: the caller answers those itself.  Windows go to handles that are not stale;
+ * a window whose handle is (or becomes) stale is reported with status -ESTALE.
  * A layer created with EMQXGM_ASYNC_PUBLISH answers each call with emqx_broker:publish/1's
  * routing instead (emqx_broker.erl:218-300: the aggre/1 entries of match_routes(Topic) and the
  * local dispatches, dispatch/2 :326-355, from the engine's fan-out tables): the completer runs
@@ -495,7 +522,12 @@ typedef struct emqxgm_async_cfg {
                               route_ptr / deliver_ptr offset to the part; pair and entry indices
                               stay absolute).  For a caller whose per-call report is costly (the
                               NIF: terms + enif_send), so one thread does not bound the rate */
-  uint32_t reserved;
+  uint32_t fail_threshold; /* 0: no health counting (the default); k > 0: k consecutive failures
+                              -- calls cancelled while still pending (a caller that timed out) or
+                              windows that failed other than -ESTALE -- mark every handle stale
+                              (emqxgm_mark_stale), so a hung GPU costs the callers in flight one
+                              timeout each and every later call is refused at once (-ESTALE) until
+                              the index is repaired.  A window answered resets the count. */
 } emqxgm_async_cfg;
 #define EMQXGM_ASYNC_PUBLISH 1u
 typedef struct emqxgm_async_window {
@@ -540,6 +572,9 @@ int emqxgm_async_cancel(emqxgm_async_t* a, uint64_t tag, uint64_t owner);
 /* out = {calls accepted, windows submitted, calls reported, -EBUSY refusals, cancelled, -E2BIG
  * refusals (levels), windows failed, windows outstanding} */
 int emqxgm_async_stats(emqxgm_async_t* a, uint64_t out[8]);
+/* out = {handles stale now, timeouts counted (pending calls cancelled), failed windows counted,
+ * calls refused with -ESTALE}.  Returns out[0]. */
+int emqxgm_async_health(emqxgm_async_t* a, uint64_t out[4]);
 
 /* ---- filter-sharded layout over several GPUs (the subscription set partitioned by
  * filter, the topic batch broadcast, the per-GPU match lists gathered to one GPU) ----
@@ -613,7 +648,10 @@ int emqxgm_set_profiling(emqxgm_t* h, int on);
  * default, 0 = every full build blocks the writers, as before r05); "bg_delay_ms": a background
  * build holds its install back this long (tests: a build in flight on demand); "rebuild" (1):
  * start a background full build of the registry now without waiting for it (-EBUSY: one is in
- * flight; it also compacts the tables' deleted slots). */
+ * flight; it also compacts the tables' deleted slots); "probe_ms": a repair's bounded wait for
+ * the engine's streams (2000 default).  Fault injection (tests of "Health"): "fail_commits" (n):
+ * the next n commits fail before they change anything, with errno "fail_errno" (EIO default);
+ * "hang_ms": every host-pipe wait and publish pass stalls this long first (0 default). */
 int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value);
 int emqxgm_get_stats(emqxgm_t* h, emqxgm_stats* st);
 /* Last HIP error string seen by the handle (for diagnostics). */

@@ -73,15 +73,22 @@ struct emqxgm {
   MockPipe p[EMQXGM_HOST_PIPES];
   uint64_t next = 1;
   std::atomic<uint64_t> busy{0};
+  std::atomic<int> stale{0};     // the engine's health mark (emqxgm_mark_stale)
+  std::atomic<int> hang_us{0};   // health mode: waits stall this long (a hung device)
 };
 
 extern "C" {
 
 void* emqxgm_host_alloc(emqxgm_t*, uint64_t bytes) { return malloc(bytes ? bytes : 1); }
+int emqxgm_mark_stale(emqxgm_t* h, int) {
+  h->stale.store(1);
+  return 0;
+}
 void emqxgm_host_free(emqxgm_t*, void* p) { free(p); }
 
 int emqxgm_match_batch_submit_filters(emqxgm_t* h, const uint8_t* bytes, const uint32_t* off,
                                       uint32_t n, uint64_t* ticket) {
+  if (h->stale.load()) return -ESTALE;  // the real engine refuses a stale index's windows
   std::lock_guard<std::mutex> g(h->mu);
   const uint64_t tk = h->next;
   MockPipe& p = h->p[tk % EMQXGM_HOST_PIPES];
@@ -121,6 +128,7 @@ int emqxgm_match_batch_submit_filters(emqxgm_t* h, const uint8_t* bytes, const u
 }
 
 }  // extern "C"
+int gm_stale(emqxgm_t* h) { return h->stale.load(); }
 // the engine's buffers sized for the layer's windows (nothing to size in the mock)
 int gm_reserve_windows(emqxgm_t* h, uint32_t n, uint64_t) { return h && n ? 0 : -EINVAL; }
 // the layer's window submit (gm_engine.cpp skips the offsets check there; the mock checks them)
