@@ -68,7 +68,8 @@ typedef struct {
 
 static ErlNifResourceType *RT, *CALL_RT, *RETAIN_RT;
 static ERL_NIF_TERM A_OK, A_ERROR, A_TRUE, A_FALSE, A_MOD, A_ROUTES, A_NONE, A_NODE, A_GROUP, A_SUB,
-    A_SPIN_US, A_BG_BUILD, A_PUBLISH, A_UNDEFINED, A_REPORT_THREADS, A_EQ, A_WORDS, A_BINARY;
+    A_SPIN_US, A_BG_BUILD, A_PUBLISH, A_UNDEFINED, A_REPORT_THREADS, A_EQ, A_WORDS, A_BINARY,
+    A_FAIL_THRESHOLD;
 
 static int tab_init(term_tab* t, char* name) {
   t->lk = enif_rwlock_create(name);
@@ -122,6 +123,7 @@ static ERL_NIF_TERM errno_atom(ErlNifEnv* env, int rc) {
     case ENOENT: a = "enoent"; break;
     case ESTALE: a = "estale"; break;
     case ESHUTDOWN: a = "eshutdown"; break;
+    case ETIMEDOUT: a = "etimedout"; break;
     default: a = "eio"; break;
   }
   return enif_make_atom(env, a);
@@ -226,17 +228,21 @@ static int opt_uint(ErlNifEnv* env, ERL_NIF_TERM map, ERL_NIF_TERM key, ErlNifSI
  * #{spin_us => N (0: a completer blocks at once instead of polling; the default),
  *   bg_build => N (emqxgm_tune "bg_build"), publish => boolean() (a publish_async layer too),
  *   report_threads => N (emqxgm_async_cfg.deliver_threads, default 8: a window's calls are
- *   answered -- terms built, enif_send -- by up to N threads, not by the completer alone)} */
+ *   answered -- terms built, enif_send -- by up to N threads, not by the completer alone),
+ *   fail_threshold => N (emqxgm_async_cfg.fail_threshold, default 3: that many timed-out calls or
+ *   failed windows in a row mark the engines stale, and every later call is refused with
+ *   {error, estale} -- the caller's reference path -- until the mirror's repair)} */
 static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   unsigned ndev, wt, wb, wus, ml;
   ERL_NIF_TERM list = argv[0], head, pub;
-  ErlNifSInt64 spin, bg, rth;
+  ErlNifSInt64 spin, bg, rth, fth;
   (void)argc;
   if (!enif_get_list_length(env, list, &ndev) || ndev == 0 || ndev > GM_MAX_DEVICES ||
       !enif_get_uint(env, argv[1], &wt) || !enif_get_uint(env, argv[2], &wb) ||
       !enif_get_uint(env, argv[3], &wus) || !enif_get_uint(env, argv[4], &ml) ||
       !opt_uint(env, argv[5], A_SPIN_US, 0, &spin) || !opt_uint(env, argv[5], A_BG_BUILD, 16384, &bg) ||
-      !opt_uint(env, argv[5], A_REPORT_THREADS, 8, &rth) || rth < 0 || rth > 64)
+      !opt_uint(env, argv[5], A_REPORT_THREADS, 8, &rth) || rth < 0 || rth > 64 ||
+      !opt_uint(env, argv[5], A_FAIL_THRESHOLD, 3, &fth) || fth < 0 || fth > 1000000)
     return enif_make_badarg(env);
   const int publish = enif_get_map_value(env, argv[5], A_PUBLISH, &pub) && pub == A_TRUE;
   gm_res* r = enif_alloc_resource(RT, sizeof(gm_res));
@@ -273,6 +279,7 @@ static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
   ac.window_us = wus;
   ac.max_levels = ml;
   ac.deliver_threads = (uint32_t)rth;
+  ac.fail_threshold = (uint32_t)fth;
   if (!rc) rc = emqxgm_async_create(r->h, r->nh, &ac, on_window, r, &r->a);
   if (!rc && publish) {
     ac.flags = EMQXGM_ASYNC_PUBLISH;
@@ -378,10 +385,10 @@ static int on_engines(gm_res* r, size_t n, int (*fn)(void*, emqxgm_t*, uint64_t*
       started[k] = 1;
   }
   /* engine 0 on this (dirty) scheduler thread; the others in theirs, or here when a thread could
-   * not start */
+   * not start.  Every engine runs the call even after one refused it: the refusing engine marked
+   * itself stale (it answers no match until a repair), the others must not miss the change. */
   for (unsigned k = 0; k < r->nh; ++k) {
     if (started[k]) continue;
-    if (!par && rc) break;
     eng_job_run(&job[k]);
     if (!rc) rc = job[k].rc;
   }
@@ -639,11 +646,12 @@ static ERL_NIF_TERM nif_set_local_node(ErlNifEnv* env, int argc, const ERL_NIF_T
   unsigned v;
   (void)argc;
   if (!get_res(env, argv[0], &r) || !enif_get_uint(env, argv[1], &v)) return enif_make_badarg(env);
-  for (unsigned k = 0; k < r->nh; ++k) {
-    const int rc = emqxgm_set_local_node(r->h[k], v);
-    if (rc) return err_term(env, rc);
+  int rc = 0;
+  for (unsigned k = 0; k < r->nh; ++k) { /* every engine, as on_engines */
+    const int e = emqxgm_set_local_node(r->h[k], v);
+    if (!rc) rc = e;
   }
-  return A_OK;
+  return rc ? err_term(env, rc) : A_OK;
 }
 
 /* route_set(Res, Filter, Present) -> ok | {error, Reason}: one filter's membership in every engine
@@ -656,11 +664,12 @@ static ERL_NIF_TERM nif_route_set(ErlNifEnv* env, int argc, const ERL_NIF_TERM a
       (argv[2] != A_TRUE && argv[2] != A_FALSE))
     return enif_make_badarg(env);
   if (bin.size > GM_MAX_TOPIC) return err_term(env, -E2BIG);
-  for (unsigned k = 0; k < r->nh; ++k) {
-    const int rc = emqxgm_route_set(r->h[k], bin.data, (uint32_t)bin.size, argv[2] == A_TRUE);
-    if (rc) return err_term(env, rc);
+  int rc = 0;
+  for (unsigned k = 0; k < r->nh; ++k) { /* every engine, as on_engines */
+    const int e = emqxgm_route_set(r->h[k], bin.data, (uint32_t)bin.size, argv[2] == A_TRUE);
+    if (!rc) rc = e;
   }
-  return A_OK;
+  return rc ? err_term(env, rc) : A_OK;
 }
 
 /* sync_begin(Res) -> {ok, Gen}: a full resync starts (emqxgm_route_sync_begin on every engine;
@@ -697,20 +706,23 @@ static ERL_NIF_TERM nif_sync_end(ErlNifEnv* env, int argc, const ERL_NIF_TERM ar
   return enif_make_tuple2(env, A_OK, enif_make_uint64(env, removed));
 }
 
-/* commit(Res) -> {ok, Epoch}: everything pending visible on every engine (a delta patch, or a full
- * build -- in the background for a large registry, this call waiting for its install; dirty CPU) */
+/* commit(Res) -> {ok, Epoch} | {error, R}: everything pending visible on every engine (a delta
+ * patch, or a full build -- in the background for a large registry, this call waiting for its
+ * install; dirty CPU).  Every engine commits even after one failed; {error, estale}: committed,
+ * but an engine is still stale (no resync since its last failure, include "Health"). */
 static ERL_NIF_TERM nif_commit(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   gm_res* r;
   uint64_t epoch = 0;
+  int rc = 0;
   (void)argc;
   if (!get_res(env, argv[0], &r)) return enif_make_badarg(env);
   for (unsigned k = 0; k < r->nh; ++k) {
     uint64_t e = 0;
-    const int rc = emqxgm_commit(r->h[k], &e);
-    if (rc) return err_term(env, rc);
+    const int c = emqxgm_commit(r->h[k], &e);
+    if (!rc) rc = c;
     if (k == 0) epoch = e;
   }
-  return enif_make_tuple2(env, A_OK, enif_make_uint64(env, epoch));
+  return rc ? err_term(env, rc) : enif_make_tuple2(env, A_OK, enif_make_uint64(env, epoch));
 }
 
 /* snapshot_save(Res, Path :: binary()) -> ok | {error, R}: the committed index of engine 0 (every
@@ -858,7 +870,7 @@ static ERL_NIF_TERM nif_tune(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
 }
 
 /* stats(Res) -> #{calls, windows, reported, busy, cancelled, too_deep, failed, outstanding,
- * bg_builds, bg_waits, last_build_ms} */
+ * bg_builds, bg_waits, last_build_ms, stale_engines, timeouts, refused, marks, repairs} */
 static ERL_NIF_TERM nif_stats(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   static const char* keys[8] = {"calls", "windows", "reported", "busy",
                                 "cancelled", "too_deep", "failed", "outstanding"};
@@ -876,6 +888,24 @@ static ERL_NIF_TERM nif_stats(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
   enif_make_map_put(env, m, enif_make_atom(env, "bg_builds"), enif_make_uint64(env, st.bg_builds), &m);
   enif_make_map_put(env, m, enif_make_atom(env, "bg_waits"), enif_make_uint64(env, st.bg_waits), &m);
   enif_make_map_put(env, m, enif_make_atom(env, "last_build_ms"), enif_make_double(env, st.last_build_ms), &m);
+  /* health (include "Health"): engines stale now, timed-out calls, calls refused; engine marks
+   * and repairs summed */
+  uint64_t hv[4];
+  if (emqxgm_async_health(r->a, hv) >= 0) {
+    enif_make_map_put(env, m, enif_make_atom(env, "stale_engines"), enif_make_uint64(env, hv[0]), &m);
+    enif_make_map_put(env, m, enif_make_atom(env, "timeouts"), enif_make_uint64(env, hv[1]), &m);
+    enif_make_map_put(env, m, enif_make_atom(env, "refused"), enif_make_uint64(env, hv[3]), &m);
+  }
+  uint64_t marks = 0, repairs = 0;
+  for (unsigned k = 0; k < r->nh; ++k) {
+    emqxgm_health_t h;
+    if (emqxgm_get_health(r->h[k], &h) >= 0) {
+      marks += h.marks;
+      repairs += h.repairs;
+    }
+  }
+  enif_make_map_put(env, m, enif_make_atom(env, "marks"), enif_make_uint64(env, marks), &m);
+  enif_make_map_put(env, m, enif_make_atom(env, "repairs"), enif_make_uint64(env, repairs), &m);
   return m;
 }
 
@@ -1102,6 +1132,7 @@ static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   A_SPIN_US = enif_make_atom(env, "spin_us");
   A_BG_BUILD = enif_make_atom(env, "bg_build");
   A_REPORT_THREADS = enif_make_atom(env, "report_threads");
+  A_FAIL_THRESHOLD = enif_make_atom(env, "fail_threshold");
   A_EQ = enif_make_atom(env, "eq");
   A_WORDS = enif_make_atom(env, "words");
   A_BINARY = enif_make_atom(env, "binary");

@@ -26,8 +26,12 @@ report_threads     8                  ``emqxgm_async_cfg.deliver_threads``: a wi
                                       terms and enif_send), not by one completer per GPU
 snapshot_dir       (none)             ``emqxgm_snapshot_save`` at the mirror's shutdown,
                                       ``emqxgm_snapshot_load`` at its next start (no full build)
-timeout_ms         5000               a publisher's wait before it cancels and takes the
+timeout_ms         500                a publisher's wait before it cancels and takes the
                                       reference's match (src/emqx_trie_gpu.erl)
+fail_threshold     3                  ``emqxgm_async_cfg.fail_threshold``: that many timed-out
+                                      calls or failed windows in a row mark the engines stale
+                                      (every later call refused at once until the mirror's
+                                      repair; include/emqx_gpumatch.h "Health")
 resync_interval_ms (role)             period of the mirror's full resync (``emqxgm_route_sync_begin``
                                       / ``_end``): none (0) on a core node, 30000 on a replicant
 ================== ================== ======================================================
@@ -53,7 +57,8 @@ class GpuMatchConfig:
     spin_us: int = 0
     report_threads: int = 8
     snapshot_dir: Optional[str] = None
-    timeout_ms: int = 5000
+    timeout_ms: int = 500
+    fail_threshold: int = 3
     resync_interval_ms: Optional[int] = None  # None: by the node's mria role
 
     @classmethod
@@ -82,6 +87,7 @@ class GpuMatchConfig:
         rng("batch_window_us", self.batch_window_us, 1, 1_000_000)
         rng("max_levels", self.max_levels, 1, 65535)
         rng("timeout_ms", self.timeout_ms, 1, 600_000)
+        rng("fail_threshold", self.fail_threshold, 0, 1_000_000)
         if self.resync_interval_ms is not None:
             rng("resync_interval_ms", self.resync_interval_ms, 0, 86_400_000)
         rng("bg_build", self.bg_build, 0, 1 << 62)
@@ -100,7 +106,7 @@ class GpuMatchConfig:
         """``emqxgm_async_cfg`` fields (emqx_amd.AsyncMatcher keywords)."""
         return {"window_topics": self.batch_max, "window_bytes": 64 * self.batch_max,
                 "window_us": self.batch_window_us, "max_levels": self.max_levels,
-                "deliver_threads": self.report_threads}
+                "deliver_threads": self.report_threads, "fail_threshold": self.fail_threshold}
 
     def batcher_kwargs(self) -> Dict[str, int]:
         """``emqxgm_batcher_cfg`` fields (emqx_amd.Batcher keywords: the single-driver batcher

@@ -17,7 +17,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libemqx_gpumatch.so")
 NONE = 0xFFFFFFFF
-ABI_VERSION = 4  # include/emqx_gpumatch.h EMQXGM_ABI_VERSION
+ABI_VERSION = 5  # include/emqx_gpumatch.h EMQXGM_ABI_VERSION
 SET_COMMIT = 1  # EMQXGM_SET_COMMIT
 TAG_CANCELLED = 0xFFFFFFFFFFFFFFFF  # EMQXGM_TAG_CANCELLED
 
@@ -74,7 +74,16 @@ class _AsyncCfg(C.Structure):
     _fields_ = [("window_topics", C.c_uint32), ("window_bytes", C.c_uint32),
                 ("window_us", C.c_uint32), ("max_levels", C.c_uint32),
                 ("queued_windows", C.c_uint32), ("flags", C.c_uint32),
-                ("deliver_threads", C.c_uint32), ("reserved", C.c_uint32)]
+                ("deliver_threads", C.c_uint32), ("fail_threshold", C.c_uint32)]
+
+
+class _Health(C.Structure):  # emqxgm_health_t
+    _fields_ = [("stale", C.c_uint32), ("last_error", C.c_int32), ("marks", C.c_uint64),
+                ("repairs", C.c_uint64), ("refused", C.c_uint64)]
+
+
+STALE_COMMIT = 1  # EMQXGM_STALE_COMMIT
+STALE_RESYNC = 2  # EMQXGM_STALE_RESYNC
 
 
 ASYNC_PUBLISH = 1  # EMQXGM_ASYNC_PUBLISH
@@ -144,6 +153,8 @@ SYMBOLS = {
     "emqxgm_route_sync_end": (C.c_int, [_P, C.c_uint32, _U64P]),
     "emqxgm_route_member": (C.c_int, [_P, C.c_char_p, C.c_uint32]),
     "emqxgm_commit": (C.c_int, [_P, _U64P]),
+    "emqxgm_get_health": (C.c_int, [_P, C.POINTER(_Health)]),
+    "emqxgm_mark_stale": (C.c_int, [_P, C.c_int]),
     "emqxgm_trie_empty": (C.c_int, [_P]),
     "emqxgm_snapshot_save": (C.c_int, [_P, C.c_char_p]),
     "emqxgm_snapshot_load": (C.c_int, [_P, C.c_char_p]),
@@ -204,6 +215,7 @@ SYMBOLS = {
     "emqxgm_async_match": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.c_uint64, C.c_uint64]),
     "emqxgm_async_cancel": (C.c_int, [_P, C.c_uint64, C.c_uint64]),
     "emqxgm_async_stats": (C.c_int, [_P, _U64P]),
+    "emqxgm_async_health": (C.c_int, [_P, _U64P]),
     "emqxgm_set_profiling": (C.c_int, [_P, C.c_int]),
     "emqxgm_tune": (C.c_int, [_P, C.c_char_p, C.c_int64]),
     "emqxgm_get_stats": (C.c_int, [_P, C.POINTER(_Stats)]),
@@ -710,6 +722,16 @@ class Engine:
                     "match_rules")
         return out
 
+    def health(self) -> dict:
+        """emqxgm_get_health: {stale (EMQXGM_STALE_* bits, 0 = healthy), last_error, marks,
+        repairs, refused} (include/emqx_gpumatch.h "Health")."""
+        h = _Health()
+        self._check(self._lib.emqxgm_get_health(self._h, C.byref(h)), "health")
+        return {k: getattr(h, k) for k, _ in _Health._fields_}
+
+    def mark_stale(self, err: int = errno.ETIMEDOUT) -> None:
+        self._check(self._lib.emqxgm_mark_stale(self._h, -abs(err)), "mark_stale")
+
     def tune(self, key: str, value: int) -> None:
         self._check(self._lib.emqxgm_tune(self._h, key.encode(), int(value)), f"tune({key})")
 
@@ -829,7 +851,8 @@ class AsyncMatcher:
 
     def __init__(self, engines: Sequence[Engine], callback=None, window_topics: int = 0,
                  window_bytes: int = 0, window_us: int = 0, max_levels: int = 0,
-                 queued_windows: int = 0, publish: bool = False, deliver_threads: int = 0):
+                 queued_windows: int = 0, publish: bool = False, deliver_threads: int = 0,
+                 fail_threshold: int = 0):
         import threading
         self._engines = list(engines)  # kept alive: the layer uses their handles
         self._lib = self._engines[0]._lib
@@ -874,7 +897,7 @@ class AsyncMatcher:
                     self._cv.notify_all()
         self._cb = ASYNC_CB(on_window)  # kept alive as long as the layer
         cfg = _AsyncCfg(window_topics, window_bytes, window_us, max_levels, queued_windows,
-                        ASYNC_PUBLISH if publish else 0, deliver_threads)
+                        ASYNC_PUBLISH if publish else 0, deliver_threads, fail_threshold)
         arr = (C.c_void_p * len(self._engines))(*[e._h for e in self._engines])
         a = C.c_void_p()
         self._engines[0]._check(self._lib.emqxgm_async_create(arr, len(self._engines), C.byref(cfg),
@@ -883,7 +906,8 @@ class AsyncMatcher:
         self._a = a
 
     def match(self, topic: bytes, tag: int, owner: int = 0) -> int:
-        """0: accepted (reported later); -E2BIG / -EBUSY / -EINVAL: the caller answers it."""
+        """0: accepted (reported later); -E2BIG / -EBUSY / -ESTALE / -EINVAL: the caller answers
+        it."""
         return self._lib.emqxgm_async_match(self._a, topic, len(topic), tag, owner)
 
     def cancel(self, tag: int, owner: int = 0) -> bool:
@@ -907,6 +931,13 @@ class AsyncMatcher:
         self._engines[0]._check(self._lib.emqxgm_async_stats(self._a, v), "async_stats")
         return dict(zip(("calls", "windows", "reported", "busy", "cancelled", "too_deep",
                          "failed", "outstanding"), list(v)))
+
+    def health(self) -> dict:
+        """emqxgm_async_health: handles stale now, timeouts and failed windows counted, calls
+        refused with -ESTALE."""
+        v = (C.c_uint64 * 4)()
+        self._lib.emqxgm_async_health(self._a, v)
+        return dict(zip(("stale_handles", "timeouts", "failed_windows", "refused"), list(v)))
 
     def close(self):
         if getattr(self, "_a", None):

@@ -17,6 +17,14 @@ number and order -- it reads the table as it is now and sets T's dests on the de
 * ``resync``: ``sync_begin``, every topic of the table in chunks of ``chunk`` distinct topics per
   call, ``sync_end`` (removes every route key the scan did not see), then the subscriber lists.
 
+Failing closed (r06, SURVEY 5 "Failure detection").  A device call the engine refuses never
+crashes the mirror or a hook, and never leaves publishers on an index that lacks a committed
+change: the engine marks itself stale on the failed commit (include/emqx_gpumatch.h "Health") and
+refuses every match until a repair, so publishers take the reference's path meanwhile; the
+hooks return ``ok`` whatever happened; the mirror repairs (a full resync and a commit) with
+backoff until the engine is healthy again; the index is published only after its first
+successful repair.
+
 ``table`` is anything with ``lookup_routes(topic)`` ([(topic, dest)]; a dest is a node name or a
 ``(group, node)`` tuple) and ``topics()`` -- ``oracle.emqx_ref.Router`` in the tests (the route bag
 ``emqx_route``, emqx_router.erl:155-161, 186-188).  ``subscribers``: topic -> local subscriber
@@ -28,7 +36,7 @@ from __future__ import annotations
 from collections import deque
 from typing import Deque, Dict, Hashable, List, Optional, Sequence, Tuple
 
-from .engine import NONE
+from .engine import NONE, EngineError
 
 
 class Handles:
@@ -53,6 +61,8 @@ class Handles:
 
 
 class RouteTableMirror:
+    BACKOFF_MS = (100, 30000)  # the repair's first retry and its cap (emqx_trie_gpu_sync.erl)
+
     def __init__(self, engines: Sequence, table, subscribers: Optional[Dict] = None,
                  local_node: Hashable = "n1", chunk: int = 65536):
         self.engines = list(engines)
@@ -62,6 +72,15 @@ class RouteTableMirror:
         self.chunk = chunk
         self.queue: Deque[Tuple[str, bytes]] = deque()  # the process's mailbox of table events
         self.local = self.handles("node", local_node)  # set on the engines by init()
+        self.published = False      # persistent_term {emqx_trie_gpu, route} set
+        self.repair_pending = False  # a `resync` cast queued (repair/1)
+        self.backoff_ms = 0          # the next retry's delay after a failed repair (0: none due)
+        self.errors = 0              # device calls refused so far
+
+    def _refused(self) -> None:
+        """check/2, sync_result/1: the engine refused (it marked itself stale): a repair."""
+        self.errors += 1
+        self.repair_pending = True
 
     # -- mnesia table events: {write, Route, _} / {delete_object, Route, _} / {delete, {Tab, T}, _}
     def event(self, kind: str, topic: bytes) -> None:
@@ -84,35 +103,109 @@ class RouteTableMirror:
     def items(self, topics) -> list:
         return [(t, [self.handles.dest(d) for _, d in self.table.lookup_routes(t)]) for t in topics]
 
-    def sync(self, topics, commit: bool = True) -> None:
+    def _each(self, f) -> None:
+        """f(engine) on EVERY engine, then the first error raised: an engine that refused is
+        stale, the others must still get the change (the NIF's on_engines)."""
+        err = None
+        for e in self.engines:
+            try:
+                f(e)
+            except EngineError as ex:
+                err = err or ex
+        if err is not None:
+            raise err
+
+    def _dests(self, topics, commit: bool) -> None:
         items = self.items(topics)
-        for e in self.engines:
-            e.route_dests_batch(items, commit=commit)
+        self._each(lambda e: e.route_dests_batch(items, commit=commit))
 
-    # -- the writing node's hooks (src/emqx_trie_gpu.erl route_changed/1, subscribers_changed/1)
-    def route_changed(self, topic: bytes) -> None:
+    def sync(self, topics, commit: bool = True) -> bool:
+        """sync/2 + check/2: the topics' state := the table's now; False: refused (repair due)."""
+        try:
+            self._dests(topics, commit)
+        except EngineError:
+            self._refused()
+            return False
+        return True
+
+    # -- the writing node's hooks (src/emqx_trie_gpu.erl route_changed/1, subscribers_changed/1):
+    # "ok" whatever the device did (a refused change is repaired; the engine refuses matches
+    # until then)
+    def route_changed(self, topic: bytes) -> str:
         self.sync([topic])
+        return "ok"
 
-    def subscribers_changed(self, topic: bytes, commit: bool = True) -> None:
+    def _subs(self, topic: bytes, commit: bool) -> None:
         subs = [self.handles("sub", s) for s in (self.subscribers or {}).get(topic, [])]
-        for e in self.engines:
-            e.subscribers_batch([(topic, subs)], commit=commit)
+        self._each(lambda e: e.subscribers_batch([(topic, subs)], commit=commit))
+
+    def subscribers_changed(self, topic: bytes, commit: bool = True) -> str:
+        try:
+            self._subs(topic, commit)
+        except EngineError:
+            self._refused()
+        return "ok"
 
     def resync(self) -> int:
         """A full resync: every topic of the table in chunks, every other route key removed,
-        every subscriber list set.  Returns how many route keys the sweep removed."""
+        every subscriber list set.  Returns how many route keys the sweep removed; raises
+        EngineError when the engine refuses a step (resync/1 returns {error, _})."""
         gens = [e.sync_begin() for e in self.engines]
         topics = list(self.table.topics())
         for i in range(0, len(topics), self.chunk):
-            self.sync(topics[i:i + self.chunk], commit=False)
+            self._dests(topics[i:i + self.chunk], commit=False)
         removed = [e.sync_end(g) for e, g in zip(self.engines, gens)]
         for t in sorted(self.subscribers or {}):
-            self.subscribers_changed(t, commit=False)
+            self._subs(t, commit=False)
         return removed[0] if removed else 0
 
     def commit(self) -> None:
-        for e in self.engines:
-            e.commit()
+        """Raises EngineError; -ESTALE: committed, but an engine is still stale (no resync since
+        its last mark, or its streams did not answer)."""
+        self._each(lambda e: e.commit())
+
+    def repair(self) -> bool:
+        """handle_cast(resync) / handle_info(repair): a full resync and a commit.  True: every
+        engine healthy (and the index published, if it was not yet); False: the next try is due
+        after ``backoff_ms`` (doubling from BACKOFF_MS[0] up to BACKOFF_MS[1])."""
+        self.repair_pending = False
+        try:
+            self.resync()
+            self.commit()
+        except EngineError:
+            self.errors += 1
+            lo, hi = self.BACKOFF_MS
+            self.backoff_ms = min(hi, max(lo, 2 * self.backoff_ms))
+            return False
+        self.backoff_ms = 0
+        self.published = True
+        return True
+
+    def healthy(self) -> bool:
+        return all(e.health()["stale"] == 0 for e in self.engines)
+
+    def device_offered(self) -> bool:
+        """Whether a publisher's call may be answered by the device: the index is published and
+        some engine is not stale (emqxgm_async_match refuses -ESTALE when none is)."""
+        return self.published and any(e.health()["stale"] == 0 for e in self.engines)
+
+    def match_routes(self, topic: bytes):
+        """emqx_trie_gpu:match_routes/1 with one engine's synchronous match standing in for the
+        NIF's window: [(topic, dest)] in match_routes order (the topic's own rows, then each matched
+        filter's).  The table's own match_routes (the reference's path) answers before the first
+        repair and whenever the device refuses (-ESTALE) or fails (a repair is then due)."""
+        if not self.published:
+            return list(self.table.match_routes(topic))
+        try:
+            r = self.engines[0].match([topic])
+        except EngineError as ex:
+            if "ESTALE" not in str(ex):
+                self._refused()
+            return list(self.table.match_routes(topic))
+        filters = self.engines[0].filters_bytes(r.row(0).tolist())
+        exact = int(r.exact_id[0]) != NONE
+        heads = ([topic] if exact else []) + list(filters)
+        return [rt for f in heads for rt in self.table.lookup_routes(f)]
 
     def init(self, snapshot: Optional[str] = None) -> None:
         """handle_continue(open): fresh engines start from `snapshot` (broker.perf.gpu_match.
@@ -131,8 +224,8 @@ class RouteTableMirror:
         # loads into fresh engines only)
         for e in self.engines:
             e.set_local_node(self.local)
-        self.resync()
-        self.commit()
+        if not self.repair():  # unpublished: publishers take the reference's path until it works
+            self.repair_pending = True
 
     def save(self, snapshot: str) -> None:
         """terminate/2: the committed index to `snapshot` (engine 0: they all hold the same)."""

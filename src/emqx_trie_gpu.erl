@@ -24,10 +24,22 @@
 %% the table and set the device to it.  With enable = false, before the first sync, and whenever the
 %% device cannot answer (a topic deeper than max_levels, every window busy, a device error, a
 %% timeout) the call is the reference's own.
+%%
+%% Failing closed (r06, SURVEY 5 "Failure detection").  The reference's route write fails in its
+%% caller (an aborted mria transaction, emqx_router_utils.erl:114-118); here the table already holds
+%% the change when the device refuses it.  The engine then marks itself stale and refuses every call
+%% ({error, estale}) until the mirror's repair (a full resync and a commit) -- so no publish is ever
+%% answered from an index that lacks a committed change -- and the hooks still return ok.  A
+%% publisher that times out cancels its call; fail_threshold such timeouts (or failed windows) in a
+%% row mark the engines stale too, so a hung GPU costs the calls in flight one timeout_ms each and
+%% every later call is refused at once.  Timeouts and failed windows ask the mirror to repair.  (The
+%% persistent_term handle stays: erasing it would make OTP scan every process's heap; the engine's
+%% refusal is one atomic load.)
 %%--------------------------------------------------------------------
 -module(emqx_trie_gpu).
 
 -include_lib("emqx/include/emqx.hrl").
+-include_lib("emqx/include/logger.hrl").
 
 -export([child_specs/0, enabled/0, handle/1, publish/2]).
 -export([match/1, match_session/1, match_trie/1, match_routes/1, empty/0, empty_session/0]).
@@ -112,10 +124,11 @@ device_match(Index, H, Topic) ->
         {ok, Call} ->
             receive
                 {emqx_trie_gpu, Ref, Filters, Exact} -> {Filters, Exact};
-                {emqx_trie_gpu, Ref, {error, _}} -> {ref_match(Index, Topic), unknown}
-            after ?CONF(timeout_ms, 5000) ->
+                {emqx_trie_gpu, Ref, {error, E}} -> failed(Index, E), {ref_match(Index, Topic), unknown}
+            after ?CONF(timeout_ms, 500) ->
                 case emqx_trie_gpu_nif:cancel(H, Call) of
                     true ->
+                        failed(Index, timeout),
                         {ref_match(Index, Topic), unknown};
                     false ->
                         %% answered while we gave up: the answer is in the mailbox already
@@ -127,10 +140,15 @@ device_match(Index, H, Topic) ->
                 end
             end;
         {error, _} ->
-            %% deeper than max_levels, longer than a topic can be, every window busy, or shutting
-            %% down: the reference's own path
+            %% deeper than max_levels, longer than a topic can be, every window busy, the index
+            %% stale (estale: a repair is under way), or shutting down: the reference's own path
             {ref_match(Index, Topic), unknown}
     end.
+
+%% a window that failed or a call that timed out: the mirror repairs the index (a cast it dedups;
+%% a stale engine's refusals, estale, need none -- whoever marked it asked already)
+failed(_Index, estale) -> ok;
+failed(Index, _) -> emqx_trie_gpu_sync:repair(Index).
 
 %% emqx_router:match_trie/1
 match_trie(Topic) ->
@@ -199,10 +217,11 @@ publish_match(Topic) ->
                 {ok, Call} ->
                     receive
                         {emqx_trie_gpu, Ref, {routes, Es, Subs}} -> {ok, Es, Subs};
-                        {emqx_trie_gpu, Ref, {error, _}} -> reference
-                    after ?CONF(timeout_ms, 5000) ->
+                        {emqx_trie_gpu, Ref, {error, E}} -> failed(route, E), reference
+                    after ?CONF(timeout_ms, 500) ->
                         case emqx_trie_gpu_nif:cancel(H, Call) of
                             true ->
+                                failed(route, timeout),
                                 reference;
                             false ->
                                 receive
@@ -250,7 +269,16 @@ forward(Node, To, Delivery, async) ->
     emqx_metrics:inc('messages.forward');
 forward(Node, To, Delivery, sync) ->
     case emqx_broker_proto_v1:forward(Node, To, Delivery) of
-        {Err, _Reason} when Err =:= badrpc; Err =:= badtcp ->
+        {Err, Reason} when Err =:= badrpc; Err =:= badtcp ->
+            ?SLOG(
+                error,
+                #{
+                    msg => "sync_forward_msg_to_node_failed",
+                    node => Node,
+                    Err => Reason
+                },
+                #{topic => To}
+            ),
             {error, badrpc};
         Result ->
             emqx_metrics:inc('messages.forward'),
@@ -308,8 +336,11 @@ inc_dropped_cnt(Msg) ->
 
 %% after emqx_router:do_add_route/2 and do_delete_route/2 returned ok (emqx_router.erl:124-138,
 %% 171-179: the post-maybe_trans hook of SURVEY 8b).  Topic's rows of emqx_route, read now, go to
-%% the device and are committed before this returns: the node's next publish matches them.  A full
-%% build in the background is never waited for (emqxgm_route_dests_batch).
+%% the device and are committed before this returns: the node's next publish matches them.  Always
+%% ok: an engine that refuses the commit marks itself stale and answers nothing until the mirror's
+%% repair (publishers take the reference's path meanwhile).  When the delta does not fit the
+%% current tables while a background full build runs, the commit waits for that build's install
+%% (emqxgm_route_dests_batch, EMQXGM_SET_COMMIT; a dirty CPU scheduler is held meanwhile).
 route_changed(Topic) ->
     case handle(route) of
         undefined -> ok;
@@ -323,7 +354,10 @@ session_route_changed(Topic) ->
             ok;
         H ->
             Tab = emqx_trie_gpu_sync:table(session),
-            sync_result(emqx_trie_gpu_nif:route_sync(H, [{Topic, ets:member(Tab, Topic)}]))
+            case emqx_trie_gpu_nif:route_sync(H, [{Topic, ets:member(Tab, Topic)}]) of
+                {ok, _} -> ok;
+                {error, _} -> emqx_trie_gpu_sync:repair(session)
+            end
     end.
 
 %% after emqx_broker's do_subscribe/4, do_unsubscribe/4 and subscriber_down/1 changed Topic's
@@ -334,9 +368,11 @@ subscribers_changed(Topic) ->
         H -> sync_result(emqx_trie_gpu_nif:subscribers(H, subscriber_items([Topic]), true))
     end.
 
-%% a refused change is repaired by the mirror's next event or resync
+%% a refused change: the engine is stale now (it refuses every publisher until the repair, so no
+%% answer comes from an index without this change); the mirror repairs it.  The hook's caller
+%% (the broker pool's subscribe) goes on as the reference's would.
 sync_result({ok, _Epoch}) -> ok;
-sync_result({error, _} = E) -> emqx_trie_gpu_sync:repair(route), E.
+sync_result({error, _}) -> emqx_trie_gpu_sync:repair(route).
 
 %%--------------------------------------------------------------------
 %% Handles: the engine's 32-bit names of dests and subscribers

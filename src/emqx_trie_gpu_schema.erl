@@ -25,7 +25,10 @@
 %%   snapshot_dir        -> emqxgm_snapshot_save at the mirror's shutdown, emqxgm_snapshot_load at
 %%                          its next start (no full build; the resync commits the difference)
 %%   timeout_ms          -> how long a publisher waits for the device before it cancels and takes
-%%                          the reference's path
+%%                          the reference's path (r06: 500, was 5000)
+%%   fail_threshold      -> emqxgm_async_cfg.fail_threshold: that many timed-out calls or failed
+%%                          windows in a row mark the engines stale, so every later call is refused
+%%                          at once until the mirror's repair (include/emqx_gpumatch.h "Health")
 %%   resync_interval_ms  -> period of emqx_trie_gpu_sync's full resync (emqxgm_route_sync_*);
 %%                          default 0 (none) on a core node, whose table events all arrive, and
 %%                          30000 on a replicant
@@ -52,6 +55,7 @@ fields("gpu_match") ->
         {"spin_us", hoconsc:mk(range(0, 1000000), #{default => 0})},
         {"report_threads", hoconsc:mk(range(0, 64), #{default => 8})},
         {"snapshot_dir", hoconsc:mk(string(), #{required => false})},
-        {"timeout_ms", hoconsc:mk(range(1, 600000), #{default => 5000})},
+        {"timeout_ms", hoconsc:mk(range(1, 600000), #{default => 500})},
+        {"fail_threshold", hoconsc:mk(range(0, 1000000), #{default => 3})},
         {"resync_interval_ms", hoconsc:mk(range(0, 86400000), #{required => false})}
     ].

@@ -27,12 +27,21 @@
 %% chunks of ?CHUNK distinct topics per dirty NIF call, sync_end (removes every route key the
 %% scan did not see), commit.  Events that arrive during a scan are handled after it, against the
 %% table as it is then, so they win.
+%%
+%% Failing closed (r06).  No NIF result is matched with `ok =`: an engine that refuses a call has
+%% marked itself stale (it answers no publisher until a repair, include/emqx_gpumatch.h "Health"),
+%% and this process repairs it -- a full resync and a commit, retried with a doubling backoff
+%% (?BACKOFF_MIN .. ?BACKOFF_MAX ms) until the engines are healthy -- instead of crashing and taking
+%% emqx_broker_sup down with it after the restart intensity.  repair/1 casts (a hook's refused
+%% commit, a publisher's timeout or failed window) queued while one runs are folded into it.  The
+%% index is published after the first successful repair only.
 %%--------------------------------------------------------------------
 -module(emqx_trie_gpu_sync).
 
 -behaviour(gen_server).
 
 -include_lib("emqx/include/emqx.hrl").
+-include_lib("emqx/include/logger.hrl").
 
 -export([start_link/1, table/1, repair/1]).
 -export([init/1, handle_continue/2, handle_call/3, handle_cast/2, handle_info/2, terminate/2]).
@@ -40,6 +49,8 @@
 -define(CHUNK, 65536).       %% distinct topics per resync call
 -define(BATCH, 65536).       %% table events per device call
 -define(CONF(K, D), emqx_config:get([broker, perf, gpu_match, K], D)).
+-define(BACKOFF_MIN, 100).
+-define(BACKOFF_MAX, 30000).
 
 start_link(Index) ->
     gen_server:start_link({local, name(Index)}, ?MODULE, Index, []).
@@ -56,7 +67,7 @@ table(session) ->
         ram -> emqx_session_route_ram
     end.
 
-%% a device call was refused (out of memory): resync
+%% a device call was refused, a window failed or a publisher timed out: resync and commit
 repair(Index) ->
     gen_server:cast(name(Index), resync).
 
@@ -65,7 +76,16 @@ init(Index) ->
     %% (the handles table died with the old process)
     process_flag(trap_exit, true),
     ok = emqx_trie_gpu:publish(Index, undefined),
-    {ok, #{index => Index, h => undefined, tab => table(Index)}, {continue, open}}.
+    {ok,
+        #{
+            index => Index,
+            h => undefined,
+            tab => table(Index),
+            published => false,
+            backoff => 0,
+            retry => undefined
+        },
+        {continue, open}}.
 
 handle_continue(open, S = #{index := Index, tab := Tab}) ->
     case open(Index) of
@@ -75,15 +95,52 @@ handle_continue(open, S = #{index := Index, tab := Tab}) ->
             _ = Fresh andalso load_snapshot(Index, H),
             {ok, _} = mnesia:subscribe({table, Tab, simple}),
             S1 = S#{h := H},
-            ok = prepare(Index, H),
-            ok = resync(S1),
-            {ok, _Epoch} = emqx_trie_gpu_nif:commit(H),
-            %% only now may publishers use it (before, they take the reference's path)
-            ok = emqx_trie_gpu:publish(Index, H),
+            %% (a refused step leaves the engines unpublished until a repair succeeds)
+            _ = (catch prepare(Index, H)),
+            S2 = repair_now(S1),
             schedule_resync(),
-            {noreply, S1};
+            {noreply, S2};
         {error, Reason} ->
             {stop, {gpu_match_open, Reason}, S}
+    end.
+
+%% A full resync and a commit.  Success: the engines are healthy again (and the index is published,
+%% the first time: before, publishers take the reference's path).  Failure: retried after the
+%% backoff, which doubles up to ?BACKOFF_MAX.
+repair_now(S = #{index := Index, h := H, published := Pub, backoff := B}) ->
+    drop_queued_repairs(),
+    S1 = cancel_retry(S),
+    Result =
+        case resync(S1) of
+            ok -> emqx_trie_gpu_nif:commit(H);
+            {error, _} = E -> E
+        end,
+    case Result of
+        {ok, _Epoch} ->
+            _ = Pub orelse emqx_trie_gpu:publish(Index, H),
+            S1#{published := true, backoff := 0};
+        {error, Reason} ->
+            B1 = min(?BACKOFF_MAX, max(?BACKOFF_MIN, 2 * B)),
+            ?SLOG(warning, #{msg => "gpu_match_repair_failed", index => Index, reason => Reason,
+                             retry_ms => B1}),
+            S1#{backoff := B1, retry := erlang:send_after(B1, self(), repair)}
+    end.
+
+cancel_retry(S = #{retry := undefined}) ->
+    S;
+cancel_retry(S = #{retry := T}) ->
+    _ = erlang:cancel_timer(T),
+    receive
+        repair -> ok
+    after 0 -> ok
+    end,
+    S#{retry := undefined}.
+
+%% repair/1 casts queued behind this one: this repair covers them
+drop_queued_repairs() ->
+    receive
+        {'$gen_cast', resync} -> drop_queued_repairs()
+    after 0 -> ok
     end.
 
 %% a restart keeps the engines (and their index) it published: the resync repairs whatever
@@ -95,6 +152,7 @@ open(Index) ->
                 spin_us => ?CONF(spin_us, 0),
                 bg_build => ?CONF(bg_build, 16384),
                 report_threads => ?CONF(report_threads, 8),
+                fail_threshold => ?CONF(fail_threshold, 3),
                 publish => Index =:= route andalso ?CONF(publish, true)
             },
             case
@@ -178,10 +236,8 @@ prepare(Index, H) ->
 handle_call(_Req, _From, S) ->
     {reply, ignored, S}.
 
-handle_cast(resync, S) ->
-    ok = resync(S),
-    {ok, _} = emqx_trie_gpu_nif:commit(maps:get(h, S)),
-    {noreply, S};
+handle_cast(resync, S = #{h := H}) when H =/= undefined ->
+    {noreply, repair_now(S)};
 handle_cast(_Msg, S) ->
     {noreply, S}.
 
@@ -191,10 +247,11 @@ handle_info({mnesia_table_event, _} = E, S) ->
     Topics = collect([event_topic(E)], ?BATCH),
     {noreply, sync(Topics, S)};
 handle_info(resync, S) ->
-    ok = resync(S),
-    {ok, _Epoch} = emqx_trie_gpu_nif:commit(maps:get(h, S)),
+    S1 = repair_now(S),
     schedule_resync(),
-    {noreply, S};
+    {noreply, S1};
+handle_info(repair, S) ->
+    {noreply, repair_now(S#{retry := undefined})};
 handle_info(_Info, S) ->
     {noreply, S}.
 
@@ -219,43 +276,50 @@ sync(Topics, S = #{index := session, h := H, tab := Tab}) ->
 check({ok, _Epoch}, S) ->
     S;
 check({error, _}, S) ->
-    %% the engine refused (out of memory): a full resync retries every key
-    gen_server:cast(self(), resync),
-    S.
+    %% the engine refused (it is stale now and answers no publisher): a full resync and a commit
+    %% retry every key
+    repair_now(S).
 
 %% every topic of the table (and for the route index every local subscriber list), in chunks of
 %% ?CHUNK distinct topics per dirty NIF call; then every route key the scan did not see goes.
 %% A bag's rows of one key come together in the scan: the key is read once, with all its rows.
+%% ok | {error, Reason}: the first refused step ends it (the caller retries the whole resync)
 resync(#{index := Index, h := H, tab := Tab}) ->
-    {ok, Gen} = emqx_trie_gpu_nif:sync_begin(H),
-    Flush = fun(Topics) -> flush(Index, H, Tab, Topics) end,
-    {_, Last, _} = ets:foldl(
-        fun(Row, {Prev, Acc, N}) ->
-            case element(2, Row) of
-                Prev ->
-                    {Prev, Acc, N};
-                T when N + 1 >= ?CHUNK ->
-                    ok = Flush([T | Acc]),
-                    {T, [], 0};
-                T ->
-                    {T, [T | Acc], N + 1}
-            end
-        end,
-        {undefined, [], 0},
-        Tab
-    ),
-    ok = Flush(Last),
-    {ok, _Removed} = emqx_trie_gpu_nif:sync_end(H, Gen),
-    case Index of
-        route -> resync_subscribers(H);
-        session -> ok
+    try
+        {ok, Gen} = emqx_trie_gpu_nif:sync_begin(H),
+        Flush = fun(Topics) -> ok = flush(Index, H, Tab, Topics) end,
+        {_, Last, _} = ets:foldl(
+            fun(Row, {Prev, Acc, N}) ->
+                case element(2, Row) of
+                    Prev ->
+                        {Prev, Acc, N};
+                    T when N + 1 >= ?CHUNK ->
+                        Flush([T | Acc]),
+                        {T, [], 0};
+                    T ->
+                        {T, [T | Acc], N + 1}
+                end
+            end,
+            {undefined, [], 0},
+            Tab
+        ),
+        Flush(Last),
+        {ok, _Removed} = emqx_trie_gpu_nif:sync_end(H, Gen),
+        case Index of
+            route -> resync_subscribers(H);
+            session -> ok
+        end
+    catch
+        error:{badmatch, {error, Reason}} -> {error, Reason}
     end.
 
 flush(_Index, _H, _Tab, []) ->
     ok;
 flush(route, H, Tab, Topics) ->
-    {ok, _} = emqx_trie_gpu_nif:route_dests(H, emqx_trie_gpu:route_items(Tab, Topics), false),
-    ok;
+    case emqx_trie_gpu_nif:route_dests(H, emqx_trie_gpu:route_items(Tab, Topics), false) of
+        {ok, _} -> ok;
+        E -> E
+    end;
 flush(session, H, _Tab, Topics) ->
     emqx_trie_gpu_nif:route_set_many(H, Topics, true).
 

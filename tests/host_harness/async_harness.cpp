@@ -147,11 +147,14 @@ int emqxgm_filters_copy(emqxgm_t*, const uint32_t*, uint64_t, uint8_t*, uint64_t
   return -EIO;
 }
 
+std::atomic<int> g_hang{0};  // health mode: every wait blocks while set (a hung device)
+
 int emqxgm_match_batch_wait_filters(emqxgm_t* h, uint64_t ticket, emqxgm_batch_out* out,
                                     const uint32_t** foff, const uint8_t** fbytes) {
   // the "device" takes a while; the layer must not hold its own lock meanwhile
   thread_local std::mt19937 rng(std::hash<std::thread::id>()(std::this_thread::get_id()));
   std::this_thread::sleep_for(std::chrono::microseconds(rng() % 300));
+  while (g_hang.load()) std::this_thread::sleep_for(std::chrono::microseconds(200));
   std::lock_guard<std::mutex> g(h->mu);
   MockPipe& p = h->p[ticket % EMQXGM_HOST_PIPES];
   if (ticket == 0 || p.ticket != ticket || p.state != 1) return -ENOENT;
@@ -224,6 +227,103 @@ std::string rand_topic(std::mt19937& rng, bool filter) {
 
 }  // namespace
 
+// Health mode ("a window that never completes"): publishers that wait for
+// their answer with a deadline and cancel on timeout, as src/emqx_trie_gpu.erl does.  Phase 1 the
+// device answers; phase 2 it hangs (every wait blocks): the first calls time out, and after
+// fail_threshold timeouts the layer marks the handles stale and refuses every call at once
+// (-ESTALE) -- the bound checked is that no more than the calls in flight at the hang, plus the
+// threshold, ever pay a timeout; phase 3 the device answers again and the handles are repaired:
+// calls are accepted and answered correctly again.  Prints "OK <accepted> <reported> <cancelled>
+// <busy> <too_deep>" like the main mode.
+int health_main(unsigned seed, int threads, int handles, uint32_t window) {
+  std::mt19937 rng(seed);
+  std::vector<emqxgm> engines(handles);
+  std::vector<emqxgm_t*> hs;
+  for (auto& e : engines) hs.push_back(&e);
+  const uint64_t per_phase = 200;
+  std::vector<CallState> calls(3 * threads * per_phase);
+  g_calls = &calls;
+  std::vector<std::atomic<int64_t>> outstanding(threads);
+  g_outstanding = outstanding.data();
+  emqxgm_async_cfg cfg{};
+  cfg.window_topics = window;
+  cfg.window_us = 20;
+  cfg.fail_threshold = 3;
+  emqxgm_async_t* a = nullptr;
+  CHECK(emqxgm_async_create(hs.data(), handles, &cfg, on_window, nullptr, &a) == 0, "create");
+  std::atomic<uint64_t> accepted{0}, cancelled{0}, busy{0}, refused{0}, timeouts_paid[3];
+  for (auto& t : timeouts_paid) t = 0;
+  const auto timeout = std::chrono::milliseconds(20);
+  auto run_phase = [&](int phase) {
+    std::vector<std::thread> th;
+    for (int k = 0; k < threads; ++k) {
+      th.emplace_back([&, k, phase] {
+        std::mt19937 r(seed * 7919 + k + 1000 * phase);
+        for (uint64_t i = 0; i < per_phase; ++i) {
+          const uint64_t tag = (uint64_t)phase * threads * per_phase + k * per_phase + i;
+          CallState& c = calls[tag];
+          c.topic = r() % g_topics.size();
+          const std::string& t = g_topics[c.topic];
+          outstanding[k].fetch_add(1);
+          const int rc = emqxgm_async_match(a, (const uint8_t*)t.data(), (uint32_t)t.size(), tag, k);
+          if (rc != 0) {  // the publisher's reference path
+            outstanding[k].fetch_sub(1);
+            c.cancelled.store(2);
+            CHECK(rc == -ESTALE || rc == -EBUSY || rc == -E2BIG, "async_match %d", rc);
+            (rc == -ESTALE ? refused : busy)++;
+            CHECK(phase == 1 || rc != -ESTALE, "refused -ESTALE in phase %d", phase);
+            continue;
+          }
+          accepted++;
+          const auto t0 = std::chrono::steady_clock::now();
+          while (c.reported.load() == 0 && std::chrono::steady_clock::now() - t0 < timeout)
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+          if (c.reported.load()) continue;
+          const int cr = emqxgm_async_cancel(a, tag, k);  // timed out
+          CHECK(cr == 0 || cr == 1, "cancel %d", cr);
+          if (cr == 1) {
+            c.cancelled.store(1);
+            cancelled++;
+            timeouts_paid[phase]++;
+            outstanding[k].fetch_sub(1);
+          }
+        }
+      });
+    }
+    for (auto& t : th) t.join();
+  };
+  run_phase(0);
+  CHECK(timeouts_paid[0] == 0, "%llu timeouts with a working device",
+        (unsigned long long)timeouts_paid[0].load());
+  g_hang.store(1);
+  run_phase(1);
+  uint64_t hv[4];
+  CHECK(emqxgm_async_health(a, hv) == handles, "every handle stale after the hang (%llu)",
+        (unsigned long long)hv[0]);
+  CHECK(refused.load() > 0, "no call refused while the device hung");
+  // bounded: the calls in flight when the hang began (one per publisher) and those accepted
+  // before the threshold's third timeout
+  CHECK(timeouts_paid[1] <= (uint64_t)(2 * threads + cfg.fail_threshold),
+        "%llu calls paid a timeout (threads %d)", (unsigned long long)timeouts_paid[1].load(), threads);
+  g_hang.store(0);  // the device answers again; the mirror's repair clears the marks
+  for (auto& e : engines) e.stale.store(0);
+  run_phase(2);
+  CHECK(timeouts_paid[2] == 0, "%llu timeouts after the repair",
+        (unsigned long long)timeouts_paid[2].load());
+  emqxgm_async_destroy(a);
+  uint64_t never = 0;
+  for (auto& c : calls)
+    if (c.cancelled.load() == 0 && c.reported.load() != 1) ++never;
+  CHECK(never == 0, "%llu accepted calls never reported", (unsigned long long)never);
+  CHECK(g_reported.load() + cancelled.load() == accepted.load(), "report count");
+  fprintf(stderr, "timeouts paid %llu, refused %llu\n", (unsigned long long)timeouts_paid[1].load(),
+          (unsigned long long)refused.load());
+  printf("OK %llu %llu %llu %llu %llu\n", (unsigned long long)accepted.load(),
+         (unsigned long long)g_reported.load(), (unsigned long long)cancelled.load(),
+         (unsigned long long)busy.load(), 0ull);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const unsigned seed = argc > 1 ? atoi(argv[1]) : 1;
   const int threads = argc > 2 ? atoi(argv[2]) : 16;
@@ -231,6 +331,7 @@ int main(int argc, char** argv) {
   const uint32_t window = argc > 4 ? atoi(argv[4]) : 64;
   const uint64_t calls_per_thread = argc > 5 ? atoll(argv[5]) : 3000;
   const uint32_t cancel_every = argc > 6 ? (uint32_t)atoi(argv[6]) : 17;  // 0: no cancels
+  const bool health = argc > 7 && strcmp(argv[7], "health") == 0;
   std::mt19937 rng(seed);
   // the index: random filters (trie + route keys) and some exact keys
   std::vector<uint8_t> fb;
@@ -270,6 +371,11 @@ int main(int argc, char** argv) {
       g_want.push_back(v);
     }
     ref_free(ids);
+  }
+  if (health) {
+    const int rc = health_main(seed, threads, handles, window);
+    ref_destroy(g_ref);
+    return rc;
   }
   std::vector<emqxgm> engines(handles);
   std::vector<emqxgm_t*> hs;

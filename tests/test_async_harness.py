@@ -62,3 +62,13 @@ def test_async_layer_under_asan(seed, threads, handles, window, calls):
                  ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"])
     _run(exe, [seed, threads, handles, window, calls],
          {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=1"})
+
+
+@pytest.mark.skipif(not os.path.exists(CLANG), reason="clang++ (ThreadSanitizer runtime) absent")
+@pytest.mark.parametrize("seed,threads,handles,window", [(7, 16, 2, 64), (8, 8, 1, 16)])
+def test_hung_device_costs_one_timeout_then_refuses(seed, threads, handles, window):
+    """Health mode: the device hangs; publishers that time out cancel; after
+    fail_threshold timeouts every handle is stale and later calls are refused at once (-ESTALE);
+    after the repair calls are answered correctly again."""
+    exe = _build("async_tsan", CLANG, ["-fsanitize=thread"])
+    _run(exe, [seed, threads, handles, window, 0, 0, "health"], {"TSAN_OPTIONS": "halt_on_error=1"})
