@@ -787,20 +787,32 @@ int patch_wait(emqxgm* h);
 // Without growth and with a patch list, the new tail (whole dwords) goes into the list.  Readers
 // of committed epochs only read the prefix those epochs knew, so the tail is written while they
 // run; a grown mirror moves to a new buffer and the epochs holding the old one keep it.
+// A mirror regrown to hold `need` bytes with headroom (half again, at least 1 MiB, or double):
+// a new buffer holding [0, uploaded).  A synchronous allocation and device copy (a ~1 GB mirror at
+// cfg3: milliseconds), so it runs at full builds and on the commit paths off the hook
+// (grow_ahead), never -- while the headroom lasts -- inside a subscribe.
+int mirror_grow(emqxgm* h, Mirror& m, uint64_t need) {
+  if (int rc = patch_wait(h)) return rc;  // earlier patches into the old buffer have landed
+  DevBuf nb;
+  nb.bytes = std::max<uint64_t>(need + std::max<uint64_t>(need / 2, 1u << 20), m.b.bytes * 2);
+  nb.bytes = (nb.bytes + 15) & ~15ull;
+  HIPCHK(h, hipMalloc(&nb.p, nb.bytes));
+  auto o = std::make_shared<DevOwner>();
+  o->bufs.push_back(nb);
+  if (m.uploaded) HIPCHK(h, hipMemcpy(nb.p, m.b.p, m.uploaded, hipMemcpyDeviceToDevice));
+  m.b = nb;
+  m.o = std::move(o);  // the old buffer lives on with the epochs that read it
+  std::lock_guard<std::mutex> g(h->stmu);
+  h->st.buffer_grows += 1;
+  return 0;
+}
+
 int append_upload(emqxgm* h, Mirror& m, const void* src, uint64_t total, PatchList* pl) {
   DevBuf& buf = m.b;
   uint64_t& uploaded = m.uploaded;
   const uint64_t need = std::max<uint64_t>(16, (total + 3) & ~3ull);
   if (need > buf.bytes) {
-    if (int rc = patch_wait(h)) return rc;  // earlier patches into the old buffer have landed
-    DevBuf nb;
-    nb.bytes = std::max<uint64_t>(need, buf.bytes * 2);
-    HIPCHK(h, hipMalloc(&nb.p, nb.bytes));
-    auto o = std::make_shared<DevOwner>();
-    o->bufs.push_back(nb);
-    if (uploaded) HIPCHK(h, hipMemcpy(nb.p, buf.p, uploaded, hipMemcpyDeviceToDevice));
-    buf = nb;
-    m.o = std::move(o);  // the old buffer lives on with the epochs that read it
+    if (int rc = mirror_grow(h, m, need)) return rc;
     pl = nullptr;
   }
   if (total > uploaded) {
@@ -825,6 +837,8 @@ int patch_wait(emqxgm* h) {
   if (h->patch_ev) HIPCHK(h, hipEventSynchronize(h->patch_ev));
   return 0;
 }
+
+constexpr uint64_t PATCH_STAGE0 = 4ull << 20;  // patch staging at create (pinned and device)
 
 int patch_flush(emqxgm* h) {
   PatchList& pl = h->patches;
@@ -1823,6 +1837,18 @@ int publish_epoch(emqxgm* h, bool delta) {
     if (rc || (rc = patch_flush(h))) return rc;
   }
   HIPCHK(h, hipEventRecord(E->ready, h->wstream));
+  // an epoch that holds a buffer the new one does not (replaced tables, a regrown mirror, rebuilt
+  // fan-out tables) is heavy: its last reference frees device memory (a hipFree synchronises the
+  // device), so a subscribe's commit never sweeps it -- emqxgm_commit and the builder thread do
+  auto heavy = [&](Epoch& x) {
+    for (const OwnerP& o : x.owners)
+      if (o && std::find(E->owners.begin(), E->owners.end(), o) == E->owners.end()) {
+        x.heavy = true;
+        return;
+      }
+  };
+  if (h->cur) heavy(*h->cur);
+  for (auto& e : h->graveyard) heavy(*e);
   if (h->cur) h->graveyard.push_back(std::move(h->cur));
   h->cur = std::move(E);
   h->cur_trie_empty.store(h->cur->ix.trie_empty ? 1 : 0);
@@ -1924,6 +1950,35 @@ int full_now(emqxgm* h, std::chrono::steady_clock::time_point t0) {
   commit_stats(h, ms, false);
   std::lock_guard<std::mutex> g(h->stmu);
   h->st.last_build_ms = ms;
+  return 0;
+}
+
+// Off the hook path (emqxgm_commit, a background build's install; wmu held): an append-only
+// mirror (filter pool, offsets, verify records) past 7/8 of its buffer, or fan-out tables past 7/8
+// of their ids or pools (or with stale entries past a quarter), are regrown now, so that the
+// subscribes' delta commits keep finding room and never allocate.  The index
+// is left dirty: the caller's commit publishes the new buffers.
+int grow_ahead(emqxgm* h) {
+  bool grew = false;
+  for (Mirror* m : {&h->m_pool, &h->m_foff, &h->m_fver})
+    if (m->b.bytes && m->uploaded * 8 > m->b.bytes * 7) {
+      if (int rc = mirror_grow(h, *m, m->uploaded)) return rc;
+      grew = true;
+    }
+  if (grew) {
+    h->ix.fbytes = (const uint8_t*)h->m_pool.b.p;
+    h->ix.foff = (const uint64_t*)h->m_foff.b.p;
+    h->ix.fver = (const uint4*)h->m_fver.b.p;
+  }
+  const FanModel& fm = h->fm;
+  if (fm.valid && fm.cap &&
+      (h->filters.size() * 8 > fm.cap * 7 || fm.rt_used * 8 > fm.rt_cap * 7 ||
+       fm.dl_used * 8 > fm.dl_cap * 7 || fm.garbage * 4 > fm.rt_used + fm.dl_used + 65536)) {
+    if (int rc = patch_wait(h)) return rc;
+    if (int rc = fan_full(h)) return rc;
+    grew = true;
+  }
+  if (grew) h->dirty = true;
   return 0;
 }
 
@@ -2084,10 +2139,14 @@ int install_build(emqxgm* h, std::unique_ptr<BuildJob>& spent) {
   h->changed.clear();
   h->dirty = false;
   commit_stats(h, ms_since(t0), false);
-  std::lock_guard<std::mutex> g(h->stmu);
-  h->st.last_build_ms = J->build_ms;
-  h->st.catchup_changes = n_catchup;
-  return 0;
+  {
+    std::lock_guard<std::mutex> g(h->stmu);
+    h->st.last_build_ms = J->build_ms;
+    h->st.catchup_changes = n_catchup;
+  }
+  // room for the subscribes that follow (the install's publish already holds the index; what
+  // this regrows goes out with the next commit)
+  return grow_ahead(h);
 }
 
 // Make the pending registry the committed index (wmu held; lk: the caller's lock on it, which
@@ -2893,6 +2952,16 @@ int emqxgm_create(const emqxgm_cfg* cfg, emqxgm_t** out) {
     return -EIO;
   }
   h->wstream = h->sync.stream;
+  // the delta commits' patch staging (pinned + device) and its event, sized now: a subscribe's
+  // commit never allocates (patch_flush grows them only for larger deltas)
+  h->h_stage_bytes = h->d_patch.bytes = PATCH_STAGE0;
+  if (hipHostMalloc((void**)&h->h_stage, PATCH_STAGE0, hipHostMallocDefault) != hipSuccess ||
+      hipMalloc(&h->d_patch.p, PATCH_STAGE0) != hipSuccess ||
+      hipEventCreateWithFlags(&h->patch_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventRecord(h->patch_ev, h->wstream) != hipSuccess) {
+    emqxgm_destroy(h);
+    return -EIO;
+  }
   h->geom = walk_geometry(h->cfg.device, h->cfg.walk_wg_per_cu);
   h->geom.xrange_bytes = h->xrange_bytes;
   h->geom.pair = h->walk_pair_on;
@@ -3292,12 +3361,17 @@ int emqxgm_commit(emqxgm_t* h, uint64_t* epoch) {
     seq0 = h->stale_seq;
   }
   int rc = injected(h);
+  if (rc == 0 && !h->job) rc = grow_ahead(h);  // (a build in flight: its install does it)
   if (rc == 0) rc = commit_locked(h, &lk, true);
   if (epoch) *epoch = h->epoch;
   if (rc < 0) {
     mark_stale(h, EMQXGM_STALE_COMMIT, rc);
     return rc;
   }
+  // the replaced buffers of earlier commits are freed here, off the subscribe path (a pass that
+  // still reads one is waited for briefly; what is left goes with the next commit)
+  for (int i = 0; i < 200 && sweep_graveyard(h, true) != 0; ++i)
+    std::this_thread::sleep_for(std::chrono::microseconds(500));
   return h->stale.load() ? try_repair(h, seq0) : 0;
 }
 

@@ -26,12 +26,20 @@ hipError_t hipGetDeviceProperties(hipDeviceProp_t* p, int) {
   return hipSuccess;
 }
 const char* hipGetErrorString(hipError_t) { return "fake hip error"; }
+// device / pinned allocations and frees so far (tests/test_hook_alloc.py: a subscribe's commit
+// must not allocate)
+static unsigned long long g_allocs = 0, g_frees = 0;
+extern "C" unsigned long long fakehip_allocs(void) { return __atomic_load_n(&g_allocs, __ATOMIC_RELAXED); }
+extern "C" unsigned long long fakehip_frees(void) { return __atomic_load_n(&g_frees, __ATOMIC_RELAXED); }
+
 hipError_t hipMalloc(void** p, size_t bytes) {
+  __atomic_fetch_add(&g_allocs, 1, __ATOMIC_RELAXED);
   *p = malloc(bytes ? bytes : 1);
   if (*p) memset(*p, 0xA5, bytes);  // device memory starts undefined: poison it
   return *p ? hipSuccess : hipErrorUnknown;
 }
 hipError_t hipFree(void* p) {
+  if (p) __atomic_fetch_add(&g_frees, 1, __ATOMIC_RELAXED);
   free(p);
   return hipSuccess;
 }
