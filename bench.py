@@ -424,6 +424,9 @@ def main():
         dist.destroy_process_group()
 
 
+WATCHDOG_EXIT = 3  # the rank's exit status when the N>1 watchdog ends it
+
+
 def _guarded(run, timeout_s, rank, line):
     """run() under a watchdog thread: past timeout_s the rank ends itself (rank 0 first prints
     the line with the timeout recorded), so a collective that never completes cannot take the
@@ -440,7 +443,8 @@ def _guarded(run, timeout_s, rank, line):
         log(f"[rank {rank}] filter-sharded run timed out after {timeout_s:.0f} s: exiting")
         sys.stdout.flush()
         sys.stderr.flush()
-        os._exit(0)
+        # non-zero: a hung collective is a failure the driver must see, even with the line printed
+        os._exit(WATCHDOG_EXIT)
     threading.Thread(target=watchdog, daemon=True).start()
     try:
         r = run()

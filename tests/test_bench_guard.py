@@ -1,6 +1,6 @@
 """bench.py's watchdog around the filter-sharded N>1 run: a run that hangs
-ends the rank after the timeout with the replicas' line printed and the timeout recorded in
-config.filter_sharded; a run that raises is recorded as the result.  CPU only (no collective:
+ends the rank after the timeout -- with exit status 3 -- with the replicas' line printed and the
+timeout recorded in config.filter_sharded; a run that raises is recorded as the result.  CPU only (no collective:
 the run is a stand-in that sleeps or raises)."""
 import json
 import os
@@ -34,8 +34,9 @@ def _run(mode):
 
 
 def test_hanging_filter_sharded_run_still_prints_the_line():
+    """...and exits non-zero (a hung RCCL run must not report success)."""
     rc, out = _run("hang")
-    assert rc == 0
+    assert rc == 3  # bench.WATCHDOG_EXIT
     assert len(out) == 1, out  # one JSON line, and the code after the hang never ran
     line = json.loads(out[0])
     assert line["value"] == 1.0

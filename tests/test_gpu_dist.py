@@ -149,7 +149,7 @@ def _free_port():
     return p
 
 
-def _rank(rank, world, port, q, backend="gloo"):
+def _rank(rank, world, port, q, backend="gloo", shape=(2, 30000, 5000)):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -163,7 +163,7 @@ def _rank(rank, world, port, q, backend="gloo"):
         from emqx_amd import dist as D
         from oracle.cref import RefIndex
         dev = torch.device("cuda", gpu)
-        w = workloads.generate(2, 30000, 5000)
+        w = workloads.generate(*shape)
         mine = np.nonzero(D.filter_shards(w.fbytes, w.foff, world) == rank)[0]
         fb, fo = _subset(w, mine)
         eng = Engine(device=gpu)
@@ -225,3 +225,31 @@ def test_sharded_matcher_two_ranks(emqx, backend):
     status, pairs, on_rank0 = q.get(timeout=5)
     assert status == "ok", status
     assert pairs > 0 and on_rank0 > 0
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("backend", ["gloo", "nccl"])
+def test_sharded_matcher_cfg3_slice_every_gpu(emqx, backend):
+    """The north-star layout at a BASELINE shape: a 1M-filter slice of cfg3
+    (site/+/device/+/#) sharded by filter hash, 200k topics broadcast, the wire results merged on
+    rank 0 -- every row and exact id equal to the unsharded oracle's (oracle/ref_trie.cpp).  nccl:
+    one rank per GPU over RCCL on every GPU of the node (up to 8), skipped on a one-GPU box (the
+    first multi-GPU GPUTEST pins it); gloo: the same control flow with two ranks sharing this
+    box's GPU."""
+    world = 2 if backend == "gloo" else min(torch.cuda.device_count(), 8)
+    if world < 2:
+        pytest.skip("the RCCL branch needs two or more GPUs (this box has one)")
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q, backend, (3, 1_000_000, 200_000)))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(840)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    status, pairs, on_rank0 = q.get(timeout=5)
+    assert status == "ok", status
+    assert pairs > 1_000_000 and on_rank0 > 0
