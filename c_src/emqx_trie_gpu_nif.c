@@ -40,12 +40,17 @@
 
 /* The terms the engine's 32-bit handles stand for (node atoms, shared-subscription groups,
  * subscriber pids), registered by the mirror: the engine's fan-out answers in handles, a
- * publisher gets the terms. */
+ * publisher gets the terms.  Each slot holds its copy in an environment of its own, freed when
+ * the handle is released (r06: handles are reused, emqxgm_handles_*, so the table stays as large
+ * as the live subscribers, not as every pid ever seen). */
+typedef struct {
+  ErlNifEnv* env; /* NULL: no term */
+  ERL_NIF_TERM t;
+} term_slot;
 typedef struct {
   ErlNifRWLock* lk;
-  ErlNifEnv* env; /* holds the copies (a re-registered handle's old copy stays until unload) */
-  ERL_NIF_TERM* v;
-  unsigned n;     /* handles [0, n) have a slot; v[i] == 0: none */
+  term_slot* v;
+  unsigned n;     /* handles [0, n) have a slot */
 } term_tab;
 
 typedef struct {
@@ -53,6 +58,7 @@ typedef struct {
   emqxgm_t* h[GM_MAX_DEVICES];
   emqxgm_async_t* a;  /* match_async */
   emqxgm_async_t* ap; /* publish_async (open option publish) */
+  emqxgm_handles_t* hr; /* the handle numbers (node 0, group 1, sub 2), reused after quiescence */
   uint64_t next_tag;  /* call tags: unique per resource, so a stale one never matches a cancel */
   term_tab nodes, groups, subs;
 } gm_res;
@@ -73,27 +79,29 @@ static ERL_NIF_TERM A_OK, A_ERROR, A_TRUE, A_FALSE, A_MOD, A_ROUTES, A_NONE, A_N
 
 static int tab_init(term_tab* t, char* name) {
   t->lk = enif_rwlock_create(name);
-  t->env = enif_alloc_env();
   t->v = NULL;
   t->n = 0;
-  return t->lk && t->env;
+  return t->lk != NULL;
 }
 
 static void tab_free(term_tab* t) {
   if (t->lk) enif_rwlock_destroy(t->lk);
-  if (t->env) enif_free_env(t->env);
+  for (unsigned i = 0; i < t->n; ++i)
+    if (t->v[i].env) enif_free_env(t->v[i].env);
   enif_free(t->v);
   memset(t, 0, sizeof *t);
 }
 
 /* the term behind handle h copied into env, or `undefined` (caller holds the read lock) */
 static ERL_NIF_TERM tab_get(ErlNifEnv* env, const term_tab* t, uint32_t h) {
-  return (h < t->n && t->v[h]) ? enif_make_copy(env, t->v[h]) : A_UNDEFINED;
+  return (h < t->n && t->v[h].env) ? enif_make_copy(env, t->v[h].t) : A_UNDEFINED;
 }
 
 static void gm_res_dtor(ErlNifEnv* env, void* obj) {
   gm_res* r = (gm_res*)obj;
   (void)env;
+  if (r->hr) emqxgm_handles_destroy(r->hr);
+  r->hr = NULL;
   if (r->a) emqxgm_async_destroy(r->a); /* reports every accepted call first */
   if (r->ap) emqxgm_async_destroy(r->ap);
   for (unsigned k = 0; k < r->nh; ++k)
@@ -284,6 +292,10 @@ static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
   if (!rc && publish) {
     ac.flags = EMQXGM_ASYNC_PUBLISH;
     rc = emqxgm_async_create(r->h, r->nh, &ac, on_window, r, &r->ap);
+  }
+  if (!rc) {
+    emqxgm_async_t* layers[2] = {r->a, r->ap};
+    rc = emqxgm_handles_create(layers, r->ap ? 2 : 1, &r->hr);
   }
   if (rc) {
     enif_release_resource(r); /* the destructor frees what was made */
@@ -624,20 +636,91 @@ static ERL_NIF_TERM nif_register(ErlNifEnv* env, int argc, const ERL_NIF_TERM ar
     if (hv >= t->n) {
       unsigned n2 = t->n ? t->n : 64;
       while (n2 <= hv) n2 *= 2;
-      ERL_NIF_TERM* v = enif_realloc(t->v, sizeof(ERL_NIF_TERM) * n2);
+      term_slot* v = enif_realloc(t->v, sizeof(term_slot) * n2);
       if (!v) {
         bad = 2;
         break;
       }
-      memset(v + t->n, 0, sizeof(ERL_NIF_TERM) * (n2 - t->n));
+      memset(v + t->n, 0, sizeof(term_slot) * (n2 - t->n));
       t->v = v;
       t->n = n2;
     }
-    t->v[hv] = enif_make_copy(t->env, el[1]);
+    term_slot* sl = &t->v[hv];
+    if (sl->env) {
+      enif_clear_env(sl->env);
+    } else if (!(sl->env = enif_alloc_env())) {
+      bad = 2;
+      break;
+    }
+    sl->t = enif_make_copy(sl->env, el[1]);
   }
   enif_rwlock_rwunlock(t->lk);
   if (bad == 1) return enif_make_badarg(env);
   return bad ? err_term(env, -ENOMEM) : A_OK;
+}
+
+static term_tab* kind_tab(gm_res* r, ERL_NIF_TERM k, uint32_t* kind) {
+  if (k == A_NODE) return *kind = 0, &r->nodes;
+  if (k == A_GROUP) return *kind = 1, &r->groups;
+  if (k == A_SUB) return *kind = 2, &r->subs;
+  return NULL;
+}
+
+/* alloc_handle(Res, node | group | sub) -> {ok, N} | {error, e2big}: a handle number for a new
+ * term (emqxgm_handles_alloc: a released one once every window submitted before its release was
+ * answered, else a never-used one); register/3 then gives it its term */
+static ERL_NIF_TERM nif_alloc_handle(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_res* r;
+  uint32_t kind, h;
+  (void)argc;
+  if (!get_res(env, argv[0], &r) || !r->hr || !kind_tab(r, argv[1], &kind)) return enif_make_badarg(env);
+  const int rc = emqxgm_handles_alloc(r->hr, kind, &h);
+  return rc ? err_term(env, rc) : enif_make_tuple2(env, A_OK, enif_make_uint(env, h));
+}
+
+/* release_handle(Res, node | group | sub, N) -> ok | {error, enoent}: N's term is gone from
+ * every list on the device (the hooks that removed it committed): its term copy is freed now
+ * (a window still in flight answers `undefined` for it, which dispatch skips) and the number is
+ * reused once the windows submitted before now are answered (emqx_broker.erl:361-380) */
+static ERL_NIF_TERM nif_release_handle(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_res* r;
+  uint32_t kind;
+  unsigned hv;
+  (void)argc;
+  term_tab* t;
+  if (!get_res(env, argv[0], &r) || !r->hr || !(t = kind_tab(r, argv[1], &kind)) ||
+      !enif_get_uint(env, argv[2], &hv))
+    return enif_make_badarg(env);
+  enif_rwlock_rwlock(t->lk);
+  if (hv < t->n && t->v[hv].env) {
+    enif_free_env(t->v[hv].env);
+    t->v[hv].env = NULL;
+    t->v[hv].t = 0;
+  }
+  enif_rwlock_rwunlock(t->lk);
+  const int rc = emqxgm_handles_release(r->hr, kind, hv);
+  return rc ? err_term(env, rc) : A_OK;
+}
+
+/* reset_handles(Res) -> ok: every allocated handle of every kind released and its term copy
+ * freed (a restarted mirror, whose handles table died with the old process) */
+static ERL_NIF_TERM nif_reset_handles(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  gm_res* r;
+  (void)argc;
+  if (!get_res(env, argv[0], &r) || !r->hr) return enif_make_badarg(env);
+  term_tab* tabs[3] = {&r->nodes, &r->groups, &r->subs};
+  for (int k = 0; k < 3; ++k) {
+    term_tab* t = tabs[k];
+    enif_rwlock_rwlock(t->lk);
+    for (unsigned i = 0; i < t->n; ++i)
+      if (t->v[i].env) {
+        enif_free_env(t->v[i].env);
+        t->v[i].env = NULL;
+      }
+    enif_rwlock_rwunlock(t->lk);
+  }
+  const int rc = emqxgm_handles_reset(r->hr);
+  return rc ? err_term(env, rc) : A_OK;
 }
 
 /* set_local_node(Res, NodeH) -> ok: node()'s dest handle (emqxgm_set_local_node) */
@@ -1150,6 +1233,9 @@ static ErlNifFunc funcs[] = {
     {"route_dests", 3, nif_route_dests, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"subscribers", 3, nif_subscribers, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"register", 3, nif_register, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"alloc_handle", 2, nif_alloc_handle, 0},
+    {"release_handle", 3, nif_release_handle, 0},
+    {"reset_handles", 1, nif_reset_handles, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"set_local_node", 2, nif_set_local_node, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"sync_begin", 1, nif_sync_begin, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"sync_end", 2, nif_sync_end, ERL_NIF_DIRTY_JOB_CPU_BOUND},

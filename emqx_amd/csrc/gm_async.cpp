@@ -80,6 +80,7 @@ struct Slot {
   int status = 0;         // a failed submit's error (the completer reports it)
   uint32_t hi = 0;        // handle it went to
   uint64_t ticket = 0, flush_ns = 0;
+  uint64_t seq = 0;       // submission order (the handle registry's quiescence marks)
 };
 
 // Calls on their way into a window: a thread's staging chunk, or one long call on its own.
@@ -158,6 +159,22 @@ struct emqxgm_async {
   // that timed out, windows that failed -- until every handle is marked stale
   std::atomic<uint32_t> fails{0};
   std::atomic<uint64_t> st_timeouts{0}, st_failed{0}, st_stale{0};
+  uint64_t submit_seq = 1;  // the next window's submission number (mu)
+
+  // The handle registry's quiescence (emqxgm_handles_*): mark() = the next submission number;
+  // passed(m): every window submitted before the mark has been reported (its pass read whatever
+  // epoch it took; later windows take epochs published before the mark)
+  uint64_t mark() {
+    std::lock_guard<std::mutex> g(mu);
+    return submit_seq;
+  }
+  bool passed(uint64_t m) {
+    std::lock_guard<std::mutex> g(mu);
+    for (auto& sp : slots)
+      if ((sp->state == SUBMITTING || sp->state == INFLIGHT || sp->state == DELIVERING) && sp->seq < m)
+        return false;
+    return true;
+  }
 
   bool all_stale() const {
     for (emqxgm_t* h : hs)
@@ -460,6 +477,7 @@ struct emqxgm_async {
         }
         rr = (k + 1) % H;
         s.state = SUBMITTING;
+        s.seq = submit_seq++;
         s.hi = k;
         outstanding[k] += 1;
         g.unlock();
@@ -842,6 +860,120 @@ int emqxgm_async_stats(emqxgm_async_t* a, uint64_t out[8]) {
   uint64_t q = 0;
   for (auto v : a->outstanding) q += v;
   out[7] = q;
+  return 0;
+}
+
+}  // extern "C"
+
+// ---- the handle registry (include/emqx_gpumatch.h "Handle registry") ----
+struct emqxgm_handles {
+  std::mutex mu;
+  std::vector<emqxgm_async*> layers;
+  struct Kind {
+    uint32_t next = 0;                 // numbers made so far
+    std::vector<uint32_t> free_;       // released and quiesced: reused first
+    struct Limbo {
+      uint32_t h;
+      std::vector<uint64_t> marks;     // each layer's mark at the release
+    };
+    std::deque<Limbo> limbo;           // released, windows from before the release in flight
+    std::vector<uint8_t> live;         // per number: 1 allocated, 0 not
+    uint64_t n_live = 0;
+  } k[EMQXGM_HANDLE_KINDS];
+
+  // limbo entries whose marks every layer has passed become free (in release order: marks only
+  // grow, so the first entry not passed stops the scan)
+  void promote(Kind& K) {
+    while (!K.limbo.empty()) {
+      const auto& e = K.limbo.front();
+      for (size_t i = 0; i < layers.size(); ++i)
+        if (!layers[i]->passed(e.marks[i])) return;
+      K.free_.push_back(e.h);
+      K.limbo.pop_front();
+    }
+  }
+};
+
+extern "C" {
+
+int emqxgm_handles_create(emqxgm_async_t* const* layers, uint32_t n_layers, emqxgm_handles_t** out) {
+  if (!out || (n_layers && !layers)) return -EINVAL;
+  *out = nullptr;
+  emqxgm_handles* r = new (std::nothrow) emqxgm_handles();
+  if (!r) return -ENOMEM;
+  for (uint32_t i = 0; i < n_layers; ++i) {
+    if (!layers[i]) {
+      delete r;
+      return -EINVAL;
+    }
+    r->layers.push_back(layers[i]);
+  }
+  *out = r;
+  return 0;
+}
+
+void emqxgm_handles_destroy(emqxgm_handles_t* r) { delete r; }
+
+int emqxgm_handles_alloc(emqxgm_handles_t* r, uint32_t kind, uint32_t* handle) {
+  if (!r || !handle || kind >= EMQXGM_HANDLE_KINDS) return -EINVAL;
+  std::lock_guard<std::mutex> g(r->mu);
+  auto& K = r->k[kind];
+  if (K.free_.empty()) r->promote(K);
+  uint32_t h;
+  if (!K.free_.empty()) {
+    h = K.free_.back();
+    K.free_.pop_back();
+  } else {
+    if (K.next >= EMQXGM_HANDLE_MAX) return -E2BIG;
+    h = K.next++;
+    K.live.push_back(0);
+  }
+  K.live[h] = 1;
+  K.n_live += 1;
+  *handle = h;
+  return 0;
+}
+
+int emqxgm_handles_release(emqxgm_handles_t* r, uint32_t kind, uint32_t handle) {
+  if (!r || kind >= EMQXGM_HANDLE_KINDS) return -EINVAL;
+  std::lock_guard<std::mutex> g(r->mu);
+  auto& K = r->k[kind];
+  if (handle >= K.next || !K.live[handle]) return -ENOENT;
+  K.live[handle] = 0;
+  K.n_live -= 1;
+  emqxgm_handles::Kind::Limbo e;
+  e.h = handle;
+  for (emqxgm_async* a : r->layers) e.marks.push_back(a->mark());
+  K.limbo.push_back(std::move(e));
+  r->promote(K);
+  return 0;
+}
+
+int emqxgm_handles_reset(emqxgm_handles_t* r) {
+  if (!r) return -EINVAL;
+  std::lock_guard<std::mutex> g(r->mu);
+  std::vector<uint64_t> marks;
+  for (emqxgm_async* a : r->layers) marks.push_back(a->mark());
+  for (auto& K : r->k) {
+    for (uint32_t h = 0; h < K.next; ++h)
+      if (K.live[h]) {
+        K.live[h] = 0;
+        K.limbo.push_back(emqxgm_handles::Kind::Limbo{h, marks});
+      }
+    K.n_live = 0;
+    r->promote(K);
+  }
+  return 0;
+}
+
+int emqxgm_handles_stats(emqxgm_handles_t* r, uint32_t kind, uint64_t out[4]) {
+  if (!r || !out || kind >= EMQXGM_HANDLE_KINDS) return -EINVAL;
+  std::lock_guard<std::mutex> g(r->mu);
+  auto& K = r->k[kind];
+  out[0] = K.next;
+  out[1] = K.n_live;
+  out[2] = K.limbo.size();
+  out[3] = K.free_.size();
   return 0;
 }
 

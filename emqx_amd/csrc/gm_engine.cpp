@@ -438,6 +438,10 @@ struct emqxgm {
   bool dirty = false;
   // emqxgm_route_sync_begin/_end: generation of the resync in progress (0: none)
   uint32_t sync_gen = 0, sync_next = 1;
+  // filters whose local subscriber list a set call gave during the resync in progress (bitmap):
+  // _end clears every other list (a topic whose subscribers all went is absent from the table
+  // the resync scans; its old list must not survive it -- r06, with handle reuse)
+  std::vector<uint64_t> sub_seen;
 
   // ---- the writer's working copy of the committed index (published as epochs) ----
   uint64_t epoch = 0;
@@ -3153,6 +3157,18 @@ int emqxgm_route_sync_end(emqxgm_t* h, uint32_t gen, uint64_t* removed) {
       ++k;
     }
   }
+  // local subscriber lists the resync did not give (their topics left the subscriber table)
+  for (auto it = h->lsubs.begin(); it != h->lsubs.end();) {
+    const uint64_t id = it->first;
+    if ((id >> 6) < h->sub_seen.size() && bit(h->sub_seen, id)) {
+      ++it;
+      continue;
+    }
+    h->fan_changed.push_back(it->first);
+    h->dirty = true;
+    it = h->lsubs.erase(it);
+  }
+  std::vector<uint64_t>().swap(h->sub_seen);
   h->sync_gen = 0;
   if (removed) *removed = k;
   std::lock_guard<std::mutex> hg(h->hmu);
@@ -3556,6 +3572,10 @@ int emqxgm_subscribers_batch(emqxgm_t* h, const uint8_t* bytes, const uint64_t* 
       }
       const uint32_t id = find_id(h, p, len, !ss.empty());
       if (id == NONE) continue;
+      if (h->sync_gen) {
+        if (((uint64_t)id >> 6) >= h->sub_seen.size()) h->sub_seen.resize(((uint64_t)id >> 6) + 1, 0);
+        bset(h->sub_seen, id);
+      }
       auto it = h->lsubs.find(id);
       std::vector<uint32_t> old;
       if (it != h->lsubs.end()) old = it->second;

@@ -216,6 +216,12 @@ SYMBOLS = {
     "emqxgm_async_cancel": (C.c_int, [_P, C.c_uint64, C.c_uint64]),
     "emqxgm_async_stats": (C.c_int, [_P, _U64P]),
     "emqxgm_async_health": (C.c_int, [_P, _U64P]),
+    "emqxgm_handles_create": (C.c_int, [_P, C.c_uint32, C.POINTER(_P)]),
+    "emqxgm_handles_destroy": (None, [_P]),
+    "emqxgm_handles_alloc": (C.c_int, [_P, C.c_uint32, _U32P]),
+    "emqxgm_handles_release": (C.c_int, [_P, C.c_uint32, C.c_uint32]),
+    "emqxgm_handles_reset": (C.c_int, [_P]),
+    "emqxgm_handles_stats": (C.c_int, [_P, C.c_uint32, _U64P]),
     "emqxgm_set_profiling": (C.c_int, [_P, C.c_int]),
     "emqxgm_tune": (C.c_int, [_P, C.c_char_p, C.c_int64]),
     "emqxgm_get_stats": (C.c_int, [_P, C.POINTER(_Stats)]),
@@ -943,6 +949,55 @@ class AsyncMatcher:
         if getattr(self, "_a", None):
             self._lib.emqxgm_async_destroy(self._a)  # reports every accepted call first
             self._a = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class HandleRegistry:
+    """emqxgm_handles_*: the 32-bit names of dest and subscriber terms, reused once every window
+    the layers submitted before a release has been answered (include/emqx_gpumatch.h "Handle
+    registry"; the NIF's alloc_handle/2, release_handle/3, reset_handles/1)."""
+    KINDS = {"node": 0, "group": 1, "sub": 2}
+
+    def __init__(self, layers: Sequence["AsyncMatcher"] = (), library: Optional[C.CDLL] = None):
+        self._layers = list(layers)  # kept alive: the registry reads their windows
+        self._lib = library or (self._layers[0]._lib if self._layers else lib())
+        arr = (C.c_void_p * max(1, len(self._layers)))(*[x._a for x in self._layers])
+        r = C.c_void_p()
+        rc = self._lib.emqxgm_handles_create(arr, len(self._layers), C.byref(r))
+        if rc:
+            raise EngineError(f"handles_create: {errno.errorcode.get(-rc, rc)}")
+        self._r = r
+
+    def _chk(self, rc, what):
+        if rc < 0:
+            raise EngineError(f"{what}: {errno.errorcode.get(-rc, rc)}")
+        return rc
+
+    def alloc(self, kind: str) -> int:
+        h = C.c_uint32()
+        self._chk(self._lib.emqxgm_handles_alloc(self._r, self.KINDS[kind], C.byref(h)), "alloc")
+        return int(h.value)
+
+    def release(self, kind: str, h: int) -> None:
+        self._chk(self._lib.emqxgm_handles_release(self._r, self.KINDS[kind], h), "release")
+
+    def reset(self) -> None:
+        self._chk(self._lib.emqxgm_handles_reset(self._r), "reset")
+
+    def stats(self, kind: str) -> dict:
+        v = (C.c_uint64 * 4)()
+        self._chk(self._lib.emqxgm_handles_stats(self._r, self.KINDS[kind], v), "stats")
+        return dict(zip(("made", "live", "waiting", "free"), list(v)))
+
+    def close(self):
+        if getattr(self, "_r", None):
+            self._lib.emqxgm_handles_destroy(self._r)
+            self._r = None
 
     def __del__(self):
         try:

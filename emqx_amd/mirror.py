@@ -41,18 +41,36 @@ from .engine import NONE, EngineError
 
 class Handles:
     """The engine's 32-bit names of dests (nodes, groups) and subscribers (emqx_trie_gpu's
-    handles table; the NIF maps them back to terms)."""
+    handles table; the NIF maps them back to terms).  Numbers come from the handle registry
+    (emqxgm_handles_*: a released number is reused once the windows submitted before its release
+    were answered); without one, from a counter."""
 
-    def __init__(self):
+    def __init__(self, registry=None):
         self.ids: Dict[Tuple[str, Hashable], int] = {}
-        self.names: Dict[str, List[Hashable]] = {"node": [], "group": [], "sub": []}
+        self.names: Dict[str, Dict[int, Hashable]] = {"node": {}, "group": {}, "sub": {}}
+        self.registry = registry
+        self._next = {"node": 0, "group": 0, "sub": 0}
 
     def __call__(self, kind: str, name: Hashable) -> int:
         k = (kind, name)
         if k not in self.ids:
-            self.ids[k] = len(self.names[kind])
-            self.names[kind].append(name)
+            if self.registry is not None:
+                h = self.registry.alloc(kind)
+            else:
+                h = self._next[kind]
+                self._next[kind] += 1
+            self.ids[k] = h
+            self.names[kind][h] = name
         return self.ids[k]
+
+    def release(self, kind: str, name: Hashable) -> None:
+        """term gone (emqx_trie_gpu:subscriber_down/1 -> the NIF's release_handle/3)."""
+        h = self.ids.pop((kind, name), None)
+        if h is None:
+            return
+        del self.names[kind][h]
+        if self.registry is not None:
+            self.registry.release(kind, h)
 
     def dest(self, d) -> Tuple[int, int]:
         if isinstance(d, tuple):  # {Group, Node}
@@ -64,11 +82,11 @@ class RouteTableMirror:
     BACKOFF_MS = (100, 30000)  # the repair's first retry and its cap (emqx_trie_gpu_sync.erl)
 
     def __init__(self, engines: Sequence, table, subscribers: Optional[Dict] = None,
-                 local_node: Hashable = "n1", chunk: int = 65536):
+                 local_node: Hashable = "n1", chunk: int = 65536, registry=None):
         self.engines = list(engines)
         self.table = table
         self.subscribers = subscribers
-        self.handles = Handles()
+        self.handles = Handles(registry)
         self.chunk = chunk
         self.queue: Deque[Tuple[str, bytes]] = deque()  # the process's mailbox of table events
         self.local = self.handles("node", local_node)  # set on the engines by init()
@@ -146,6 +164,13 @@ class RouteTableMirror:
             self._refused()
         return "ok"
 
+    def subscriber_down(self, sub: Hashable) -> str:
+        """emqx_trie_gpu:subscriber_down/1, after emqx_broker:subscriber_down/1 removed the
+        subscriber's rows and each of its topics' subscribers_changed/1 committed: its handle goes
+        back to the registry (emqx_broker.erl:361-380)."""
+        self.handles.release("sub", sub)
+        return "ok"
+
     def resync(self) -> int:
         """A full resync: every topic of the table in chunks, every other route key removed,
         every subscriber list set.  Returns how many route keys the sweep removed; raises
@@ -154,9 +179,10 @@ class RouteTableMirror:
         topics = list(self.table.topics())
         for i in range(0, len(topics), self.chunk):
             self._dests(topics[i:i + self.chunk], commit=False)
-        removed = [e.sync_end(g) for e, g in zip(self.engines, gens)]
+        # the subscriber lists before sync_end, which clears every list the resync did not give
         for t in sorted(self.subscribers or {}):
             self._subs(t, commit=False)
+        removed = [e.sync_end(g) for e, g in zip(self.engines, gens)]
         return removed[0] if removed else 0
 
     def commit(self) -> None:

@@ -576,6 +576,33 @@ int emqxgm_async_stats(emqxgm_async_t* a, uint64_t out[8]);
  * calls refused with -ESTALE}.  Returns out[0]. */
 int emqxgm_async_health(emqxgm_async_t* a, uint64_t out[4]);
 
+/* ---- handle registry: the 32-bit names of dest and subscriber terms, reused (r06) ----------
+ * The engine's fan-out tables name nodes, shared-subscription groups and subscribers by handles
+ * the caller chooses (emqxgm_route_dests_batch / _subscribers_batch); the NIF maps them back to
+ * terms.  A broker whose clients reconnect sees a new subscriber pid per connection, so handles
+ * must be reused or the tables grow without bound (the reference's subscriber_down/1 removes every
+ * trace of a pid, emqx_broker.erl:361-380, emqx_broker_helper.erl:133-165).  A handle may be
+ * reused only when no answer can still name it for its old term: the caller releases it after the
+ * commit that removed it from every list (its lists were set without it and committed), and the
+ * registry hands it out again only once every window the layers had submitted before the release
+ * has been reported (windows submitted later read an epoch without it).  _alloc: a quiesced
+ * released handle of `kind`, else the next never-used number (-E2BIG past EMQXGM_HANDLE_MAX);
+ * _release: -ENOENT if not allocated; _stats: {numbers made, allocated, released and waiting for
+ * their windows, free}.  Thread-safe.  A released subscriber's lists must all have been committed
+ * without it; a full resync (emqxgm_route_sync_begin .. _end) clears every subscriber list it did
+ * not set, so a topic whose last subscriber left cannot keep a reused number. */
+#define EMQXGM_HANDLE_KINDS 3 /* 0 node, 1 group, 2 subscriber */
+#define EMQXGM_HANDLE_MAX 0x7FFFFFFFu
+typedef struct emqxgm_handles emqxgm_handles_t;
+int emqxgm_handles_create(emqxgm_async_t* const* layers, uint32_t n_layers, emqxgm_handles_t** out);
+void emqxgm_handles_destroy(emqxgm_handles_t* r);
+int emqxgm_handles_alloc(emqxgm_handles_t* r, uint32_t kind, uint32_t* handle);
+int emqxgm_handles_release(emqxgm_handles_t* r, uint32_t kind, uint32_t handle);
+int emqxgm_handles_stats(emqxgm_handles_t* r, uint32_t kind, uint64_t out[4]);
+/* every allocated handle of every kind released at once (a restarted mirror whose own table of
+ * them was lost; its resync then rewrites every list) */
+int emqxgm_handles_reset(emqxgm_handles_t* r);
+
 /* ---- filter-sharded layout over several GPUs (the subscription set partitioned by
  * filter, the topic batch broadcast, the per-GPU match lists gathered to one GPU) ----
  * emqxgm_export copies a device-resident result (emqxgm_match_device / _wait) into the caller's

@@ -45,7 +45,7 @@
 -export([match/1, match_session/1, match_trie/1, match_routes/1, empty/0, empty_session/0]).
 -export([route/2]).
 %% the writing node's hooks (INTEGRATION.md 4) and the mirror's helpers
--export([route_changed/1, session_route_changed/1, subscribers_changed/1]).
+-export([route_changed/1, session_route_changed/1, subscribers_changed/1, subscriber_down/1]).
 -export([route_items/2, subscriber_items/1, dest_handles/1, handles_table/0]).
 
 -define(KEY(Index), {?MODULE, Index}).
@@ -405,20 +405,46 @@ subscribers(Topic) ->
         [S || {_, S} <- ets:lookup(emqx_subscriber, Topic)]
     ).
 
-%% the handle of Term (allocated and registered with the NIF on first use; never reused)
+%% the handle of Term: allocated by the NIF's handle registry (a released number once every
+%% window submitted before its release was answered, else a new one) and registered on first use.
+%% Only called once the route index's engines are open (emqx_trie_gpu_sync:prepare/2 publishes the
+%% registry before it makes the first handle; the hooks run once the index is published).
 term_handle(Kind, Term) ->
     case ets:lookup(?HANDLES, {Kind, Term}) of
         [{_, H}] ->
             H;
         [] ->
-            N = ets:update_counter(?HANDLES, {next, Kind}, 1, {{next, Kind}, -1}),
+            N = new_handle(Kind),
             case ets:insert_new(?HANDLES, {{Kind, Term}, N}) of
                 true ->
                     ok = register_term(Kind, N, Term),
                     N;
                 false ->
+                    %% another process made Term's handle first: N was never in a list
+                    ok = release_number(Kind, N),
                     term_handle(Kind, Term)
             end
+    end.
+
+new_handle(Kind) ->
+    {ok, N} = emqx_trie_gpu_nif:alloc_handle(persistent_term:get(?KEY(registry)), Kind),
+    N.
+
+release_number(Kind, N) ->
+    case persistent_term:get(?KEY(registry), undefined) of
+        undefined -> ok;
+        H -> _ = emqx_trie_gpu_nif:release_handle(H, Kind, N), ok
+    end.
+
+%% after emqx_broker:subscriber_down/1 (emqx_broker.erl:361-380) removed SubPid's rows and the
+%% subscribers_changed/1 hook of each of its topics committed the lists without it: SubPid's handle
+%% goes back to the registry and its term copy is freed, so a broker whose clients reconnect (a new
+%% pid per connection) keeps handle and term tables as large as its live subscribers
+%% (emqx_broker_helper.erl:133-165 removes every trace of the pid likewise).
+subscriber_down(SubPid) ->
+    case ets:take(?HANDLES, {sub, SubPid}) of
+        [{_, N}] -> release_number(sub, N);
+        [] -> ok
     end.
 
 %% (registered as soon as the route index's engines are open: emqx_trie_gpu_sync sweeps the

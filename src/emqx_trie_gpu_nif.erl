@@ -12,6 +12,9 @@
     route_dests/3,
     subscribers/3,
     register/3,
+    alloc_handle/2,
+    release_handle/3,
+    reset_handles/1,
     set_local_node/2,
     sync_begin/1,
     sync_end/2,
@@ -63,6 +66,15 @@ route_dests(_Res, _Items, _Commit) -> ?NOT_LOADED.
 subscribers(_Res, _Items, _Commit) -> ?NOT_LOADED.
 %% register(Res, node | group | sub, [{Handle, Term}]) -> ok
 register(_Res, _Kind, _Items) -> ?NOT_LOADED.
+
+%% alloc_handle(Res, node | group | sub) -> {ok, N} | {error, e2big}
+alloc_handle(_Res, _Kind) -> ?NOT_LOADED.
+
+%% release_handle(Res, node | group | sub, N) -> ok | {error, enoent}
+release_handle(_Res, _Kind, _N) -> ?NOT_LOADED.
+
+%% reset_handles(Res) -> ok: every handle released (a restarted mirror's, whose table died)
+reset_handles(_Res) -> ?NOT_LOADED.
 %% set_local_node(Res, NodeH) -> ok
 set_local_node(_Res, _NodeH) -> ?NOT_LOADED.
 %% sync_begin(Res) -> {ok, Gen}

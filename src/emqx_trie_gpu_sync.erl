@@ -24,8 +24,8 @@
 %% Full resyncs: at start (handle_continue, so the supervisor is not held) and, where table events
 %% may be missed -- a mria replicant, whose route shard is replayed from the core nodes' rlog
 %% (emqx_router.erl:78-92) -- every resync_interval_ms.  sync_begin, every topic of the table in
-%% chunks of ?CHUNK distinct topics per dirty NIF call, sync_end (removes every route key the
-%% scan did not see), commit.  Events that arrive during a scan are handled after it, against the
+%% chunks of ?CHUNK distinct topics per dirty NIF call, the local subscriber lists, sync_end
+%% (removes every route key and subscriber list the scan did not give), commit.  Events that arrive during a scan are handled after it, against the
 %% table as it is then, so they win.
 %%
 %% Failing closed (r06).  No NIF result is matched with `ok =`: an engine that refuses a call has
@@ -221,6 +221,10 @@ prepare(Index, H) ->
             Tab = emqx_trie_gpu:handles_table(),
             _ = ets:info(Tab, name) =:= undefined andalso
                 ets:new(Tab, [named_table, public, set, {read_concurrency, true}]),
+            %% a restarted mirror's handles table died with the old process: every number the
+            %% engines' registry still holds goes back (reused once the windows in flight are
+            %% answered; the resync rewrites every list with the new numbers)
+            ok = emqx_trie_gpu_nif:reset_handles(H),
             ok = emqx_trie_gpu:publish(registry, H),
             {NodeH, none} = hd(emqx_trie_gpu:dest_handles([node()])),
             lists:foreach(
@@ -304,11 +308,15 @@ resync(#{index := Index, h := H, tab := Tab}) ->
             Tab
         ),
         Flush(Last),
+        %% the subscriber lists before sync_end: it clears every list the resync did not give
+        %% (a topic whose subscribers all left is not in the table any more)
+        ok =
+            case Index of
+                route -> resync_subscribers(H);
+                session -> ok
+            end,
         {ok, _Removed} = emqx_trie_gpu_nif:sync_end(H, Gen),
-        case Index of
-            route -> resync_subscribers(H);
-            session -> ok
-        end
+        ok
     catch
         error:{badmatch, {error, Reason}} -> {error, Reason}
     end.

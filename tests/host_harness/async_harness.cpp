@@ -324,6 +324,67 @@ int health_main(unsigned seed, int threads, int handles, uint32_t window) {
   return 0;
 }
 
+// Handles mode: the handle registry over a real layer.  A number released
+// while a window submitted before the release is still in flight (the device hangs) is not handed
+// out again; once that window has been reported it is.  Prints "OK ..." like the main mode.
+int handles_main() {
+  emqxgm e;
+  emqxgm_t* hs[1] = {&e};
+  g_calls = new std::vector<CallState>(4);
+  std::vector<std::atomic<int64_t>> outstanding(1);
+  g_outstanding = outstanding.data();
+  emqxgm_async_cfg cfg{};
+  cfg.window_topics = 64;
+  cfg.window_us = 20;
+  emqxgm_async_t* a = nullptr;
+  CHECK(emqxgm_async_create(hs, 1, &cfg, on_window, nullptr, &a) == 0, "create");
+  emqxgm_handles_t* r = nullptr;
+  CHECK(emqxgm_handles_create(&a, 1, &r) == 0, "handles_create");
+  uint32_t h0, h1, h2, h3;
+  CHECK(emqxgm_handles_alloc(r, 2, &h0) == 0 && emqxgm_handles_alloc(r, 2, &h1) == 0, "alloc");
+  CHECK(h0 == 0 && h1 == 1, "fresh numbers %u %u", h0, h1);
+  g_hang.store(1);
+  (*g_calls)[0].topic = 0;
+  outstanding[0].fetch_add(1);
+  const std::string& t = g_topics[0];
+  CHECK(emqxgm_async_match(a, (const uint8_t*)t.data(), (uint32_t)t.size(), 0, 0) == 0, "match");
+  // wait until the window is submitted (its wait is blocked on the hang)
+  uint64_t st[8];
+  for (int i = 0; i < 2000; ++i) {
+    emqxgm_async_stats(a, st);
+    if (st[1] >= 1) break;
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  }
+  CHECK(st[1] >= 1, "the window was never submitted");
+  CHECK(emqxgm_handles_release(r, 2, h0) == 0, "release");
+  CHECK(emqxgm_handles_release(r, 2, h0) == -ENOENT, "double release");
+  CHECK(emqxgm_handles_alloc(r, 2, &h2) == 0 && h2 == 2, "a number released under a window in "
+        "flight was reused: %u", h2);
+  uint64_t hv[4];
+  emqxgm_handles_stats(r, 2, hv);
+  CHECK(hv[0] == 3 && hv[1] == 2 && hv[2] == 1 && hv[3] == 0, "stats %llu %llu %llu %llu",
+        (unsigned long long)hv[0], (unsigned long long)hv[1], (unsigned long long)hv[2],
+        (unsigned long long)hv[3]);
+  g_hang.store(0);
+  while ((*g_calls)[0].reported.load() == 0) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  // reported: released before the report's release of its slot?  wait for the slot to free
+  for (int i = 0; i < 2000; ++i) {
+    emqxgm_async_stats(a, st);
+    if (st[7] == 0) break;
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  }
+  CHECK(emqxgm_handles_alloc(r, 2, &h3) == 0 && h3 == h0, "the quiesced number %u was not reused "
+        "(got %u)", h0, h3);
+  CHECK(emqxgm_handles_reset(r) == 0, "reset");
+  emqxgm_handles_stats(r, 2, hv);
+  CHECK(hv[1] == 0 && hv[0] == 3, "after reset %llu live", (unsigned long long)hv[1]);
+  emqxgm_handles_destroy(r);
+  emqxgm_async_destroy(a);
+  delete g_calls;
+  printf("OK 1 1 0 0 0\n");
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const unsigned seed = argc > 1 ? atoi(argv[1]) : 1;
   const int threads = argc > 2 ? atoi(argv[2]) : 16;
@@ -371,6 +432,11 @@ int main(int argc, char** argv) {
       g_want.push_back(v);
     }
     ref_free(ids);
+  }
+  if (argc > 7 && strcmp(argv[7], "handles") == 0) {
+    const int rc = handles_main();
+    ref_destroy(g_ref);
+    return rc;
   }
   if (health) {
     const int rc = health_main(seed, threads, handles, window);

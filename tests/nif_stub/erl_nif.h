@@ -15,7 +15,7 @@ typedef enum { ERL_NIF_RT_CREATE = 1 } ErlNifResourceFlags;
 #define ERL_NIF_DIRTY_JOB_IO_BOUND 2
 typedef struct { const char* name; unsigned arity; ERL_NIF_TERM (*fptr)(ErlNifEnv*, int, const ERL_NIF_TERM[]); unsigned flags; } ErlNifFunc;
 typedef void ErlNifResourceDtor(ErlNifEnv*, void*);
-ErlNifEnv* enif_alloc_env(void); void enif_free_env(ErlNifEnv*);
+ErlNifEnv* enif_alloc_env(void); void enif_free_env(ErlNifEnv*); void enif_clear_env(ErlNifEnv*);
 void* enif_alloc_resource(ErlNifResourceType*, size_t); void enif_release_resource(void*);
 int enif_get_atom(ErlNifEnv*, ERL_NIF_TERM, char*, unsigned, ErlNifCharEncoding);
 int enif_get_int(ErlNifEnv*, ERL_NIF_TERM, int*); int enif_get_uint(ErlNifEnv*, ERL_NIF_TERM, unsigned*);

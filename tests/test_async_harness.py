@@ -72,3 +72,11 @@ def test_hung_device_costs_one_timeout_then_refuses(seed, threads, handles, wind
     after the repair calls are answered correctly again."""
     exe = _build("async_tsan", CLANG, ["-fsanitize=thread"])
     _run(exe, [seed, threads, handles, window, 0, 0, "health"], {"TSAN_OPTIONS": "halt_on_error=1"})
+
+
+@pytest.mark.skipif(not os.path.exists(CLANG), reason="clang++ (ThreadSanitizer runtime) absent")
+def test_handle_registry_waits_for_windows_in_flight():
+    """emqxgm_handles_* over a real layer: a number released while a window
+    submitted before the release is in flight is not reused until that window was reported."""
+    exe = _build("async_tsan", CLANG, ["-fsanitize=thread"])
+    _run(exe, [9, 1, 1, 64, 0, 0, "handles"], {"TSAN_OPTIONS": "halt_on_error=1"})
