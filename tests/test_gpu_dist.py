@@ -252,4 +252,4 @@ def test_sharded_matcher_cfg3_slice_every_gpu(emqx, backend):
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     status, pairs, on_rank0 = q.get(timeout=5)
     assert status == "ok", status
-    assert pairs > 1_000_000 and on_rank0 > 0
+    assert pairs > 50_000 and on_rank0 > 0
