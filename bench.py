@@ -544,6 +544,10 @@ def _window_sweep(Batcher, eng, w, sizes):
     return out
 
 
+POINT_S = 1.0              # a load point's measured duration at least
+NIF_MAX_CALLS = 160_000_000  # (4 B of latency per call kept for the percentiles)
+
+
 def _nif_concurrent(eng, w, spec):
     """The NIF's concurrent entry under load: T publisher threads (BEAM
     schedulers) each run P publisher processes calling emqxgm_async_match one topic at a time --
@@ -571,6 +575,11 @@ def _nif_concurrent(eng, w, spec):
         calls = max(2 * procs, min(8_000_000, 100 * W) // T)
         publishers.run([eng], tb, to, T, procs, min(calls, 4 * procs), W, deliver_threads=dth,
                        report_ns=rns)  # warm-up
+        # the measured point lasts at least POINT_S (its p99.9 and max are then
+        # a steady-state tail, not ~100 windows'): calls sized from a pilot run's rate
+        pilot = publishers.run([eng], tb, to, T, procs, calls, W, deliver_threads=dth, report_ns=rns)
+        rate = pilot["calls"] / max(pilot["seconds"], 1e-6)
+        calls = max(calls, min(int(rate * POINT_S * 1.1) // T + 1, NIF_MAX_CALLS // T))
         th0, s0 = _cgroup_throttled(), eng.stats()
         r = publishers.run([eng], tb, to, T, procs, calls, W, deliver_threads=dth, report_ns=rns)
         th1, s1 = _cgroup_throttled(), eng.stats()
@@ -582,7 +591,8 @@ def _nif_concurrent(eng, w, spec):
         if th0 and th1:  # the job's CPU quota stopping every thread (publishers + the layer's)
             out[key]["cgroup_throttled"] = {"periods": th1[0] - th0[0], "us": th1[1] - th0[1]}
     if runs:
-        r = publishers.run([eng], tb, to, 16, 1, 2000, 65536)
+        # the idle point: one call in flight per thread, so ~1 / latency calls per second each
+        r = publishers.run([eng], tb, to, 16, 1, 20000, 65536)
         out["idle_T16_P1"] = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}
     out["includes"] = ("T threads x P processes, one emqxgm_async_match call per topic (the NIF's "
                        "match_async/3), windows filled lock-free and flushed when full or "
@@ -605,7 +615,7 @@ def _subscribe_latency(eng, w, n_idle=400, max_build_s=30.0):
         v = np.asarray(v) * 1e6
         return {"n": int(v.size), "p50_us": round(float(np.percentile(v, 50)), 1),
                 "p99_us": round(float(np.percentile(v, 99)), 1),
-                "max_us": round(float(v.max()), 1)} if v.size else {"n": 0}
+                "max_us": round(float(v.max()), 1), "max_at": int(v.argmax())} if v.size else {"n": 0}
 
     base = w.topic(0).split(b"/")
 

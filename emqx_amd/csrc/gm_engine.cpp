@@ -2966,6 +2966,24 @@ int emqxgm_create(const emqxgm_cfg* cfg, emqxgm_t** out) {
     emqxgm_destroy(h);
     return -EIO;
   }
+  {
+    // a kernel's first launch in the process loads its code object (r05's first subscribe paid
+    // 5-8 ms for it): k_patch runs once now -- one entry copying a staging word onto another --
+    // so the first subscribe's delta commit does not
+    PatchEnt pe{};
+    pe.dst = (uint64_t)(uintptr_t)((uint8_t*)h->d_patch.p + 64);
+    pe.s = 0;
+    pe.w = 1;
+    memcpy(h->h_stage, &pe, sizeof pe);
+    memset(h->h_stage + sizeof pe, 0, 16);
+    const uint32_t* src = (const uint32_t*)((uint8_t*)h->d_patch.p + sizeof pe);
+    if (hipMemcpyAsync(h->d_patch.p, h->h_stage, sizeof pe + 16, hipMemcpyHostToDevice, h->wstream) != hipSuccess ||
+        launch_patch((const PatchEnt*)h->d_patch.p, 1, src, h->wstream) != hipSuccess ||
+        hipStreamSynchronize(h->wstream) != hipSuccess) {
+      emqxgm_destroy(h);
+      return -EIO;
+    }
+  }
   h->geom = walk_geometry(h->cfg.device, h->cfg.walk_wg_per_cu);
   h->geom.xrange_bytes = h->xrange_bytes;
   h->geom.pair = h->walk_pair_on;
@@ -3998,6 +4016,36 @@ int emqxgm_match_device(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_o
   out->filter_id = h->sync.sc.out;
   out->exact_id = h->sync.sc.exact_id;
   out->n_words = h->sync.sc.nw;
+  return 0;
+}
+
+int emqxgm_key_owners(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                      uint32_t parts, uint32_t* owner) {
+  if (!h || !offsets || !owner || parts == 0 || (!bytes && n && offsets[n])) return -EINVAL;
+  const uint64_t fmask = h->cfg.full_hash_bits >= 64 ? ~0ull : ((1ull << h->cfg.full_hash_bits) - 1ull);
+  for (uint64_t i = 0; i < n; ++i) {
+    if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > 65535) return -EINVAL;
+    const uint64_t fh = key_hash(bytes + offsets[i], (uint32_t)(offsets[i + 1] - offsets[i]), fmask);
+    owner[i] = (uint32_t)(fh >> 32) % parts;
+  }
+  return 0;
+}
+
+int emqxgm_exact_owned_device(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_offsets,
+                              uint32_t n, uint32_t parts, uint32_t part, uint32_t* d_out) {
+  if (!h || (!d_offsets && n) || (!d_out && n) || parts == 0 || part >= parts) return -EINVAL;
+  if (int rc = refuse_stale(h)) return rc;
+  std::lock_guard<std::mutex> g(h->mmu);
+  if (hipSetDevice(h->cfg.device) != hipSuccess) return -EIO;
+  EpochP E;
+  {
+    std::lock_guard<std::mutex> ge(h->emu);
+    E = h->cur;
+  }
+  hipStream_t st = h->sync.stream;
+  if (!E->ready_seen.load(std::memory_order_relaxed)) HIPCHK(h, hipStreamWaitEvent(st, E->ready, 0));
+  HIPCHK(h, launch_exact_owned(d_bytes, d_offsets, n, E->ix, parts, part, d_out, st));
+  HIPCHK(h, hipStreamSynchronize(st));  // (the epoch is held until its tables were read)
   return 0;
 }
 

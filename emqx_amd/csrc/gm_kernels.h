@@ -161,6 +161,10 @@ hipError_t launch_tok(const uint8_t* bytes, const uint32_t* off, uint32_t n, con
                       const uint32_t* claim0 = nullptr, const uint8_t* src_bytes = nullptr,
                       const uint32_t* src_off = nullptr);
 // exact route-key ids of every name (after launch_tok; a no-op when there are no plain keys)
+// the route-key probe of the names key shard `part` of `parts` owns (others: NONE) into out
+hipError_t launch_exact_owned(const uint8_t* bytes, const uint32_t* off, uint32_t n,
+                              const DevIndex& ix, uint32_t parts, uint32_t part, uint32_t* out,
+                              hipStream_t s);
 hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, const DevIndex& ix,
                         Scratch& sc, const WalkGeom& g, hipStream_t s);
 

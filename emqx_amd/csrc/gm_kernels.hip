@@ -646,6 +646,16 @@ hipError_t launch_exact(const uint8_t* bytes, const uint32_t* off, uint32_t n, c
   return hipGetLastError();
 }
 
+hipError_t launch_exact_owned(const uint8_t* bytes, const uint32_t* off, uint32_t n,
+                              const DevIndex& ix, uint32_t parts, uint32_t part, uint32_t* out,
+                              hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (ix.plain_empty) return hipMemsetAsync(out, 0xFF, (size_t)n * 4, s);
+  hipLaunchKernelGGL(k_exact_owned, dim3(grid_for(n, 1u << 20)), dim3(WG), 0, s, bytes, off, n,
+                     out, exact_args(ix, 0), parts, part);
+  return hipGetLastError();
+}
+
 // Workgroups of one walk launch.  The deep-stack variants fit fewer blocks per CU (LDS): only
 // as many are launched as are resident at once, so that no block of the persistent grid starts
 // after the others have drained.  A batch that gives the grid less than one topic per lane

@@ -19,6 +19,15 @@ export's entry counts, and the lengths on rank 0; the batch shape is known to ev
 ``shard="topics"`` (replicas): every rank holds the whole index (it fits: SURVEY 8e capacity
 note) and matches its own batch; no collective is on the data path.
 
+``shard="keys"`` (r06, SURVEY 8e's alternative for a route-key-heavy index, cfg4): the plain route
+keys are partitioned by key hash (``emqxgm_key_owners``), every rank also holds every wildcard
+filter.  Per batch, broadcast to every rank: rank r matches its block of topics [r n / G,
+(r + 1) n / G) (tokenizer, trie walk, wildcard-key probe, and the plain keys it owns) and probes
+the route key of every name it owns (``emqxgm_exact_owned_device``: a hash per name, one probe per
+owned name on a table of 1/G of the keys -- below the TLB's reach at cfg4); the dense per-rank
+parts go to rank 0 and are merged by ``emqxgm_merge`` (a topic's trie row comes from its block's
+rank, its exact id from its key's owner).  ``KeyShardedMatcher``; DESIGN.md 5 models when it pays.
+
 The collective code (broadcast_batch, gather_wire_to_root) is device-agnostic: with the gloo
 backend it runs on CPU tensors, which is how tests/test_dist.py covers world_size 2 without a GPU
 (the per-rank matcher, the wire export and the merge there are the test's torch restatements).
@@ -298,3 +307,115 @@ class ShardedMatcher:
     def step(self, tbytes: Optional[torch.Tensor], toff: Optional[torch.Tensor], shape) -> Optional[Merged]:
         """One batch: broadcast, match this shard, wire to root, merge there."""
         return next(self.run([(tbytes, toff)], [shape]))
+
+
+# ---- shard="keys": plain route keys partitioned by key hash, wildcard filters on every rank ----
+
+def key_shard_filters(eng, fbytes: np.ndarray, foff: np.ndarray, fwild: np.ndarray,
+                      world: int, rank: int) -> np.ndarray:
+    """Global indices of the filters rank `rank` holds in the key-partitioned layout: every
+    wildcard filter, and the plain route keys whose owner (emqxgm_key_owners, over the packed
+    filters as they are) is `rank`."""
+    wild = np.asarray(fwild).astype(bool)
+    if world == 1:
+        return np.arange(len(wild))
+    own = eng.key_owners(fbytes, np.asarray(foff, np.uint64), world)
+    return np.nonzero(wild | (own == rank))[0]
+
+
+def gather_dense_to_root(part: Part, root: int = 0, group=None) -> Optional[List[Part]]:
+    """Each rank's dense part (row [n+1], fid [pairs], exact [n]; int32 device tensors) to
+    `root`: the pair counts by one all_gather, then sized point-to-point receives."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    row, fid, ex = part
+    dev = row.device
+    cdev = "cpu" if _comm_on_cpu(group) else dev
+    mine = torch.tensor([fid.numel()], dtype=torch.int64, device=cdev)
+    allp = [torch.zeros(1, dtype=torch.int64, device=cdev) for _ in range(world)]
+    dist.all_gather(allp, mine, group=group)
+    if rank != root:
+        ops = [dist.P2POp(dist.isend, t.to(cdev), root, group) for t in (row, fid, ex) if t.numel()]
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+        return None
+    out, ops = [], []
+    for r in range(world):
+        if r == root:
+            out.append(part)
+            continue
+        q = (torch.empty_like(row, device=cdev), torch.empty(int(allp[r]), dtype=torch.int32, device=cdev),
+             torch.empty_like(ex, device=cdev))
+        ops += [dist.P2POp(dist.irecv, t, r, group) for t in q if t.numel()]
+        out.append(q)
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    return [tuple(t.to(dev) for t in q) for q in out]
+
+
+class KeyShardedMatcher:
+    """One rank of the key-partitioned layout (shard="keys"): `eng` holds every wildcard filter
+    and this rank's plain route keys (``key_shard_filters``), `gid_map` (int32 device tensor)
+    maps its local ids to global ones.  ``step`` broadcasts a batch from the root, matches this
+    rank's topic block and probes the names it owns, and merges every rank's part on the root."""
+
+    def __init__(self, eng, gid_map: torch.Tensor, device, group=None, root: int = 0):
+        self.eng = eng
+        self.gid_map = gid_map.to(torch.int64)
+        self.device = device
+        self.group = group
+        self.root = root
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+
+    def _global(self, ids: torch.Tensor) -> torch.Tensor:
+        """local ids (int32, NONE = -1) -> global ids (int32 bits)"""
+        hit = ids != -1
+        g = torch.full_like(ids, -1)
+        g[hit] = self.gid_map[ids[hit].to(torch.int64)].to(torch.int32)
+        return g
+
+    def part(self, b: torch.Tensor, o: torch.Tensor, n: int) -> Part:
+        """This rank's dense part of a batch already in HBM (bytes u8, offsets i32 [n+1])."""
+        G, r = self.world, self.rank
+        b0, b1 = n * r // G, n * (r + 1) // G
+        lo, hi = (int(x) for x in o[[b0, b1]].tolist())
+        bo = (o[b0:b1 + 1] - lo).contiguous()
+        bb = b[lo:hi].contiguous() if hi > lo else torch.zeros(1, dtype=torch.uint8, device=self.device)
+        own = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
+        torch.cuda.current_stream(self.device).synchronize()
+        self.eng.exact_owned_device(b.data_ptr(), o.data_ptr(), n, G, r, own.data_ptr())
+        res = self.eng.match_device(bb.data_ptr(), bo.data_ptr(), b1 - b0, hi - lo)
+        m = b1 - b0
+        brow = torch.empty(m + 1, dtype=torch.int32, device=self.device)
+        bfid = torch.empty(max(res.n_pairs, 1), dtype=torch.int32, device=self.device)
+        bex = torch.empty(max(m, 1), dtype=torch.int32, device=self.device)
+        self.eng.export(res, 0, brow.data_ptr(), bfid.data_ptr(), bex.data_ptr())
+        row = torch.empty(n + 1, dtype=torch.int32, device=self.device)
+        row[:b0 + 1] = 0
+        row[b0:b1 + 1] = brow
+        row[b1 + 1:] = brow[m]
+        fid = self._global(bfid[:res.n_pairs])
+        ex = self._global(own[:n])
+        if m:
+            blk = self._global(bex[:m])
+            ex[b0:b1] = torch.where(ex[b0:b1] != -1, ex[b0:b1], blk)
+        return row, fid, ex
+
+    def step(self, tbytes: Optional[torch.Tensor], toff: Optional[torch.Tensor], shape) -> Optional[Merged]:
+        nb, nt = shape
+        cdev = "cpu" if _comm_on_cpu(self.group) else self.device
+        if self.rank == self.root:
+            b, o = tbytes.to(cdev), toff.to(cdev)
+        else:
+            b = torch.empty(nb, dtype=torch.uint8, device=cdev)
+            o = torch.empty(nt + 1, dtype=torch.int32, device=cdev)
+        if nb:
+            dist.broadcast(b, self.root, group=self.group)
+        dist.broadcast(o, self.root, group=self.group)
+        p = self.part(b.to(self.device), o.to(self.device), nt)
+        parts = gather_dense_to_root(p, self.root, self.group)
+        if parts is None:
+            return None
+        return merge_parts(self.eng, parts, nt)

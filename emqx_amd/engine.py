@@ -176,6 +176,8 @@ SYMBOLS = {
                                                   C.POINTER(_U32P), C.POINTER(_U8P)]),
     "emqxgm_walk_census": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint64, _U64P]),
     "emqxgm_walk_census_levels": (C.c_int, [_P, _U64P, C.c_uint32]),
+    "emqxgm_key_owners": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P]),
+    "emqxgm_exact_owned_device": (C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint32, C.c_uint32, _P]),
     "emqxgm_export": (C.c_int, [_P, C.POINTER(_DevOut), _P, _P, _P, _P]),
     "emqxgm_merge": (C.c_int, [_P, C.c_uint32, _P, _P, _P, C.c_uint32, _P, _P, _P, _U32P]),
     "emqxgm_export_wire": (C.c_int, [_P, C.POINTER(_DevOut), _P, C.c_uint32, _P, _P, _P, _P,
@@ -648,6 +650,21 @@ class Engine:
         if copy:
             return MatchResult(row.astype(np.uint64), fid.copy(), ex.copy())
         return MatchResult(row, fid, ex)
+
+    def key_owners(self, buf: np.ndarray, off: np.ndarray, parts: int) -> np.ndarray:
+        """emqxgm_key_owners: the key shard of each packed key (u8 bytes, u64 offsets[n+1])."""
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        out = np.empty(len(off) - 1, np.uint32)
+        self._check(self._lib.emqxgm_key_owners(self._h, _ptr(np.ascontiguousarray(buf, np.uint8)),
+                                                _ptr(off), len(off) - 1, parts, _ptr(out)),
+                    "key_owners")
+        return out
+
+    def exact_owned_device(self, d_bytes: int, d_off: int, n: int, parts: int, part: int,
+                           d_out: int) -> None:
+        """emqxgm_exact_owned_device: route-key ids of the names key shard `part` owns."""
+        self._check(self._lib.emqxgm_exact_owned_device(self._h, d_bytes, d_off, n, parts, part,
+                                                        d_out), "exact_owned_device")
 
     def export(self, r: "DeviceResult", id_map: int, row: int, fid: int, exact: int) -> None:
         """emqxgm_export: copy a device-resident result into device buffers (pointers), ids

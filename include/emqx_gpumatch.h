@@ -618,6 +618,18 @@ int emqxgm_merge(emqxgm_t* h, uint32_t parts, const uint32_t* const* rows,
                  const uint32_t* const* fids, const uint32_t* const* exacts, uint32_t n,
                  uint32_t* out_row, uint32_t* out_fid, uint32_t* out_exact, uint32_t* n_pairs);
 
+/* The key-partitioned layout of a route-key-heavy index (cfg4: 100M exact keys, DESIGN.md 5,
+ * SURVEY 8e's alternative): the plain route keys are split over `parts` engines by key hash
+ * (emqxgm_key_owners: owner[i] of packed key i, a function of its bytes and the engine's
+ * full_hash_bits only), each engine also holding every wildcard filter.  A batch's names are
+ * probed each by its owner only: emqxgm_exact_owned_device writes to d_out (device, n u32) the
+ * owned names' route-key ids and EMQXGM_NONE for the others, without a probe (the trie walk of a
+ * topic and its wildcard-key probe are its topic block's, emqxgm_match_device on that block). */
+int emqxgm_key_owners(emqxgm_t* h, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                      uint32_t parts, uint32_t* owner);
+int emqxgm_exact_owned_device(emqxgm_t* h, const uint8_t* d_bytes, const uint32_t* d_offsets,
+                              uint32_t n, uint32_t parts, uint32_t part, uint32_t* d_out);
+
 /* The compact wire form of a shard's result for the exchange to the root:
  *   cnt  per-topic pair counts: n u8 (255 = in ovf), or with EMQXGM_WIRE_CNT2 two bit planes per
  *        64 topics (16 B per 64 topics, 2 bits a topic; 3 = in ovf) -- for sparse results;

@@ -112,6 +112,7 @@ hipError_t launch_scan(const uint32_t*, uint32_t*, uint32_t, uint32_t*, uint32_t
 hipError_t launch_tok(const uint8_t*, const uint32_t*, uint32_t, const DevIndex&, Scratch&, hipStream_t, uint32_t, bool, const uint32_t*, const uint8_t*, const uint32_t*) { NOT_HERE; }
 void walk_claim_init(const WalkGeom&, uint32_t, uint32_t, uint32_t*) {}
 hipError_t launch_exact(const uint8_t*, const uint32_t*, uint32_t, const DevIndex&, Scratch&, const WalkGeom&, hipStream_t) { NOT_HERE; }
+hipError_t launch_exact_owned(const uint8_t*, const uint32_t*, uint32_t, const DevIndex&, uint32_t, uint32_t, uint32_t*, hipStream_t) { NOT_HERE; }
 hipError_t launch_walk(const DevIndex&, Scratch&, uint32_t, const WalkGeom&, hipStream_t, unsigned long long*, uint32_t, uint32_t) { NOT_HERE; }
 uint32_t walk_blocks(const WalkGeom&, uint32_t, uint32_t) { return 0; }
 uint32_t walk_static_chunks(const WalkGeom&, uint32_t, uint32_t, uint32_t) { return 0; }

@@ -218,3 +218,87 @@ def test_filter_shards_stable_and_balanced():
         counts = np.bincount(s, minlength=world)
         assert counts.min() > 0.8 * len(fs) / world
         assert np.array_equal(s, D.filter_shards(fb, fo, world))
+
+
+def _worker_keys(rank, world, port, q, libpath):
+    """The key-partitioned layout (dist.KeyShardedMatcher, shard="keys") with the oracle as each
+    rank's matcher: rank r holds every wildcard filter and the plain keys emqxgm_key_owners gives
+    it (the engine's host code, on the fake HIP runtime); its part is its topic block's rows and
+    the exact ids of the names it owns; gather_dense_to_root brings the parts to rank 0, whose
+    merge (the restatement of emqxgm_merge) must equal the unsharded answer."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import workloads
+        from emqx_amd import dist as D
+        from emqx_amd.engine import Engine, load_library
+        from oracle.cref import RefIndex
+        eng = Engine(library=load_library(libpath, allow_missing=True))
+        w = workloads.generate(4, 40_400, 6000)
+        mine = D.key_shard_filters(eng, w.fbytes, w.foff, w.fwild, world, rank)
+        assert w.fwild[mine].sum() == w.fwild.sum()  # every wildcard filter on every rank
+        fb, fo = _subset(w, mine)
+        ref = RefIndex(True)
+        ref.add_many(fb, fo, 2 + w.fwild[mine])
+        tb = torch.from_numpy(w.tbytes) if rank == 0 else None
+        to = torch.from_numpy(w.toff.view(np.int32)) if rank == 0 else None
+        tb, to = D.broadcast_batch(tb, to, "cpu")
+        tbn, ton = tb.numpy(), to.numpy().view(np.uint32)
+        n = len(ton) - 1
+        b0, b1 = n * rank // world, n * (rank + 1) // world
+        # the block's rows (local ids -> global)
+        bo = (ton[b0:b1 + 1] - ton[b0]).astype(np.uint32)
+        brow, bids, bex = ref.match(tbn[ton[b0]:ton[b1]], bo)
+        # the owned names' exact ids: every name's, kept where this rank owns the name
+        _, _, ex_all = ref.match(tbn, ton)
+        names = [tbn[ton[t]:ton[t + 1]].tobytes() for t in range(n)]
+        from emqx_amd.engine import pack
+        nb, no = pack(names)
+        own = eng.key_owners(nb, no, world)
+        g = lambda a: np.where(a == D.NONE, D.NONE, mine[np.minimum(a, len(mine) - 1).astype(np.int64)]).astype(np.uint32)  # noqa: E731
+        ex = np.where(own == rank, g(ex_all), D.NONE).astype(np.uint32)
+        blk = g(bex)
+        ex[b0:b1] = np.where(ex[b0:b1] != D.NONE, ex[b0:b1], blk)
+        row = np.zeros(n + 1, np.uint32)
+        row[b0:b1 + 1] = brow
+        row[b1 + 1:] = brow[-1]
+        i32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.uint32).view(np.int32))  # noqa: E731
+        parts = D.gather_dense_to_root((i32(row), i32(g(bids)), i32(ex)))
+        if rank != 0:
+            assert parts is None
+        else:
+            merged = _ref_merge(parts, n)
+            full = RefIndex(True)
+            full.add_many(w.fbytes, w.foff, 2 + w.fwild)
+            frow, fids, fex = full.match(w.tbytes, w.toff)
+            ok = np.array_equal(merged[0], frow.astype(np.int64))
+            for t in range(n):
+                a, b = int(frow[t]), int(frow[t + 1])
+                ok = ok and np.array_equal(np.sort(merged[1][a:b]), fids[a:b].astype(np.int64))
+            ok = ok and np.array_equal(merged[2], fex.astype(np.int64))
+            assert (fex != D.NONE).sum() > 4000 and int(frow[-1]) > 0
+            q.put(("ok" if ok else "mismatch", len(mine), w.nf))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put(("error", repr(e), 0))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_key_sharded_world2_gloo():
+    """the routing and the merge of the key-partitioned cfg4 layout."""
+    from tests.test_route_mirror import build_fake_lib
+    lib = build_fake_lib()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_keys, args=(r, 2, port, q, lib)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    status, on_rank0, total = q.get(timeout=5)
+    assert status == "ok", status
+    assert 0 < on_rank0 < total

@@ -253,3 +253,108 @@ def test_sharded_matcher_cfg3_slice_every_gpu(emqx, backend):
     status, pairs, on_rank0 = q.get(timeout=5)
     assert status == "ok", status
     assert pairs > 50_000 and on_rank0 > 0
+
+
+def _rank_keys(rank, world, port, q, backend="gloo", shape=(4, 404_000, 50_000)):
+    """One rank of the key-partitioned layout (dist.KeyShardedMatcher): every wildcard filter and
+    this rank's plain route keys; the merged result on rank 0 against the unsharded oracle."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    gpu = rank if backend == "nccl" else 0
+    torch.cuda.set_device(gpu)
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    try:
+        import workloads
+        from emqx_amd import Engine
+        from emqx_amd import dist as D
+        from oracle.cref import RefIndex
+        dev = torch.device("cuda", gpu)
+        w = workloads.generate(*shape)
+        eng = Engine(device=gpu)
+        mine = D.key_shard_filters(eng, w.fbytes, w.foff, w.fwild, world, rank)
+        fb, fo = _subset(w, mine)
+        rid = eng.route_ref_many(fb, fo)
+        wsel = np.nonzero(w.fwild[mine])[0]
+        wb, wo = _subset(type("W", (), {"fbytes": fb, "foff": fo})(), wsel)
+        tid = eng.trie_insert_many(wb, wo)
+        eng.commit()
+        gid = np.full(int(max(rid.max(), tid.max(initial=0))) + 1, 0xFFFFFFFF, np.uint32)
+        gid[rid] = mine
+        gid[tid] = mine[wsel]
+        km = D.KeyShardedMatcher(eng, torch.from_numpy(gid.view(np.int32)).to(dev), dev)
+        tb = torch.from_numpy(w.tbytes).to(dev) if rank == 0 else None
+        to = torch.from_numpy(w.toff.view(np.int32)).to(dev) if rank == 0 else None
+        m = km.step(tb, to, (int(w.toff[-1]), w.nt))
+        if rank == 0:
+            full = RefIndex(True)
+            full.add_many(w.fbytes, w.foff, 2 + w.fwild)
+            frow, fids, fex = full.match(w.tbytes, w.toff)
+            row = m.row_ptr.cpu().numpy().astype(np.int64)
+            got = m.filter_id.cpu().numpy().view(np.uint32)
+            ok = np.array_equal(row, frow.astype(np.int64))
+            for t in range(w.nt):
+                a, b = int(frow[t]), int(frow[t + 1])
+                ok = ok and np.array_equal(np.sort(got[a:b]), fids[a:b])
+            gx = m.exact_id.cpu().numpy().view(np.uint32)
+            ok = ok and np.array_equal(gx, fex)
+            q.put(("ok" if ok else "mismatch", int((fex != 0xFFFFFFFF).sum()), len(mine)))
+        else:
+            assert m is None
+        eng.close()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put(("error", repr(e), 0))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("backend", ["gloo", "nccl"])
+def test_key_sharded_matcher_cfg4_shape(emqx, backend):
+    """SURVEY 8e's alternative for cfg4: plain route keys partitioned by key
+    hash, wildcard filters on every rank; each name's route key probed by its owner only, each
+    topic's trie walk by its block's rank; the merged rows and exact ids equal the unsharded
+    oracle's (cfg4 shape: 400k exact keys + 4k wildcards, 50k topics, 90% exact hits).  gloo:
+    two ranks sharing this box's GPU; nccl: every GPU of the node (skipped on one)."""
+    world = 2 if backend == "gloo" else min(torch.cuda.device_count(), 8)
+    if world < 2:
+        pytest.skip("the RCCL branch needs two or more GPUs (this box has one)")
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_keys, args=(r, world, port, q, backend)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(560)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    status, hits, on_rank0 = q.get(timeout=5)
+    assert status == "ok", status
+    assert hits > 40_000 and 0 < on_rank0 < 404_000
+
+
+def test_key_owners_partition(emqx):
+    """emqxgm_key_owners splits keys evenly and every key has one owner; the owned-name probe
+    finds exactly the owned keys' ids."""
+    eng = emqx.Engine()
+    keys = [b"dev/%09d/state" % i for i in range(20000)]
+    buf, off = emqx.engine.pack(keys)
+    own = eng.key_owners(buf, off, 4)
+    assert set(own.tolist()) == {0, 1, 2, 3} and np.bincount(own).min() > 4500
+    assert (eng.key_owners(buf, off, 1) == 0).all()
+    mine = [k for k, o in zip(keys, own) if o == 1]
+    ids = {eng.route_ref(k): k for k in mine}
+    eng.commit()
+    names = keys[:3000] + [b"x/y", b""]
+    nb, no = emqx.engine.pack(names, np.uint32)
+    db = torch.from_numpy(nb).cuda()
+    do = torch.from_numpy(no.view(np.int32)).cuda()
+    out = torch.empty(len(names), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    eng.exact_owned_device(db.data_ptr(), do.data_ptr(), len(names), 4, 1, out.data_ptr())
+    got = out.cpu().numpy().view(np.uint32)
+    want = [next((i for i, k in ids.items() if k == nm), 0xFFFFFFFF) for nm in names]
+    assert got.tolist() == want
+    eng.close()
