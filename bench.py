@@ -357,6 +357,24 @@ def main():
     if rank == 0 and world == 1 and not args.no_subscribe:
         subscribe = _subscribe_latency(eng, w)
 
+    # the low-load crossover: one publish answered by the device at idle (a
+    # window's timer and one pass) against the reference's walk on one core (emqx_trie_gpu's
+    # adaptive_below_rate chooses between them by the measured rate)
+    crossover = None
+    if cpu and nif and cpu.get("one_thread") and "idle_T16_P1" in nif:
+        one_us = cpu["one_thread"]["us_per_topic"]
+        idle = nif["idle_T16_P1"]
+        crossover = {
+            "device_idle_p50_us": idle["latency_us_p50"], "device_idle_p99_us": idle["latency_us_p99"],
+            "reference_us_per_topic_one_core": one_us,
+            "reference_capacity_topics_per_s": cpu["value"], "reference_cores": cpu["cores"],
+            "reference_faster_at_idle": one_us < idle["latency_us_p50"],
+            # the rate at which the reference path needs half of the cores the baseline used:
+            # below it, answering on the publishers' cores costs little and is faster at idle
+            "reference_half_cores_rate": round(0.5 * cpu["value"], 1),
+            "note": ("broker.perf.gpu_match.adaptive_below_rate: publishes/s under which "
+                     "emqx_trie_gpu answers on the publisher's core (0 = never)")}
+
     line = None
     if rank == 0:
         line = {
@@ -404,6 +422,7 @@ def main():
             },
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "crossover": crossover,
             "end_to_end": e2e,
             "nif_windows": windows,
             "nif_concurrent": nif,
@@ -1064,6 +1083,10 @@ def _cpu_baseline(w, args, job):
     rate, n, reps, dt = _cpu_leg(ref, w, threads, args.cpu_seconds)
     log(f"cpu baseline: index build {build_s:.1f}s, {n} topics in {dt:.2f}s on {threads} threads "
         f"(affinity {aff}, quota {quota})")
+    # one thread: the reference's per-topic latency on the publisher's own core (the crossover)
+    r1, n1, reps1, dt1 = _cpu_leg(ref, w, 1, args.cpu_seconds / 4)
+    one_thread = {"value": round(r1, 1), "us_per_topic": round(1e6 / max(r1, 1e-9), 2),
+                  "sample": f"first {n1} topics" + (f" (x{reps1}, mean)" if reps1 > 1 else "")}
     share_leg = None
     if aff > threads:
         r2, n2, reps2, dt2 = _cpu_leg(ref, w, aff, args.cpu_seconds / 2)
@@ -1079,6 +1102,7 @@ def _cpu_baseline(w, args, job):
             "cpu_model": model, "host_cpus": os.cpu_count(), "affinity_cpus": aff,
             "cgroup_quota_cpus": quota, "effective_cpus": eff,
             "at_affinity_threads": share_leg,
+            "one_thread": one_thread,
             "index_build_s": round(build_s, 1),
             "sample": f"first {n} topics of batch 0" + (f" (x{reps}, mean)" if reps > 1 else "")
                   + f" against the same {w.nf} filters "

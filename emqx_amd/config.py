@@ -32,6 +32,9 @@ fail_threshold     3                  ``emqxgm_async_cfg.fail_threshold``: that 
                                       calls or failed windows in a row mark the engines stale
                                       (every later call refused at once until the mirror's
                                       repair; include/emqx_gpumatch.h "Health")
+adaptive_below_rate 0                 publishes/s under which the reference path answers (its
+                                      ~22 us on the publisher's core beats the device's window
+                                      at idle); 0 = always the device (``LoadAdaptive``)
 resync_interval_ms (role)             period of the mirror's full resync (``emqxgm_route_sync_begin``
                                       / ``_end``): none (0) on a core node, 30000 on a replicant
 ================== ================== ======================================================
@@ -59,6 +62,7 @@ class GpuMatchConfig:
     snapshot_dir: Optional[str] = None
     timeout_ms: int = 500
     fail_threshold: int = 3
+    adaptive_below_rate: int = 0
     resync_interval_ms: Optional[int] = None  # None: by the node's mria role
 
     @classmethod
@@ -88,6 +92,7 @@ class GpuMatchConfig:
         rng("max_levels", self.max_levels, 1, 65535)
         rng("timeout_ms", self.timeout_ms, 1, 600_000)
         rng("fail_threshold", self.fail_threshold, 0, 1_000_000)
+        rng("adaptive_below_rate", self.adaptive_below_rate, 0, 1 << 40)
         if self.resync_interval_ms is not None:
             rng("resync_interval_ms", self.resync_interval_ms, 0, 86_400_000)
         rng("bg_build", self.bg_build, 0, 1 << 62)

@@ -256,3 +256,32 @@ class RouteTableMirror:
     def save(self, snapshot: str) -> None:
         """terminate/2: the committed index to `snapshot` (engine 0: they all hold the same)."""
         self.engines[0].snapshot_save(snapshot)
+
+
+class LoadAdaptive:
+    """emqx_trie_gpu's load-adaptive choice (low_load/0, sample_load/2): every publish counts
+    itself; a sample every `sample_ms` sets whether the rate since the last sample is under
+    `below_rate` publishes/s -- then the reference path answers (at idle its walk on the
+    publisher's core is ~4x faster than a device window: bench.py's `crossover`).  0 = always the
+    device.  `clock` (ms) is injectable for tests."""
+
+    def __init__(self, below_rate: int = 0, sample_ms: int = 100, clock=None):
+        import time
+        self.below_rate = below_rate
+        self.sample_ms = sample_ms
+        self.clock = clock or (lambda: time.monotonic() * 1e3)
+        self.count = 0
+        self.low = False
+        self._last = (0, self.clock())
+
+    def note(self) -> bool:
+        """One publish: True when it takes the reference path."""
+        self.count += 1
+        return self.low
+
+    def sample(self) -> None:
+        c0, t0 = self._last
+        t1 = self.clock()
+        rate = (self.count - c0) * 1000 // max(1, int(t1 - t0))
+        self.low = self.below_rate > 0 and rate < self.below_rate
+        self._last = (self.count, t1)

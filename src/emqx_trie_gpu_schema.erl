@@ -29,6 +29,9 @@
 %%   fail_threshold      -> emqxgm_async_cfg.fail_threshold: that many timed-out calls or failed
 %%                          windows in a row mark the engines stale, so every later call is refused
 %%                          at once until the mirror's repair (include/emqx_gpumatch.h "Health")
+%%   adaptive_below_rate -> publishes per second under which the reference path answers (its
+%%                          ~22 us on the publisher's core beats the device's window at idle);
+%%                          0 = always the device (emqx_trie_gpu "Load-adaptive choice")
 %%   resync_interval_ms  -> period of emqx_trie_gpu_sync's full resync (emqxgm_route_sync_*);
 %%                          default 0 (none) on a core node, whose table events all arrive, and
 %%                          30000 on a replicant
@@ -57,5 +60,6 @@ fields("gpu_match") ->
         {"snapshot_dir", hoconsc:mk(string(), #{required => false})},
         {"timeout_ms", hoconsc:mk(range(1, 600000), #{default => 500})},
         {"fail_threshold", hoconsc:mk(range(0, 1000000), #{default => 3})},
+        {"adaptive_below_rate", hoconsc:mk(non_neg_integer(), #{default => 0})},
         {"resync_interval_ms", hoconsc:mk(range(0, 86400000), #{required => false})}
     ].

@@ -50,6 +50,7 @@
 -define(BATCH, 65536).       %% table events per device call
 -define(CONF(K, D), emqx_config:get([broker, perf, gpu_match, K], D)).
 -define(BACKOFF_MIN, 100).
+-define(SAMPLE_MS, 100).     %% the load-adaptive choice's rate sample (emqx_trie_gpu:sample_load/2)
 -define(BACKOFF_MAX, 30000).
 
 start_link(Index) ->
@@ -83,7 +84,8 @@ init(Index) ->
             tab => table(Index),
             published => false,
             backoff => 0,
-            retry => undefined
+            retry => undefined,
+            load => undefined
         },
         {continue, open}}.
 
@@ -99,6 +101,7 @@ handle_continue(open, S = #{index := Index, tab := Tab}) ->
             _ = (catch prepare(Index, H)),
             S2 = repair_now(S1),
             schedule_resync(),
+            _ = Index =:= route andalso erlang:send_after(?SAMPLE_MS, self(), sample_load),
             {noreply, S2};
         {error, Reason} ->
             {stop, {gpu_match_open, Reason}, S}
@@ -256,6 +259,10 @@ handle_info(resync, S) ->
     {noreply, S1};
 handle_info(repair, S) ->
     {noreply, repair_now(S#{retry := undefined})};
+handle_info(sample_load, S = #{load := L}) ->
+    L1 = emqx_trie_gpu:sample_load(L, ?CONF(adaptive_below_rate, 0)),
+    erlang:send_after(?SAMPLE_MS, self(), sample_load),
+    {noreply, S#{load := L1}};
 handle_info(_Info, S) ->
     {noreply, S}.
 

@@ -26,7 +26,7 @@ def test_values_and_ranges():
                 {"delta_commit": "sometimes"}, {"batch_size": 3}, {"batch_max": True},
                 {"timeout_ms": 0}, {"resync_interval_ms": -1}, {"spin_us": -1},
                 {"publish": 1}, {"bg_build": -5}, {"report_threads": 65},
-                {"fail_threshold": -1}):
+                {"fail_threshold": -1}, {"adaptive_below_rate": -1}):
         with pytest.raises(ValueError):
             GpuMatchConfig.from_map(bad)
 
@@ -38,3 +38,25 @@ def test_erlang_schema_lists_the_same_fields():
     src = open(os.path.join(root, "src", "emqx_trie_gpu_schema.erl")).read()
     fields = re.findall(r'\{"([a-z_]+)",', src.split("fields(\"gpu_match\") ->")[1])
     assert fields == list(GpuMatchConfig.__dataclass_fields__)
+
+
+def test_load_adaptive_choice():
+    """emqx_trie_gpu's low_load/0 + sample_load/2 (restated in emqx_amd.mirror.LoadAdaptive):
+    under the rate the reference path answers, over it the device; 0 = always the device."""
+    from emqx_amd.mirror import LoadAdaptive
+    now = [0.0]
+    la = LoadAdaptive(below_rate=20000, sample_ms=100, clock=lambda: now[0])
+    for _ in range(500):   # 500 publishes in 100 ms = 5k/s: under
+        la.note()
+    now[0] += 100
+    la.sample()
+    assert la.note() is True
+    for _ in range(10000):  # 10k in 100 ms = 100k/s: over
+        la.note()
+    now[0] += 100
+    la.sample()
+    assert la.note() is False
+    off = LoadAdaptive(below_rate=0, clock=lambda: now[0])
+    now[0] += 100
+    off.sample()
+    assert off.note() is False
