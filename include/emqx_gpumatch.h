@@ -235,7 +235,8 @@ int emqxgm_trie_member(emqxgm_t* h, const uint8_t* filter, uint32_t len);
 
 int emqxgm_lookup_id(emqxgm_t* h, const uint8_t* filter, uint32_t len, uint32_t* id);
 /* Pointer to filter id's bytes in the engine's registry: valid until the next call that adds a
- * filter string (insert / route / subscriber calls may grow the registry).  Prefer the copies. */
+ * filter string or commits (insert / route / subscriber calls may grow the registry, and a commit
+ * reserves room for the deltas ahead).  Prefer the copies. */
 int emqxgm_filter_bytes(emqxgm_t* h, uint32_t id, const uint8_t** p, uint32_t* len);
 /* Copy of filter id's bytes into buf (cap bytes): *len = its length; -ENOSPC if cap < *len. */
 int emqxgm_filter_copy(emqxgm_t* h, uint32_t id, uint8_t* buf, uint32_t cap, uint32_t* len);

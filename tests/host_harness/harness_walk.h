@@ -60,6 +60,9 @@ bool mqtt_match(const std::string& t, const std::string& f) {
 }
 
 std::string filter_str(emqxgm* h, uint32_t id) {
+  // the registry lock, as the engine's readers take it (a commit may move the arrays: r06
+  // reserves room for the deltas ahead)
+  std::shared_lock<std::shared_mutex> g(h->pmu);
   const Filter& f = h->filters[id];
   return std::string((const char*)h->pool.data() + f.off, f.len);
 }
