@@ -344,6 +344,18 @@ def main():
                                       "ms_per_batch": round(best * 1e3, 3),
                                       "api": "emqxgm_match_batch (u64 row pointers)"}}
 
+    # (before the load blocks: measured in the wake of their publisher and layer threads, which
+    # spend the job's CPU quota, the idle hook took p50 51 us / max 1.0 ms in r06, against p50
+    # 25 us / max 0.27 ms in tools/subscribe_probe.py's quiet process; the cgroup's throttling
+    # during the block is recorded beside it)
+    subscribe = None
+    if rank == 0 and world == 1 and not args.no_subscribe:
+        th0 = _cgroup_throttled()
+        subscribe = _subscribe_latency(eng, w)
+        th1 = _cgroup_throttled()
+        if th0 and th1:
+            subscribe["cgroup_throttled"] = {"periods": th1[0] - th0[0], "us": th1[1] - th0[1]}
+
     nif = None
     if rank == 0 and world == 1 and args.nif:
         nif = _nif_concurrent(eng, w, args.nif)
@@ -352,10 +364,6 @@ def main():
     if rank == 0 and world == 1 and not args.no_e2e and args.windows:
         from emqx_amd.engine import Batcher
         windows = _window_sweep(Batcher, eng, w, [int(x) for x in args.windows.split(",")])
-
-    subscribe = None
-    if rank == 0 and world == 1 and not args.no_subscribe:
-        subscribe = _subscribe_latency(eng, w)
 
     # the low-load crossover: one publish answered by the device at idle (a
     # window's timer and one pass) against the reference's walk on one core (emqx_trie_gpu's
@@ -871,11 +879,12 @@ def _roofline(nt, nbytes, census, pmc, tok_ms, exact_ms, walk_ms, pipe_ms, exact
                    "census edge-bucket loads (no PMC request count committed for this batch: "
                    "L1 hits included, an over-count)")
             # the bytes this design must move per launch: one 64-B bucket line per edge probe the
-            # production walk makes (census), the 64-B topic record and 4-B count per topic, a
-            # 12-B staged pair per match.  SURVEY 8d's model (3 x 16-B probes per matched trie
+            # production walk makes (census), the 64-B topic record and 4-B count per topic, an
+            # 8-B staged pair per match (packed staging, gm_kernels.h StgFmt: every bench config
+            # fits it; a pass redone wide shows in "reruns").  SURVEY 8d's model (3 x 16-B probes per matched trie
             # state, 16-B pairs) is kept beside it, labelled: it counts states the upper levels
             # serve from the L2 and the fat buckets never probe, so it can pass the HBM peak
-            alg = 64 * census["slot_loads"] + (64 + 4) * nt + 12 * census["pairs"]
+            alg = 64 * census["slot_loads"] + (64 + 4) * nt + 8 * census["pairs"]
             model = (64 + 4) * nt + 48 * census["states"] + 16 * census["pairs"]
             pruned = 48 * (census["states"] - census.get("states_visited", census["states"]))
         else:
@@ -912,7 +921,7 @@ def _roofline(nt, nbytes, census, pmc, tok_ms, exact_ms, walk_ms, pipe_ms, exact
                             "from it, weighted by this kernel's L2 miss share (PMC)"),
             "hbm_algorithmic": {"bytes_per_launch": int(alg),
                                 "counts": ("64-B line per edge probe (census) + 68 B per topic "
-                                           "(record, count) + 12 B per staged pair"
+                                           "(record, count) + 8 B per staged pair (packed)"
                                            if dom == "k_walk" else
                                            "topic bytes + offsets + one 64-B bucket line + 4-B "
                                            "exact id per name"),

@@ -190,6 +190,8 @@ struct Epoch {
   std::atomic<uint32_t> walk_level{WALK_SHALLOW};
   std::atomic<uint32_t> census_level{WALK_SHALLOW};  // the same for diagnostic census passes
                                                       // (their unpruned walks stack deeper)
+  // a topic outgrew the packed staging's rank field (StgFmt): this epoch's passes stage wide
+  std::atomic<bool> wide_stage{false};
   mutable std::atomic<bool> ready_seen{false};  // `ready` has completed (passes skip the query)
   // retired by a background build's install: the last epoch on the replaced tables frees
   // gigabytes (hipFree synchronises), so the builder thread frees it, not a subscribe's commit
@@ -213,6 +215,7 @@ struct PassCtx {
   bool own_stream = false;    // false: the stream is one of the handle's shared pipe streams
   uint32_t walk_level = 0;    // walk variant of that pass (WalkLevel)
   bool census = false;        // that pass was a census pass
+  bool packed = false;        // that pass staged its pairs packed (StgFmt)
   bool pipelined = false;     // a device / host pipe (walks with emqxgm::geom_pipe)
   // copy-through input of the next pass enqueued here (pinned host memory, k_tok's TokArgs);
   // cleared by the enqueue
@@ -622,6 +625,9 @@ struct emqxgm {
   std::atomic<int64_t> inject_commits{0};
   std::atomic<int32_t> inject_errno{EIO};
   std::atomic<uint32_t> hang_ms{0};
+  // packed staging's rank field capped at this many bits (tune "stage_rank_bits", tests of the
+  // wide redo; 0: as many as fit)
+  std::atomic<uint32_t> stage_rank_bits{0};
 };
 
 namespace {
@@ -1145,6 +1151,7 @@ int upload_tables(emqxgm* h, const BuildIn& in, TrieModel& m, DevIndex& nx, Owne
   nx.needs_verify = m.needs_verify;
   nx.full_mask = fmask;
   nx.max_depth = m.max_depth;
+  nx.fid_bound = (uint64_t)m.fv_cap * 32;
   nx.trie_empty = (m.n_trie == 0);
   nx.plain_empty = (m.n_route_p == 0);
   nx.wild_empty = (m.n_route_w == 0);
@@ -1800,6 +1807,7 @@ int commit_delta(emqxgm* h, const std::vector<uint8_t>* base = nullptr) {
   m.root_half(ix);
   ix.needs_verify = m.needs_verify;
   ix.max_depth = m.max_depth;
+  ix.fid_bound = (uint64_t)m.fv_cap * 32;
   ix.trie_empty = (m.n_trie == 0);
   ix.plain_empty = (m.n_route_p == 0);
   ix.wild_empty = (m.n_route_w == 0);
@@ -2373,6 +2381,30 @@ int pass_prepare(emqxgm* h, PassCtx& c, uint32_t n, uint64_t bytes_len) {
   return 0;
 }
 
+// The staging layout of a pass over n topics (StgFmt): packed when topic ids, filter ids below
+// fid_bound and a rank field of at least STG_MIN_RANK_BITS fit one 64-bit word with the reject
+// bit.  The legacy path (k_verify_scatter) and an epoch that saw a rank outgrow the field stage
+// wide.
+StgFmt stg_format(uint32_t n, uint64_t fid_bound, bool wide, uint32_t rank_bits_cap) {
+  StgFmt F;
+  auto bits = [](uint64_t v) {  // bits to hold every value below v
+    uint32_t b = 1;
+    while (b < 64 && (1ull << b) < v) ++b;
+    return b;
+  };
+  static const bool force_wide = getenv("EMQXGM_STAGE_WIDE") != nullptr;  // (A/B runs)
+  if (wide || fid_bound == 0 || force_wide) return F;
+  const uint32_t tb = bits(n), fb = bits(fid_bound);
+  if (tb + fb + 1 + std::min(STG_MIN_RANK_BITS, rank_bits_cap ? rank_bits_cap : 31u) > 64) return F;
+  const uint32_t rb = std::min<uint32_t>({64 - 1 - tb - fb, 31u, rank_bits_cap ? rank_bits_cap : 31u});
+  F.pk = 1;
+  F.fsh = 1 + rb;
+  F.tsh = 64 - tb;
+  F.fmask = (uint32_t)((1ull << fb) - 1);
+  F.rmask = (uint32_t)((1ull << rb) - 1);
+  return F;
+}
+
 // Every launch of one pass against epoch E on the context's stream (caller holds emu).
 int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
                  const uint32_t* d_off, uint32_t n, bool legacy, bool census) {
@@ -2398,6 +2430,9 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
                              st));
   c.census = census;
   c.walk_level = (census ? E.census_level : E.walk_level).load(std::memory_order_relaxed);
+  s.fmt = stg_format(n, ix.fid_bound, legacy || E.wide_stage.load(std::memory_order_relaxed),
+                     h->stage_rank_bits.load(std::memory_order_relaxed));
+  c.packed = s.fmt.pk != 0;
   // (census passes and the synchronous ones keep the full geometry)
   WalkGeom WG_ = (c.pipelined && !census) ? h->geom_pipe : h->geom;
   if (census) WG_.pair = 0;  // census walks are one lane per topic (their buffers count lanes)
@@ -2508,6 +2543,12 @@ int pass_check(emqxgm* h, PassCtx& c, uint32_t n, uint64_t bytes_len, int attemp
     h->spill_want = bound;
     int rc = ensure_scratch(h, c, n, words, s.p_cap);
     return rc ? rc : 1;
+  }
+  if (c.packed && s.ctl_host[CTL_PKOVF]) {
+    // a topic's rank outgrew the packed staging's field: stage this epoch's passes wide
+    rerun();
+    E.wide_stage.store(true, std::memory_order_relaxed);
+    return 1;
   }
   if (!legacy && s.ctl_host[CTL_LEGACY]) {
     rerun();
@@ -4881,6 +4922,11 @@ int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value) {
   if (strcmp(key, "hang_ms") == 0) {  // tests: host-pipe waits and publish passes stall first
     if (value < 0 || value > 600000) return -EINVAL;
     h->hang_ms.store((uint32_t)value);
+    return 0;
+  }
+  if (strcmp(key, "stage_rank_bits") == 0) {  // tests: cap the packed staging's rank field
+    if (value < 0 || value > 31) return -EINVAL;
+    h->stage_rank_bits.store((uint32_t)value);
     return 0;
   }
   if (strcmp(key, "probe_ms") == 0) {  // a repair's bounded wait for the device's streams

@@ -36,12 +36,26 @@ struct DevIndex {
   uint64_t test_mask = 0;           // != 0: collision-test tokens (every word hashed, masked)
   uint64_t full_mask = ~0ull;
   uint32_t max_depth = 0;           // deepest trie filter in levels
+  uint64_t fid_bound = 0;           // every filter id the walk can emit is below it (0: unknown)
   bool trie_empty = true;
   bool plain_empty = true;         // no committed non-wildcard route key
   bool wild_empty = true;          // no committed wildcard route key
   bool needs_verify = false;        // some trie filter has a hashed (long or test) token
   uint32_t leafp_mask = (1u << 26) | (1u << 29);  // CF_HMASK: depth-code pruning (0: off)
 };
+
+// Layout of the staged pairs of one pass.  Wide: {topic, filter, rank | REJ_BIT}, 12 B.  Packed
+// (pk, when the batch's topic ids, the index's filter ids and a rank field of at least
+// STG_MIN_RANK_BITS fit 64 bits): one 8-B word, topic << tsh | filter << fsh | rank << 1 | rejected
+// -- a third less for the walk to write and the scatter to read.  A topic with more pairs than
+// the rank field holds flags CTL_PKOVF and the pass is redone wide.
+struct StgFmt {
+  uint32_t pk = 0;
+  uint32_t tsh = 0, fsh = 0;  // shifts of the topic and filter fields
+  uint32_t fmask = 0;         // filter field mask
+  uint32_t rmask = 0;         // rank field mask (ranks <= rmask)
+};
+constexpr uint32_t STG_MIN_RANK_BITS = 10;
 
 // Per-batch scratch (device memory, owned by the engine, grown on demand).
 struct Scratch {
@@ -58,6 +72,8 @@ struct Scratch {
   uint2* xh = nullptr;        // [n]   exact probe over a huge table: {home bucket, h32} per name
   uint32_t p_cap = 0;   // pair staging capacity
   uint3* stg = nullptr;       // staged pairs {topic, filter, rank | REJ_BIT} (12 B), CH-slot chunks
+                              // (or 8-B packed words, fmt)
+  StgFmt fmt;                 // this pass's staging layout (set by the engine per pass)
   uint32_t* chk = nullptr;    // per staged chunk: pairs in it (written by the walk)
   uint32_t xseq = 1;          // this pass's sequence number (CTL_XHIT), set by the engine
   uint32_t o_cap = 0;
@@ -86,6 +102,7 @@ enum : int {
   CTL_NREJ = 5,       // rejected pairs appended to rlist
   CTL_LEGACY = 6,     // deferred scatter could not place rejects: re-run with the fix-up path
   CTL_ERR = 7,        // walk item stack outgrew its spill: re-run with a larger spill
+  CTL_PKOVF = 8,      // a topic's rank outgrew the packed staging's field: re-run wide
   CTL_FAN_R = 9,      // publish fan-out: aggre entries of the batch
   CTL_FAN_D = 10,     //   local deliveries of the batch
   CTL_CLAIM0 = 16,    // walk topic-claim counters, one per shard, CTL_CLAIM_STRIDE apart

@@ -214,6 +214,22 @@ __global__ __launch_bounds__(WG) void k_scan_final(const uint32_t* __restrict__ 
       ctl_dst[i] = i == CTL_TOTAL ? carry + tot : ctl_src[i];
 }
 
+// Staged pairs (StgFmt, gm_kernels.h): the packed word and back; rank carries REJ_BIT when the
+// pair was rejected, as the wide layout's z does.
+__device__ __forceinline__ uint64_t stg_pack(const StgFmt& F, uint32_t t, uint32_t f, uint32_t r) {
+  return ((uint64_t)t << F.tsh) | ((uint64_t)f << F.fsh) | ((uint64_t)(r & F.rmask) << 1) |
+         ((r & REJ_BIT) ? 1ull : 0ull);
+}
+__device__ __forceinline__ uint3 stg_unpack(const StgFmt& F, uint64_t w) {
+  return make_uint3((uint32_t)(w >> F.tsh), (uint32_t)(w >> F.fsh) & F.fmask,
+                    ((uint32_t)(w >> 1) & F.rmask) | ((w & 1ull) ? REJ_BIT : 0u));
+}
+template <bool PK>
+__device__ __forceinline__ uint3 stg_load(const uint3* stg, const StgFmt& F, uint64_t i) {
+  if constexpr (PK) return stg_unpack(F, ((const uint64_t*)stg)[i]);
+  else return stg[i];
+}
+
 #include "gm_tok.inc"
 #include "gm_walk.inc"
 #include "gm_verify.inc"
@@ -751,6 +767,7 @@ hipError_t launch_walk(const DevIndex& ix, Scratch& sc, uint32_t n, const WalkGe
   a.ctl = sc.ctl;
   a.cnt = sc.cnt;
   a.stg = sc.stg;
+  a.fmt = sc.fmt;
   a.chk = sc.chk;
   a.pcap = sc.p_cap;
   a.spill = sc.spill;
@@ -807,6 +824,7 @@ hipError_t launch_verify(const uint8_t* bytes, const uint32_t* off, const DevInd
   a.fver = ix.fver;
   a.fvbits = ix.fvbits;
   a.stg = sc.stg;
+  a.fmt = sc.fmt;
   a.chk = sc.chk;
   a.pcap = sc.p_cap;
   a.cnt = sc.cnt;
@@ -815,8 +833,11 @@ hipError_t launch_verify(const uint8_t* bytes, const uint32_t* off, const DevInd
   a.rcap = sc.r_cap;
   a.ctl = sc.ctl;
   // a wave per staging chunk, every block resident at once (k_verify: 4 blocks per CU by LDS)
-  hipLaunchKernelGGL(k_verify, dim3(std::min<uint32_t>((sc.p_cap / CH + 3) / 4, g.cus * 4)), dim3(WG),
-                     0, s, a);
+  const dim3 grid(std::min<uint32_t>((sc.p_cap / CH + 3) / 4, g.cus * 4));
+  if (sc.fmt.pk)
+    hipLaunchKernelGGL(k_verify<true>, grid, dim3(WG), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_verify<false>, grid, dim3(WG), 0, s, a);
   return hipGetLastError();
 }
 
@@ -828,6 +849,7 @@ hipError_t launch_scatter(Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_
   a.row_out = sc.row;
   a.ctl_host = mirror_ctl ? sc.ctl_host_dev : nullptr;
   a.stg = sc.stg;
+  a.fmt = sc.fmt;
   a.chk = sc.chk;
   a.pcap = sc.p_cap;
   a.row = sc.row;
@@ -842,10 +864,17 @@ hipError_t launch_scatter(Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_
     a.ctl_host = sc.ctl_host_dev;
     // (a small batch's chunks are few: 128 blocks stride over them; the full grid was
     // thousands of blocks with nothing to do)
-    hipLaunchKernelGGL(k_scatter<true>, dim3(std::min<uint32_t>(grid_for(sc.p_cap, g.cus * 8), 128u)),
-                       dim3(WG), 0, s, a);
+    const dim3 grid(std::min<uint32_t>(grid_for(sc.p_cap, g.cus * 8), 128u));
+    if (sc.fmt.pk)
+      hipLaunchKernelGGL((k_scatter<true, true>), grid, dim3(WG), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_scatter<true, false>), grid, dim3(WG), 0, s, a);
   } else {
-    hipLaunchKernelGGL(k_scatter<false>, dim3(grid_for(sc.p_cap, g.cus * 8)), dim3(WG), 0, s, a);
+    const dim3 grid(grid_for(sc.p_cap, g.cus * 8));
+    if (sc.fmt.pk)
+      hipLaunchKernelGGL((k_scatter<false, true>), grid, dim3(WG), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_scatter<false, false>), grid, dim3(WG), 0, s, a);
   }
   return hipGetLastError();
 }

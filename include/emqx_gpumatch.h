@@ -691,7 +691,9 @@ int emqxgm_set_profiling(emqxgm_t* h, int on);
  * flight; it also compacts the tables' deleted slots); "probe_ms": a repair's bounded wait for
  * the engine's streams (2000 default).  Fault injection (tests of "Health"): "fail_commits" (n):
  * the next n commits fail before they change anything, with errno "fail_errno" (EIO default);
- * "hang_ms": every host-pipe wait and publish pass stalls this long first (0 default). */
+ * "hang_ms": every host-pipe wait and publish pass stalls this long first (0 default).
+ * "stage_rank_bits": caps the rank field of the packed pair staging (tests of the wide redo a
+ * topic with more pairs than the field holds takes; 0 default = as wide as fits). */
 int emqxgm_tune(emqxgm_t* h, const char* key, int64_t value);
 int emqxgm_get_stats(emqxgm_t* h, emqxgm_stats* st);
 /* Last HIP error string seen by the handle (for diagnostics). */

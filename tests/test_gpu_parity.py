@@ -350,6 +350,52 @@ def test_many_matches_vs_oracle(emqx):
         assert sorted(res.row(i)) == list(ids[row[i]:row[i + 1]])
 
 
+def test_packed_staging_rank_overflow_redo(emqx):
+    """Pairs are staged packed (8-B words, StgFmt in gm_kernels.h) when the batch's topic ids,
+    the index's filter ids and a rank field fit; a topic with more pairs than the rank field
+    holds makes the walk flag the pass, which is redone wide, and the epoch stays wide.  The
+    rank field is capped at 3 bits here (tune "stage_rank_bits"): every topic with more than 8
+    matches overflows it."""
+    from emqx_amd.engine import pack
+    eng = emqx.Engine()
+    filters = [f"+/{i}/{w}".encode() for w in "#+z" for i in range(40)]
+    filters += [b"#", b"+/#", b"+/+/#", b"+/+/+", b"+/+/z", b"+/+"]
+    filters += [f"t{j}/+/#".encode() for j in range(0, 300, 2)] + [f"t{j}/+/+".encode() for j in range(0, 300, 3)]
+    filters += [f"t{j}/#".encode() for j in range(0, 300, 5)]
+    filters += [f"t{j}/{j % 40}/z".encode() for j in range(0, 300, 3)]  # (up to 11 per topic)
+    for f in filters:
+        eng.trie_insert(f)
+    eng.commit()
+    ref = RefIndex(True)
+    fb, fo = pack(filters)
+    ref.add_many(fb, fo, np.ones(len(filters), np.uint8))
+    topics = [f"t{j}/{j % 40}/z".encode() for j in range(300)] + [f"t{j}/{j % 9}".encode() for j in range(200)]
+    tb, to = pack(topics, np.uint32)
+    row, ids, _ = ref.match(tb, to, threads=8)
+    assert np.diff(row).max() > 8
+
+    def check(res):
+        assert np.array_equal(res.row_ptr, row)
+        for i in range(len(topics)):
+            assert sorted(res.row(i)) == list(ids[row[i]:row[i + 1]])
+
+    r0 = eng.stats()["reruns"]
+    check(eng.match(topics))  # packed, fits
+    assert eng.stats()["reruns"] == r0
+    eng.tune("stage_rank_bits", 3)
+    check(eng.match(topics))  # packed, overflows: redone wide
+    r1 = eng.stats()["reruns"]
+    assert r1 == r0 + 1
+    check(eng.match(topics))  # the epoch stays wide: no redo
+    assert eng.stats()["reruns"] == r1
+    eng.trie_insert(b"x/y")
+    eng.commit()  # a new epoch starts packed again
+    check(eng.match(topics))
+    assert eng.stats()["reruns"] == r1 + 1
+    eng.tune("stage_rank_bits", 0)
+    eng.close()
+
+
 def test_staging_overflow_rerun_and_deep_stack(emqx):
     """Filters {a,+}^k/# for k <= 10: a 12-level topic a/a/.../a matches all 2047 of them, the
     walk frontier doubles per level (stack deeper than the 8 LDS entries -> HBM spill) and
