@@ -2436,6 +2436,7 @@ int pass_enqueue(emqxgm* h, PassCtx& c, const Epoch& E, const uint8_t* d_bytes,
   // (census passes and the synchronous ones keep the full geometry)
   WalkGeom WG_ = (c.pipelined && !census) ? h->geom_pipe : h->geom;
   if (census) WG_.pair = 0;  // census walks are one lane per topic (their buffers count lanes)
+  if (!s.fmt.pk) WG_.pair = 0;  // the pair walk stages packed only (gm_walk.inc put)
   const uint32_t stat = ix.trie_empty ? 0u : walk_static_chunks(WG_, n, c.walk_level, s.p_cap);
   roctx_mark(h->roctx, "k_tok");
   // (per-topic reject counts: only the verification passes write -- and then read -- them;
