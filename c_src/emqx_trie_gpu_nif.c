@@ -442,7 +442,9 @@ static int fn_subscribers(void* a, emqxgm_t* h, uint64_t* epoch) {
 /* route_sync(Res, [{Filter, Present :: boolean()}]) -> {ok, Epoch} | {error, R}: the writing node's
  * hook after emqx_router:do_add_route/2, do_delete_route/2 (emqx_router.erl:124-138, 171-179) and
  * the mirror's batched table events: membership set AND committed before the return
- * (emqxgm_route_set_batch with EMQXGM_SET_COMMIT: never a wait for a background full build). */
+ * (emqxgm_route_set_batch with EMQXGM_SET_COMMIT).  It waits for a background full build only
+ * when the call's delta does not fit the current tables while that build runs: the dirty CPU
+ * scheduler is then held until the build's install (stats/1 bg_waits counts these). */
 static ERL_NIF_TERM nif_route_sync(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   gm_res* r;
   packed p;

@@ -2528,8 +2528,17 @@ int pass_check(emqxgm* h, PassCtx& c, uint32_t n, uint64_t bytes_len, int attemp
     // then deep + spill), kept for this committed index
     rerun();
     std::atomic<uint32_t>& lvl = c.census ? E.census_level : E.walk_level;
+    // the next variant; WALK_PAIRED is skipped when it would launch the kernel that just
+    // overflowed (a batch already walked in pairs) or pairs nothing (census and wide passes,
+    // pairs off): ADVICE r05, one wasted re-run per epoch otherwise
+    uint32_t next = c.walk_level + 1;
+    if (next == WALK_PAIRED) {
+      WalkGeom g = c.pipelined && !c.census ? h->geom_pipe : h->geom;
+      if (c.census || !c.packed) g.pair = 0;
+      if (!walk_pair(g, n, WALK_PAIRED) || walk_pair(g, n, c.walk_level)) next = WALK_DEEP;
+    }
     uint32_t cur = lvl.load();
-    while (cur <= c.walk_level && !lvl.compare_exchange_weak(cur, c.walk_level + 1)) {
+    while (cur < next && !lvl.compare_exchange_weak(cur, next)) {
     }
     return 1;
   }

@@ -115,6 +115,7 @@ hipError_t launch_exact(const uint8_t*, const uint32_t*, uint32_t, const DevInde
 hipError_t launch_exact_owned(const uint8_t*, const uint32_t*, uint32_t, const DevIndex&, uint32_t, uint32_t, uint32_t*, hipStream_t) { NOT_HERE; }
 hipError_t launch_walk(const DevIndex&, Scratch&, uint32_t, const WalkGeom&, hipStream_t, unsigned long long*, uint32_t, uint32_t) { NOT_HERE; }
 uint32_t walk_blocks(const WalkGeom&, uint32_t, uint32_t) { return 0; }
+bool walk_pair(const WalkGeom&, uint32_t, uint32_t) { return false; }
 uint32_t walk_static_chunks(const WalkGeom&, uint32_t, uint32_t, uint32_t) { return 0; }
 hipError_t launch_verify(const uint8_t*, const uint32_t*, const DevIndex&, Scratch&, uint32_t, const WalkGeom&, hipStream_t) { NOT_HERE; }
 hipError_t launch_scatter(Scratch&, uint32_t, const WalkGeom&, hipStream_t, bool, bool) { NOT_HERE; }
