@@ -371,9 +371,11 @@ def main():
     crossover = None
     if cpu and nif and cpu.get("one_thread") and "idle_T16_P1" in nif:
         one_us = cpu["one_thread"]["us_per_topic"]
-        idle = nif["idle_T16_P1"]
+        idle = nif.get("idle_T16_P1_eager") or nif["idle_T16_P1"]  # (the broker's default)
         crossover = {
             "device_idle_p50_us": idle["latency_us_p50"], "device_idle_p99_us": idle["latency_us_p99"],
+            "device_idle_point": "idle_T16_P1_eager" if "idle_T16_P1_eager" in nif else "idle_T16_P1",
+            "device_idle_p50_us_window_timer": nif["idle_T16_P1"]["latency_us_p50"],
             "reference_us_per_topic_one_core": one_us,
             "reference_capacity_topics_per_s": cpu["value"], "reference_cores": cpu["cores"],
             "reference_faster_at_idle": one_us < idle["latency_us_p50"],
@@ -618,9 +620,21 @@ def _nif_concurrent(eng, w, spec):
         if th0 and th1:  # the job's CPU quota stopping every thread (publishers + the layer's)
             out[key]["cgroup_throttled"] = {"periods": th1[0] - th0[0], "us": th1[1] - th0[1]}
     if runs:
-        # the idle point: one call in flight per thread, so ~1 / latency calls per second each
+        # the idle point: one call in flight per thread, so ~1 / latency calls per second each;
+        # with EMQXGM_ASYNC_EAGER (the broker's default since r06: a window goes out as soon as a
+        # pipe is free) and without it (window_us after a window's first call)
         r = publishers.run([eng], tb, to, 16, 1, 20000, 65536)
         out["idle_T16_P1"] = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}
+        r = publishers.run([eng], tb, to, 16, 1, 20000, 65536, eager=True)
+        out["idle_T16_P1_eager"] = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}
+        # a loaded point with it: windows still grow while every pipe is busy
+        T, W = 16, 16384
+        procs = max(1, -(-W * (eng.HOST_PIPES + 1) // T))
+        calls = max(2 * procs, min(int(out.get(f"T{T}_W{W}", {}).get("calls", 0)) // T, NIF_MAX_CALLS // T))
+        if calls > 2 * procs:
+            publishers.run([eng], tb, to, T, procs, 4 * procs, W, eager=True)  # warm-up
+            r = publishers.run([eng], tb, to, T, procs, calls, W, eager=True)
+            out[f"T{T}_W{W}_eager"] = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}
     out["includes"] = ("T threads x P processes, one emqxgm_async_match call per topic (the NIF's "
                        "match_async/3), windows filled lock-free and flushed when full or "
                        "window_us (50) after their first call, the window read from pinned memory "

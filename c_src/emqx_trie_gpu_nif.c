@@ -75,7 +75,7 @@ typedef struct {
 static ErlNifResourceType *RT, *CALL_RT, *RETAIN_RT;
 static ERL_NIF_TERM A_OK, A_ERROR, A_TRUE, A_FALSE, A_MOD, A_ROUTES, A_NONE, A_NODE, A_GROUP, A_SUB,
     A_SPIN_US, A_BG_BUILD, A_PUBLISH, A_UNDEFINED, A_REPORT_THREADS, A_EQ, A_WORDS, A_BINARY,
-    A_FAIL_THRESHOLD;
+    A_FAIL_THRESHOLD, A_EAGER;
 
 static int tab_init(term_tab* t, char* name) {
   t->lk = enif_rwlock_create(name);
@@ -239,10 +239,12 @@ static int opt_uint(ErlNifEnv* env, ERL_NIF_TERM map, ERL_NIF_TERM key, ErlNifSI
  *   answered -- terms built, enif_send -- by up to N threads, not by the completer alone),
  *   fail_threshold => N (emqxgm_async_cfg.fail_threshold, default 3: that many timed-out calls or
  *   failed windows in a row mark the engines stale, and every later call is refused with
- *   {error, estale} -- the caller's reference path -- until the mirror's repair)} */
+ *   {error, estale} -- the caller's reference path -- until the mirror's repair),
+ *   eager => boolean() (EMQXGM_ASYNC_EAGER: a window goes to the device as soon as a pipe is
+ *   free, not WindowUs after its first call: an idle broker answers in one pass)} */
 static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   unsigned ndev, wt, wb, wus, ml;
-  ERL_NIF_TERM list = argv[0], head, pub;
+  ERL_NIF_TERM list = argv[0], head, pub, eag;
   ErlNifSInt64 spin, bg, rth, fth;
   (void)argc;
   if (!enif_get_list_length(env, list, &ndev) || ndev == 0 || ndev > GM_MAX_DEVICES ||
@@ -253,6 +255,7 @@ static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
       !opt_uint(env, argv[5], A_FAIL_THRESHOLD, 3, &fth) || fth < 0 || fth > 1000000)
     return enif_make_badarg(env);
   const int publish = enif_get_map_value(env, argv[5], A_PUBLISH, &pub) && pub == A_TRUE;
+  const uint32_t eager = enif_get_map_value(env, argv[5], A_EAGER, &eag) && eag == A_TRUE ? EMQXGM_ASYNC_EAGER : 0u;
   gm_res* r = enif_alloc_resource(RT, sizeof(gm_res));
   memset(r, 0, sizeof *r);
   if (!tab_init(&r->nodes, "emqx_trie_gpu.nodes") || !tab_init(&r->groups, "emqx_trie_gpu.groups") ||
@@ -288,9 +291,10 @@ static ERL_NIF_TERM nif_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
   ac.max_levels = ml;
   ac.deliver_threads = (uint32_t)rth;
   ac.fail_threshold = (uint32_t)fth;
+  ac.flags = eager;
   if (!rc) rc = emqxgm_async_create(r->h, r->nh, &ac, on_window, r, &r->a);
   if (!rc && publish) {
-    ac.flags = EMQXGM_ASYNC_PUBLISH;
+    ac.flags = EMQXGM_ASYNC_PUBLISH | eager;
     rc = emqxgm_async_create(r->h, r->nh, &ac, on_window, r, &r->ap);
   }
   if (!rc) {
@@ -1218,6 +1222,7 @@ static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   A_BG_BUILD = enif_make_atom(env, "bg_build");
   A_REPORT_THREADS = enif_make_atom(env, "report_threads");
   A_FAIL_THRESHOLD = enif_make_atom(env, "fail_threshold");
+  A_EAGER = enif_make_atom(env, "eager");
   A_EQ = enif_make_atom(env, "eq");
   A_WORDS = enif_make_atom(env, "words");
   A_BINARY = enif_make_atom(env, "binary");

@@ -32,6 +32,9 @@ fail_threshold     3                  ``emqxgm_async_cfg.fail_threshold``: that 
                                       calls or failed windows in a row mark the engines stale
                                       (every later call refused at once until the mirror's
                                       repair; include/emqx_gpumatch.h "Health")
+eager_windows      true               ``EMQXGM_ASYNC_EAGER``: a window goes to the device as soon
+                                      as a pipe is free, not batch_window_us after its first call
+                                      (an idle broker answers in one pass; a loaded one batches)
 adaptive_below_rate 0                 publishes/s under which the reference path answers (its
                                       ~22 us on the publisher's core beats the device's window
                                       at idle); 0 = always the device (``LoadAdaptive``)
@@ -62,6 +65,7 @@ class GpuMatchConfig:
     snapshot_dir: Optional[str] = None
     timeout_ms: int = 500
     fail_threshold: int = 3
+    eager_windows: bool = True
     adaptive_below_rate: int = 0
     resync_interval_ms: Optional[int] = None  # None: by the node's mria role
 
@@ -100,6 +104,8 @@ class GpuMatchConfig:
         rng("spin_us", self.spin_us, 0, 1_000_000)
         if not isinstance(self.publish, bool):
             raise ValueError("broker.perf.gpu_match.publish: expected a boolean")
+        if not isinstance(self.eager_windows, bool):
+            raise ValueError("broker.perf.gpu_match.eager_windows: expected a boolean")
         if self.delta_commit not in DELTA_COMMIT:
             raise ValueError(f"broker.perf.gpu_match.delta_commit: one of {sorted(DELTA_COMMIT)}")
 
@@ -111,7 +117,8 @@ class GpuMatchConfig:
         """``emqxgm_async_cfg`` fields (emqx_amd.AsyncMatcher keywords)."""
         return {"window_topics": self.batch_max, "window_bytes": 64 * self.batch_max,
                 "window_us": self.batch_window_us, "max_levels": self.max_levels,
-                "deliver_threads": self.report_threads, "fail_threshold": self.fail_threshold}
+                "deliver_threads": self.report_threads, "fail_threshold": self.fail_threshold,
+                "eager": self.eager_windows}
 
     def batcher_kwargs(self) -> Dict[str, int]:
         """``emqxgm_batcher_cfg`` fields (emqx_amd.Batcher keywords: the single-driver batcher

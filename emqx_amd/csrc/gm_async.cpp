@@ -154,6 +154,7 @@ struct emqxgm_async {
   std::vector<std::vector<uint8_t>> rf_bytes;
   std::vector<std::vector<uint64_t>> rf_off;
   bool publish_mode() const { return (cfg.flags & EMQXGM_ASYNC_PUBLISH) != 0; }
+  bool eager() const { return (cfg.flags & EMQXGM_ASYNC_EAGER) != 0; }
   uint64_t st_windows = 0, st_cancelled = 0, st_errors = 0, st_delivered = 0;
   // health (cfg.fail_threshold > 0): consecutive failures -- pending calls cancelled by callers
   // that timed out, windows that failed -- until every handle is marked stale
@@ -429,7 +430,7 @@ struct emqxgm_async {
       const uint64_t fw = oi >= 0 ? slots[oi]->first_ns.load(std::memory_order_acquire) : 0;
       const uint64_t fc = oldest_staged();
       const uint64_t f = (fw && fc) ? std::min(fw, fc) : (fw | fc);
-      if (stop || (f != 0 && ready.empty() && pipe_free() && mono_ns() >= f + W)) {
+      if (stop || (f != 0 && ready.empty() && pipe_free() && (eager() || mono_ns() >= f + W))) {
         g.unlock();
         const bool drained = drain_all();
         g.lock();
@@ -506,7 +507,7 @@ struct emqxgm_async {
       if (f2 != 0) flusher_idle.store(0, std::memory_order_relaxed);
       // the next deadline: the timer seal (a pipe free) or the oldest staged call's drain
       uint64_t due = 0;
-      if (f2 != 0 && ready.empty() && pipe_free()) due = f2 + W;
+      if (f2 != 0 && ready.empty() && pipe_free()) due = eager() ? 1 : f2 + W;  // (1: now)
       if (fc2 != 0 && !drain_blocked && (due == 0 || fc2 + W < due)) due = fc2 + W;
       if (due != 0) {
         const uint64_t t = mono_ns();
@@ -626,7 +627,7 @@ int emqxgm_async_create(emqxgm_t* const* hs, uint32_t n_handles, const emqxgm_as
   if (!a->cfg.window_us) a->cfg.window_us = 50;
   if (!a->cfg.queued_windows) a->cfg.queued_windows = 2;
   if (a->cfg.window_topics >= SEAL || a->cfg.window_bytes >= SEAL ||
-      (a->cfg.flags & ~EMQXGM_ASYNC_PUBLISH) || a->cfg.deliver_threads > 64) {
+      (a->cfg.flags & ~(EMQXGM_ASYNC_PUBLISH | EMQXGM_ASYNC_EAGER)) || a->cfg.deliver_threads > 64) {
     delete a;
     return -EINVAL;
   }

@@ -87,6 +87,7 @@ STALE_RESYNC = 2  # EMQXGM_STALE_RESYNC
 
 
 ASYNC_PUBLISH = 1  # EMQXGM_ASYNC_PUBLISH
+ASYNC_EAGER = 2    # EMQXGM_ASYNC_EAGER
 
 
 class _AsyncWindow(C.Structure):
@@ -875,7 +876,7 @@ class AsyncMatcher:
     def __init__(self, engines: Sequence[Engine], callback=None, window_topics: int = 0,
                  window_bytes: int = 0, window_us: int = 0, max_levels: int = 0,
                  queued_windows: int = 0, publish: bool = False, deliver_threads: int = 0,
-                 fail_threshold: int = 0):
+                 fail_threshold: int = 0, eager: bool = False):
         import threading
         self._engines = list(engines)  # kept alive: the layer uses their handles
         self._lib = self._engines[0]._lib
@@ -920,7 +921,8 @@ class AsyncMatcher:
                     self._cv.notify_all()
         self._cb = ASYNC_CB(on_window)  # kept alive as long as the layer
         cfg = _AsyncCfg(window_topics, window_bytes, window_us, max_levels, queued_windows,
-                        ASYNC_PUBLISH if publish else 0, deliver_threads, fail_threshold)
+                        (ASYNC_PUBLISH if publish else 0) | (ASYNC_EAGER if eager else 0),
+                        deliver_threads, fail_threshold)
         arr = (C.c_void_p * len(self._engines))(*[e._h for e in self._engines])
         a = C.c_void_p()
         self._engines[0]._check(self._lib.emqxgm_async_create(arr, len(self._engines), C.byref(cfg),

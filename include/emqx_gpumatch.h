@@ -531,6 +531,10 @@ typedef struct emqxgm_async_cfg {
                               the index is repaired.  A window answered resets the count. */
 } emqxgm_async_cfg;
 #define EMQXGM_ASYNC_PUBLISH 1u
+/* flags: a window is sealed and submitted as soon as a pipe is free and no sealed window waits,
+ * instead of window_us after its first call.  An idle layer then answers a call in one pass; a
+ * loaded one still grows its windows while every pipe is busy (the pipes' pace sets their size). */
+#define EMQXGM_ASYNC_EAGER 2u
 typedef struct emqxgm_async_window {
   int status;               /* 0, or the negative errno the window's pass failed with (no result) */
   uint32_t n;               /* calls in the window, in the order they were made */

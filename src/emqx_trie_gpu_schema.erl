@@ -29,6 +29,9 @@
 %%   fail_threshold      -> emqxgm_async_cfg.fail_threshold: that many timed-out calls or failed
 %%                          windows in a row mark the engines stale, so every later call is refused
 %%                          at once until the mirror's repair (include/emqx_gpumatch.h "Health")
+%%   eager_windows       -> emqxgm_async_cfg.flags EMQXGM_ASYNC_EAGER: a window is submitted as
+%%                          soon as a pipe is free instead of batch_window_us after its first call
+%%                          (an idle broker answers in one pass; a loaded one still batches)
 %%   adaptive_below_rate -> publishes per second under which the reference path answers (its
 %%                          ~22 us on the publisher's core beats the device's window at idle);
 %%                          0 = always the device (emqx_trie_gpu "Load-adaptive choice")
@@ -60,6 +63,7 @@ fields("gpu_match") ->
         {"snapshot_dir", hoconsc:mk(string(), #{required => false})},
         {"timeout_ms", hoconsc:mk(range(1, 600000), #{default => 500})},
         {"fail_threshold", hoconsc:mk(range(0, 1000000), #{default => 3})},
+        {"eager_windows", hoconsc:mk(boolean(), #{default => true})},
         {"adaptive_below_rate", hoconsc:mk(non_neg_integer(), #{default => 0})},
         {"resync_interval_ms", hoconsc:mk(range(0, 86400000), #{required => false})}
     ].

@@ -156,6 +156,7 @@ open(Index) ->
                 bg_build => ?CONF(bg_build, 16384),
                 report_threads => ?CONF(report_threads, 8),
                 fail_threshold => ?CONF(fail_threshold, 3),
+                eager => ?CONF(eager_windows, true),
                 publish => Index =:= route andalso ?CONF(publish, true)
             },
             case

@@ -456,6 +456,7 @@ int main(int argc, char** argv) {
   cfg.window_us = 20 + seed % 100;
   cfg.max_levels = 4;
   cfg.deliver_threads = 1 + seed % 4;  // windows reported in parts by a pool (GM_DELIVER_MIN=4)
+  cfg.flags = seed % 2 == 0 ? EMQXGM_ASYNC_EAGER : 0u;  // even seeds: windows out as pipes free
   emqxgm_async_t* a = nullptr;
   CHECK(emqxgm_async_create(hs.data(), handles, &cfg, on_window, nullptr, &a) == 0, "create");
   std::atomic<uint64_t> accepted{0}, cancelled{0}, busy{0}, too_deep{0};

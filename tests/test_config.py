@@ -11,7 +11,7 @@ def test_defaults_map_onto_the_engine():
     assert c.engine_kwargs() == [{"device": 0, "batch_max": 65536}]
     assert c.async_kwargs() == {"window_topics": 65536, "window_bytes": 64 * 65536,
                                 "window_us": 50, "max_levels": 128, "deliver_threads": 8,
-                                "fail_threshold": 3}
+                                "fail_threshold": 3, "eager": True}
     assert c.timeout_ms == 500 and c.resync_ms("core") == 0 and c.resync_ms("replicant") == 30000
     assert c.tunes() == {"delta_commit": 1, "bg_build": 16384, "spin_us": 0} and c.publish
 
@@ -26,7 +26,7 @@ def test_values_and_ranges():
                 {"delta_commit": "sometimes"}, {"batch_size": 3}, {"batch_max": True},
                 {"timeout_ms": 0}, {"resync_interval_ms": -1}, {"spin_us": -1},
                 {"publish": 1}, {"bg_build": -5}, {"report_threads": 65},
-                {"fail_threshold": -1}, {"adaptive_below_rate": -1}):
+                {"fail_threshold": -1}, {"adaptive_below_rate": -1}, {"eager_windows": 1}):
         with pytest.raises(ValueError):
             GpuMatchConfig.from_map(bad)
 

@@ -230,19 +230,44 @@ def _check_load(r, want):
     assert bad.size == 0, (bad[:10], t[bad[:10]])
 
 
-@pytest.mark.parametrize("threads,window,deliver", [(16, 4096, 0), (64, 16384, 0), (16, 16384, 8)])
-def test_async_load_cfg1_every_call(emqx, threads, window, deliver):
+@pytest.mark.parametrize("threads,window,deliver,eager", [(16, 4096, 0, False), (64, 16384, 0, False),
+                                                          (16, 16384, 8, False), (16, 4096, 0, True),
+                                                          (64, 16384, 8, True)])
+def test_async_load_cfg1_every_call(emqx, threads, window, deliver, eager):
     """deliver: the layer's report pool (emqxgm_async_cfg.deliver_threads): a window's calls
-    reported in parts by several threads, each part's view offset into the window's result."""
+    reported in parts by several threads, each part's view offset into the window's result.
+    eager: EMQXGM_ASYNC_EAGER, windows sealed as soon as a pipe is free."""
     from workloads import publishers
     w, (eng,) = _cfg1(emqx, nt=100_000)
     want = _oracle_rows(w)
     procs = max(1, window * 4 // threads)
     r = publishers.run([eng], w.tbytes, w.toff.astype(np.uint64), threads, procs,
                        max(2 * procs, 300_000 // threads), window, record=True,
-                       deliver_threads=deliver, report_ns=200 if deliver else 0)
+                       deliver_threads=deliver, report_ns=200 if deliver else 0, eager=eager)
     _check_load(r, want)
     assert r["windows"] > 0 and r["calls_per_window"] > 1
+
+
+def test_async_eager_idle_call_takes_one_pass(emqx):
+    """An idle layer with EMQXGM_ASYNC_EAGER submits a lone call's window at once: its answer
+    comes back well inside the window_us timer the default layer waits for (here 20 ms), and
+    equals the oracle's."""
+    import time
+    w, (eng,) = _cfg1(emqx, nt=2_000)
+    ref = RefIndex(True)
+    ref.add_many(w.fbytes, w.foff, 2 + w.fwild.astype(np.uint8))
+    row, ids, _ = ref.match(w.tbytes, w.toff, threads=8)
+    am = emqx.AsyncMatcher([eng], window_topics=4096, window_us=20_000, eager=True)
+    for i in range(50):
+        t0 = time.perf_counter()
+        assert am.match(w.topic(i), i) == 0
+        assert am.wait([(i, 0)], timeout=10)
+        dt = time.perf_counter() - t0
+        r = am.results.pop((i, 0))
+        assert r.status == 0, r.status
+        assert sorted(r.filters) == sorted(w.filter(int(j)) for j in ids[row[i]:row[i + 1]]), i
+        assert dt < 0.01, dt
+    am.close()
 
 
 def test_async_load_two_replicas(emqx):

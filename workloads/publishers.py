@@ -43,19 +43,21 @@ def _p(a):
 
 def run(engines, tbytes, toff, threads: int, procs: int, calls_per_thread: int,
         window_topics: int, window_us: int = 50, max_levels: int = 0, record: bool = False,
-        deliver_threads: int = 0, report_ns: int = 0):
+        deliver_threads: int = 0, report_ns: int = 0, eager: bool = False):
     """One load run over the engines (one AsyncMatcher-equivalent layer inside the harness).
     Returns a dict of stats, plus 'topic', 'count', 'hash', 'exact' arrays when record.
     deliver_threads: the layer's report pool (emqxgm_async_cfg); report_ns: a busy wait per
-    reported call standing for the NIF's per-call work (terms, enif_send)."""
-    from emqx_amd.engine import _AsyncCfg
+    reported call standing for the NIF's per-call work (terms, enif_send); eager: windows sealed as
+    soon as a pipe is free (EMQXGM_ASYNC_EAGER)."""
+    from emqx_amd.engine import _AsyncCfg, ASYNC_EAGER
     lib = _load()
     tbytes = np.ascontiguousarray(tbytes, np.uint8)
     toff = np.ascontiguousarray(toff, np.uint64)
     n_topics = len(toff) - 1
     total = threads * calls_per_thread
     arr = (C.c_void_p * len(engines))(*[e._h for e in engines])
-    cfg = _AsyncCfg(window_topics, 64 * window_topics, window_us, max_levels, 0, 0, deliver_threads)
+    cfg = _AsyncCfg(window_topics, 64 * window_topics, window_us, max_levels, 0,
+                    ASYNC_EAGER if eager else 0, deliver_threads)
     topic = count = hsh = exact = None
     if record:
         topic = np.zeros(total, np.uint32)
