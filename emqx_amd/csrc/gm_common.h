@@ -183,9 +183,18 @@ constexpr uint32_t VINL = 60;
 // Per-topic record written by the tokenizer, 64 B = REC_U4 x uint4:
 //   {wbase, n_words | flags << 24, tok0.lo, tok0.hi} {tok1, tok2} {tok3, tok4} {tok5, tok6}
 // (tokens past the last level are 0); level tokens from REC_TOKS on are read from the token
-// array at wbase.  Topics have at most 32,768 levels (65,535 bytes).
+// array at wbase.  Topics have at most 32,768 levels (65,535 bytes).  Stored in blocks of
+// REC_BLOCK topics, part-major within a block (r06): part c of topic t at uint4 index
+// (t / 64) * 256 + c * 64 + t % 64, so a wave's lanes, holding consecutive topics, read and write
+// whole lines per 16-B access, and one address with immediate offsets of 1 KB reaches every part.
+// A scratch of n topics holds ceil(n / 64) whole blocks.
 constexpr uint32_t REC_U4 = 4;
+constexpr uint32_t REC_BLOCK = 64;
 constexpr uint32_t REC_TOKS = 7;
+template <class T>
+GM_HD T* rec_at(T* rec, uint32_t t) {
+  return rec + (uint64_t)(t / REC_BLOCK) * (REC_BLOCK * REC_U4) + (t % REC_BLOCK);
+}
 constexpr uint32_t T_WILD = 1u;    // some level is exactly '+' or '#'  -> trie result []
 constexpr uint32_t T_DOLLAR = 2u;  // first byte is '$' -> no root '+'/'#' (emqx_trie.erl:282)
 

@@ -2315,7 +2315,7 @@ int ensure_scratch(emqxgm* h, PassCtx& c, uint32_t n, uint64_t words, uint32_t p
   const uint32_t stw = scan_tmp_words(ncap);
   if ((rc = dev_alloc(h, c, (void**)&s.nw, (size_t)ncap * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.wh, (size_t)wcap * 8)) ||
-      (rc = dev_alloc(h, c, (void**)&s.rec, (size_t)ncap * 16 * REC_U4)) ||
+      (rc = dev_alloc(h, c, (void**)&s.rec, (size_t)(ncap + REC_BLOCK - 1) / REC_BLOCK * REC_BLOCK * 16 * REC_U4)) ||
       (rc = dev_alloc(h, c, (void**)&s.cnt, (size_t)ncap * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.row, (size_t)(ncap + 1) * 4)) ||
       (rc = dev_alloc(h, c, (void**)&s.row2, (size_t)(ncap + 1) * 4)) ||
