@@ -371,11 +371,13 @@ def main():
     crossover = None
     if cpu and nif and cpu.get("one_thread") and "idle_T16_P1" in nif:
         one_us = cpu["one_thread"]["us_per_topic"]
-        idle = nif.get("idle_T16_P1_eager") or nif["idle_T16_P1"]  # (the broker's default)
+        # one publisher on an idle broker, eager windows (the broker's default)
+        ipt = next(k for k in ("idle_T1_P1_eager", "idle_T16_P1_eager", "idle_T16_P1") if k in nif)
+        idle = nif[ipt]
         crossover = {
             "device_idle_p50_us": idle["latency_us_p50"], "device_idle_p99_us": idle["latency_us_p99"],
-            "device_idle_point": "idle_T16_P1_eager" if "idle_T16_P1_eager" in nif else "idle_T16_P1",
-            "device_idle_p50_us_window_timer": nif["idle_T16_P1"]["latency_us_p50"],
+            "device_idle_point": ipt,
+            "device_idle_p50_us_window_timer": nif.get("idle_T1_P1", nif["idle_T16_P1"])["latency_us_p50"],
             "reference_us_per_topic_one_core": one_us,
             "reference_capacity_topics_per_s": cpu["value"], "reference_cores": cpu["cores"],
             "reference_faster_at_idle": one_us < idle["latency_us_p50"],
@@ -627,6 +629,12 @@ def _nif_concurrent(eng, w, spec):
         out["idle_T16_P1"] = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}
         r = publishers.run([eng], tb, to, 16, 1, 20000, 65536, eager=True)
         out["idle_T16_P1_eager"] = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}
+        # a truly idle broker: one publisher, one call at a time (16 such callers are a light load,
+        # where eager windows trade the timer's batching for more, smaller passes)
+        for eager in (False, True):
+            r = publishers.run([eng], tb, to, 1, 1, 5000, 65536, eager=eager)
+            out["idle_T1_P1" + ("_eager" if eager else "")] = {
+                k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}
         # a loaded point with it: windows still grow while every pipe is busy
         T, W = 16, 16384
         procs = max(1, -(-W * (eng.HOST_PIPES + 1) // T))
