@@ -1,6 +1,7 @@
 """Which cfg1 topics set the walk's floor (MEASUREMENTS r06 "what bounds cfg1's walk").
 
-Walks batches of 6,250 cfg1 topics chosen by their number of trie matches (the oracle's rows):
+Walks batches of 6,250 cfg1 topics chosen by their number of trie matches (the engine's own rows
+for the whole 100k batch; parity is the tests' business):
 the lightest, a random sample, and the heaviest.  If the ~29 us floor of a small batch comes
 from its heaviest topics' chains, the light batch walks much faster; if it is a per-launch or
 per-iteration cost, all three take about as long.  Prints one JSON line of walk times (HIP
@@ -25,22 +26,19 @@ def main():
     import torch
     import workloads
     from emqx_amd import Engine
-    from oracle.cref import RefIndex
 
     w = workloads.generate(1, None, 100_000)
-    ref = RefIndex(True)
-    ref.add_many(w.fbytes, w.foff, 2 + w.fwild.astype(np.uint8))
-    row, _, _ = ref.match(w.tbytes, w.toff, threads=16)
-    cnt = np.diff(row.astype(np.int64))
-    order = np.argsort(cnt, kind="stable")
-    rng = np.random.default_rng(1)
-    picks = {"lightest": order[:a.n], "random": rng.choice(len(cnt), a.n, replace=False),
-             "heaviest": order[-a.n:]}
     eng = Engine()
     eng.route_ref_many(w.fbytes, w.foff)
     for i in np.nonzero(w.fwild)[0]:
         eng.trie_insert(w.filter(int(i)))
     eng.commit()
+    res = eng.match_packed(w.tbytes, w.toff.astype(np.uint32))
+    cnt = np.diff(np.asarray(res.row_ptr, dtype=np.int64))
+    order = np.argsort(cnt, kind="stable")
+    rng = np.random.default_rng(1)
+    picks = {"lightest": order[:a.n], "random": rng.choice(len(cnt), a.n, replace=False),
+             "heaviest": order[-a.n:]}
     dev = torch.device("cuda", 0)
     out = {"topics": a.n}
     for name, idx in picks.items():
