@@ -871,10 +871,19 @@ hipError_t launch_scatter(Scratch& sc, uint32_t n, const WalkGeom& g, hipStream_
       hipLaunchKernelGGL((k_scatter<true, false>), grid, dim3(WG), 0, s, a);
   } else {
     const dim3 grid(grid_for(sc.p_cap, g.cus * 8));
-    if (sc.fmt.pk)
-      hipLaunchKernelGGL((k_scatter<false, true>), grid, dim3(WG), 0, s, a);
-    else
-      hipLaunchKernelGGL((k_scatter<false, false>), grid, dim3(WG), 0, s, a);
+    // (EMQXGM_SCATTER_DIRECT: the ungrouped stores, for A/B runs)
+    static const bool direct = getenv("EMQXGM_SCATTER_DIRECT") != nullptr;
+    if (direct) {
+      if (sc.fmt.pk)
+        hipLaunchKernelGGL((k_scatter<false, true>), grid, dim3(WG), 0, s, a);
+      else
+        hipLaunchKernelGGL((k_scatter<false, false>), grid, dim3(WG), 0, s, a);
+    } else {
+      if (sc.fmt.pk)
+        hipLaunchKernelGGL(k_scatter_grp<true>, grid, dim3(WG), 0, s, a);
+      else
+        hipLaunchKernelGGL(k_scatter_grp<false>, grid, dim3(WG), 0, s, a);
+    }
   }
   return hipGetLastError();
 }
